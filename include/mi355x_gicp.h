@@ -1,0 +1,128 @@
+/*
+ * mi355x_gicp.h -- C-ABI of the MI355X-native GICP fine-alignment engine (libmgicp.so).
+ *
+ * This is the drop-in boundary for the reference's hot path
+ *     GICPAlignment::fineAlignment()  ->  gicp_.align(*aligned_cloud)
+ *     (/root/reference/src/GICPAlignment.cpp:86-109, the align call at :96, and the
+ *      second align in iterateFineAlignment at :116)
+ * i.e. it replaces pcl::GeneralizedIterativeClosestPoint<PointXYZRGB,PointXYZRGB>
+ * (/root/reference/include/GICPAlignment.h:153) under the unchanged GICPAlignment class.
+ * Plain pointers and sizes only; no PCL, Eigen, HIP or torch types cross this header.
+ *
+ * Matrices are 4x4 float, COLUMN-MAJOR (Eigen::Matrix4f storage order).
+ * Point clouds are passed as xyz at byte offsets 0/4/8 of records of `stride_bytes`
+ * (32 for pcl::PointXYZRGB, 16 for pcl::PointXYZ, 12 for packed xyz).
+ *
+ * Threading: one context per host thread; every call blocks until its result is on the
+ * host.  Status codes: 0 = OK, negative = error (mgicp_last_error() has the message).
+ */
+#ifndef MI355X_GICP_H
+#define MI355X_GICP_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MGICP_OK                0
+#define MGICP_E_INVALID        -1  /* bad argument / state */
+#define MGICP_E_TOO_FEW_POINTS -2  /* a cloud has fewer than k points (PCL logs and leaves
+                                      its covariances empty, gicp.hpp computeCovariances) */
+#define MGICP_E_SOLVER         -3  /* < 4 correspondences or BFGS failure: PCL's
+                                      estimateRigidTransformationBFGS throws; align() returns
+                                      this with converged = 0 and T = last good transform */
+#define MGICP_E_NONFINITE      -4  /* NaN/Inf coordinates in an input cloud */
+#define MGICP_E_HIP            -5  /* HIP runtime error */
+#define MGICP_E_COMM           -6  /* RCCL error */
+#define MGICP_E_NOMEM          -7  /* device allocation failed / grid too large */
+
+#define MGICP_SOLVER_PCL_BFGS   0  /* PCL 1.8.1 BFGS trajectory (parity mode, default) */
+
+typedef struct {
+    int    max_iter;        /* Registration::setMaximumIterations  (GICPAlignment.cpp:50; default 100) */
+    double tf_eps;          /* setTransformationEpsilon             (GICPAlignment.cpp:52; default 4e-3) */
+    double rot_eps;         /* GICP rotation_epsilon_                (PCL default 2e-3) */
+    double max_corr_dist;   /* setMaxCorrespondenceDistance          (GICPAlignment.cpp:51; default 0.04) */
+    double gicp_eps;        /* GICP gicp_epsilon_                    (PCL default 1e-3) */
+    int    k;               /* GICP k_correspondences_               (PCL default 20; max 32) */
+    int    max_inner_iter;  /* GICP max_inner_iterations_            (PCL default 20) */
+    int    solver;          /* MGICP_SOLVER_* */
+    int    device;          /* HIP device ordinal; -1 = current device */
+    int    fixed_iterations;/* 1 = ignore the delta test and run exactly max_iter iterations
+                               (matched-iteration parity protocol) */
+} mgicp_params;
+
+typedef struct {
+    int    converged;       /* Registration::hasConverged() */
+    int    iterations;      /* GICP nr_iterations_ */
+    int    n_corr;          /* correspondences in the last outer iteration (all ranks) */
+    int    n_evals;         /* BFGS objective passes over the correspondences */
+    double ms_total;        /* host call -> transform on host */
+    double ms_upload;       /* host -> HBM copies of dirty clouds */
+    double ms_prep;         /* grid build + kNN covariances (one-time per set_*) */
+    double ms_loop;         /* outer GICP loop (correspondences + BFGS) */
+} mgicp_result;
+
+typedef struct mgicp_ctx mgicp_ctx;
+
+/* ---- lifecycle ---- */
+void        mgicp_default_params(mgicp_params* p);
+int         mgicp_create(mgicp_ctx** ctx, const mgicp_params* p);
+int         mgicp_set_params(mgicp_ctx* ctx, const mgicp_params* p);
+const char* mgicp_last_error(const mgicp_ctx* ctx);
+void        mgicp_destroy(mgicp_ctx* ctx);
+int         mgicp_device_count(int* n);
+
+/* ---- inputs (Registration::setInputTarget / setInputSource) ----
+ * Host buffers are copied at call time; the cloud is marked dirty so the next align()
+ * rebuilds its grid and covariances (PCL resets its trees/covariances the same way).
+ * The *_device variants take a device pointer already resident in HBM on this context's
+ * device (no H2D copy). */
+int mgicp_set_target(mgicp_ctx* ctx, const float* xyz, size_t n, size_t stride_bytes);
+int mgicp_set_source(mgicp_ctx* ctx, const float* xyz, size_t n, size_t stride_bytes);
+int mgicp_set_target_device(mgicp_ctx* ctx, const float* d_xyz, size_t n, size_t stride_bytes);
+int mgicp_set_source_device(mgicp_ctx* ctx, const float* d_xyz, size_t n, size_t stride_bytes);
+
+/* ---- the hot path: Registration::align(output, guess) ----
+ * guess may be NULL (identity, as GICPAlignment calls align()).  out_T receives
+ * getFinalTransformation().  Returns MGICP_E_SOLVER when PCL would report !hasConverged()
+ * because the solver threw. */
+int mgicp_align(mgicp_ctx* ctx, const float guess_cm[16], float out_T_cm[16], mgicp_result* res);
+
+/* Registration::getFitnessScore(max_range) for transform T over the source cloud
+ * (GICPAlignment.cpp:103,123).  max_range <= 0 means DBL_MAX (PCL default). */
+int mgicp_fitness(mgicp_ctx* ctx, const float T_cm[16], double max_range, double* out);
+
+/* pcl::transformPointCloud(source, out, T) for the xyz fields (GICPAlignment.cpp:144-147):
+ * writes n transformed xyz triples into out (record stride out_stride_bytes), leaving the
+ * other bytes of each record untouched. */
+int mgicp_transform_source(mgicp_ctx* ctx, const float T_cm[16], float* out, size_t out_stride_bytes);
+
+/* ---- multi-GPU: one process per GPU, point-range shards of the source cloud ----
+ * Rank 0 calls mgicp_get_unique_id and broadcasts the 128 bytes out of band (bench.py uses
+ * torch.distributed); every rank then calls mgicp_comm_init before set_* / align. */
+int mgicp_get_unique_id(unsigned char id[128]);
+int mgicp_comm_init(mgicp_ctx* ctx, int nranks, int rank, const unsigned char id[128]);
+
+/* ---- introspection for parity tests (original point order) ---- */
+/* covariances of the source (which = 0) or target (which = 1): n x {c00,c01,c02,c11,c12,c22} */
+int mgicp_debug_covariances(mgicp_ctx* ctx, int which, double* out_c6);
+/* one correspondence sweep at T (col-major); out_tgt[i] = target index or -1;
+ * out_M6 (optional) = n x {m00,m01,m02,m11,m12,m22}; returns the count or < 0 */
+int mgicp_debug_correspondences(mgicp_ctx* ctx, const float T_cm[16], int* out_tgt, double* out_M6);
+/* OptimizationFunctorWithIndices::fdf at x over the last correspondence sweep */
+int mgicp_debug_fdf(mgicp_ctx* ctx, const double x[6], double* f, double g6[6]);
+/* per-iteration transformation_ of the last align (col-major, iterations x 16) */
+int mgicp_debug_trace(mgicp_ctx* ctx, float* out, int max_iters);
+/* average device time (ms) of each kernel family during the last align, for roofline
+ * reporting: [0] covariance kNN, [1] correspondence, [2] BFGS objective pass,
+ * [3] reduction finish; counts in out_counts (optional) */
+int mgicp_debug_kernel_times(mgicp_ctx* ctx, double out_ms[4], int out_counts[4]);
+/* enable (1) / disable (0) per-launch HIP event timing (off by default) */
+int mgicp_set_profiling(mgicp_ctx* ctx, int on);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

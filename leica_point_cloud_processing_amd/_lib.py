@@ -1,0 +1,121 @@
+"""ctypes binding of libmgicp.so (include/mi355x_gicp.h).
+
+The HIP engine is the only compute path of this package: if the in-tree library is missing
+or cannot be loaded, every entry point raises immediately -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmgicp.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "mi355x_gicp.h")
+
+MGICP_OK = 0
+MGICP_E_INVALID = -1
+MGICP_E_TOO_FEW_POINTS = -2
+MGICP_E_SOLVER = -3
+MGICP_E_NONFINITE = -4
+MGICP_E_HIP = -5
+MGICP_E_COMM = -6
+MGICP_E_NOMEM = -7
+
+
+class MgicpParams(ctypes.Structure):
+    _fields_ = [
+        ("max_iter", ctypes.c_int),
+        ("tf_eps", ctypes.c_double),
+        ("rot_eps", ctypes.c_double),
+        ("max_corr_dist", ctypes.c_double),
+        ("gicp_eps", ctypes.c_double),
+        ("k", ctypes.c_int),
+        ("max_inner_iter", ctypes.c_int),
+        ("solver", ctypes.c_int),
+        ("device", ctypes.c_int),
+        ("fixed_iterations", ctypes.c_int),
+    ]
+
+
+class MgicpResult(ctypes.Structure):
+    _fields_ = [
+        ("converged", ctypes.c_int),
+        ("iterations", ctypes.c_int),
+        ("n_corr", ctypes.c_int),
+        ("n_evals", ctypes.c_int),
+        ("ms_total", ctypes.c_double),
+        ("ms_upload", ctypes.c_double),
+        ("ms_prep", ctypes.c_double),
+        ("ms_loop", ctypes.c_double),
+    ]
+
+
+class MgicpError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"mgicp error {code}: {msg}")
+        self.code = code
+
+
+_P = ctypes.c_void_p
+_FP = ctypes.POINTER(ctypes.c_float)
+_DP = ctypes.POINTER(ctypes.c_double)
+_IP = ctypes.POINTER(ctypes.c_int)
+_SZ = ctypes.c_size_t
+
+_SIGNATURES = {
+    "mgicp_default_params": (None, [ctypes.POINTER(MgicpParams)]),
+    "mgicp_create": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.POINTER(MgicpParams)]),
+    "mgicp_set_params": (ctypes.c_int, [_P, ctypes.POINTER(MgicpParams)]),
+    "mgicp_last_error": (ctypes.c_char_p, [_P]),
+    "mgicp_destroy": (None, [_P]),
+    "mgicp_device_count": (ctypes.c_int, [_IP]),
+    "mgicp_set_target": (ctypes.c_int, [_P, _P, _SZ, _SZ]),
+    "mgicp_set_source": (ctypes.c_int, [_P, _P, _SZ, _SZ]),
+    "mgicp_set_target_device": (ctypes.c_int, [_P, _P, _SZ, _SZ]),
+    "mgicp_set_source_device": (ctypes.c_int, [_P, _P, _SZ, _SZ]),
+    "mgicp_align": (ctypes.c_int, [_P, _FP, _FP, ctypes.POINTER(MgicpResult)]),
+    "mgicp_fitness": (ctypes.c_int, [_P, _FP, ctypes.c_double, _DP]),
+    "mgicp_transform_source": (ctypes.c_int, [_P, _FP, _P, _SZ]),
+    "mgicp_get_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
+    "mgicp_comm_init": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]),
+    "mgicp_debug_covariances": (ctypes.c_int, [_P, ctypes.c_int, _DP]),
+    "mgicp_debug_correspondences": (ctypes.c_int, [_P, _FP, _IP, _DP]),
+    "mgicp_debug_fdf": (ctypes.c_int, [_P, _DP, _DP, _DP]),
+    "mgicp_debug_trace": (ctypes.c_int, [_P, _FP, ctypes.c_int]),
+    "mgicp_debug_kernel_times": (ctypes.c_int, [_P, _DP, _IP]),
+    "mgicp_set_profiling": (ctypes.c_int, [_P, ctypes.c_int]),
+}
+
+_lib = None
+
+
+def header_symbols(path: str = HEADER_PATH) -> list[str]:
+    """Every function declared in include/mi355x_gicp.h."""
+    with open(path) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"\b(mgicp_[a-z_0-9]+)\s*\(", text)))
+
+
+def load() -> ctypes.CDLL:
+    """Load the in-tree libmgicp.so; raise loudly when it is absent (no fallback path)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} not found: build the HIP engine first (python -c 'import __graft_entry__ as g; g.build()' "
+            "or `make`). There is no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in _SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def default_params() -> MgicpParams:
+    p = MgicpParams()
+    load().mgicp_default_params(ctypes.byref(p))
+    return p

@@ -1,0 +1,1035 @@
+// mgicp_engine.hip -- host engine behind include/mi355x_gicp.h (libmgicp.so).
+//
+// Replaces pcl::GeneralizedIterativeClosestPoint<PointXYZRGB,PointXYZRGB>::align as called
+// at /root/reference/src/GICPAlignment.cpp:96 (and :116 via iterate()).  The outer loop is
+// GICP::computeTransformation (registration/impl/gicp.hpp): per iteration one correspondence
+// sweep on the GPU, then estimateRigidTransformationBFGS whose objective passes run on the
+// GPU and whose 6-DoF BFGS logic runs here (pcl_bfgs.hpp), then PCL's delta test.
+// Multi-GPU: one process per GPU, contiguous ranges of the grid-sorted source cloud per rank,
+// target replicated; every objective pass all-reduces 16 doubles over RCCL (xGMI).
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/mi355x_gicp.h"
+#include "mgicp_internal.hpp"
+#include "pcl_bfgs.hpp"
+
+using namespace mgicp;
+
+namespace {
+
+constexpr double kOccupancyTarget = 12.0;           // mean points per non-empty cell
+constexpr size_t kMaxCells = size_t(1) << 29;       // dense cell table cap (2 GiB of uint32)
+
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+struct Mat4 {  // row-major float 4x4
+  float m[4][4];
+  static Mat4 identity() {
+    Mat4 r;
+    std::memset(r.m, 0, sizeof(r.m));
+    r.m[0][0] = r.m[1][1] = r.m[2][2] = r.m[3][3] = 1.f;
+    return r;
+  }
+  static Mat4 from_cm(const float* cm) {
+    Mat4 r;
+    for (int i = 0; i < 4; ++i)
+      for (int j = 0; j < 4; ++j) r.m[i][j] = cm[j * 4 + i];
+    return r;
+  }
+  void to_cm(float* cm) const {
+    for (int i = 0; i < 4; ++i)
+      for (int j = 0; j < 4; ++j) cm[j * 4 + i] = m[i][j];
+  }
+  bool is_identity() const {
+    const Mat4 I = identity();
+    return std::memcmp(m, I.m, sizeof(m)) == 0;
+  }
+  Xf34 xf() const {
+    Xf34 x;
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 4; ++j) x.m[4 * i + j] = m[i][j];
+    return x;
+  }
+};
+
+// GICP::applyState(t = I, x): R = AngleAxisf(x5,Z) * AngleAxisf(x4,Y) * AngleAxisf(x3,X)
+// evaluated through Eigen's quaternion products, then t.col(3) += (x0, x1, x2, 0).
+struct Quat { float w, x, y, z; };
+Quat quat_axis(float angle, int axis) {
+  const float ha = 0.5f * angle;
+  const float s = std::sin(ha);
+  Quat q{std::cos(ha), 0.f, 0.f, 0.f};
+  if (axis == 0) q.x = s;
+  if (axis == 1) q.y = s;
+  if (axis == 2) q.z = s;
+  return q;
+}
+Quat quat_mul(const Quat& a, const Quat& b) {
+  Quat r;
+  r.w = a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z;
+  r.x = a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y;
+  r.y = a.w * b.y + a.y * b.w + a.z * b.x - a.x * b.z;
+  r.z = a.w * b.z + a.z * b.w + a.x * b.y - a.y * b.x;
+  return r;
+}
+Mat4 apply_state(const Vec6& x) {
+  const Quat q = quat_mul(quat_mul(quat_axis(static_cast<float>(x[5]), 2),
+                                   quat_axis(static_cast<float>(x[4]), 1)),
+                          quat_axis(static_cast<float>(x[3]), 0));
+  const float tx = 2.0f * q.x, ty = 2.0f * q.y, tz = 2.0f * q.z;
+  const float twx = tx * q.w, twy = ty * q.w, twz = tz * q.w;
+  const float txx = tx * q.x, txy = ty * q.x, txz = tz * q.x;
+  const float tyy = ty * q.y, tyz = tz * q.y, tzz = tz * q.z;
+  Mat4 T = Mat4::identity();
+  T.m[0][0] = 1.0f - (tyy + tzz);
+  T.m[0][1] = txy - twz;
+  T.m[0][2] = txz + twy;
+  T.m[1][0] = txy + twz;
+  T.m[1][1] = 1.0f - (txx + tzz);
+  T.m[1][2] = tyz - twx;
+  T.m[2][0] = txz - twy;
+  T.m[2][1] = tyz + twx;
+  T.m[2][2] = 1.0f - (txx + tyy);
+  T.m[0][3] = 0.0f + static_cast<float>(x[0]);
+  T.m[1][3] = 0.0f + static_cast<float>(x[1]);
+  T.m[2][3] = 0.0f + static_cast<float>(x[2]);
+  return T;
+}
+
+// GICP::computeRDerivative + matricesInnerProd (tr(dR * Rsum))
+void r_derivative(const Vec6& x, const double R[3][3], Vec6& g) {
+  const double phi = x[3], theta = x[4], psi = x[5];
+  const double cphi = std::cos(phi), sphi = std::sin(phi);
+  const double ctheta = std::cos(theta), stheta = std::sin(theta);
+  const double cpsi = std::cos(psi), spsi = std::sin(psi);
+  double d[3][3][3];
+  // d/dphi
+  d[0][0][0] = 0.; d[0][1][0] = 0.; d[0][2][0] = 0.;
+  d[0][0][1] = sphi * spsi + cphi * cpsi * stheta;
+  d[0][1][1] = -cpsi * sphi + cphi * spsi * stheta;
+  d[0][2][1] = cphi * ctheta;
+  d[0][0][2] = cphi * spsi - cpsi * sphi * stheta;
+  d[0][1][2] = -cphi * cpsi - sphi * spsi * stheta;
+  d[0][2][2] = -ctheta * sphi;
+  // d/dtheta
+  d[1][0][0] = -cpsi * stheta;
+  d[1][1][0] = -spsi * stheta;
+  d[1][2][0] = -ctheta;
+  d[1][0][1] = cpsi * ctheta * sphi;
+  d[1][1][1] = ctheta * sphi * spsi;
+  d[1][2][1] = -sphi * stheta;
+  d[1][0][2] = cphi * cpsi * ctheta;
+  d[1][1][2] = cphi * ctheta * spsi;
+  d[1][2][2] = -cphi * stheta;
+  // d/dpsi
+  d[2][0][0] = -ctheta * spsi;
+  d[2][1][0] = cpsi * ctheta;
+  d[2][2][0] = 0.;
+  d[2][0][1] = -cphi * cpsi - sphi * spsi * stheta;
+  d[2][1][1] = -cphi * spsi + cpsi * sphi * stheta;
+  d[2][2][1] = 0.;
+  d[2][0][2] = cpsi * sphi - cphi * spsi * stheta;
+  d[2][1][2] = sphi * spsi + cphi * cpsi * stheta;
+  d[2][2][2] = 0.;
+  for (int a = 0; a < 3; ++a) {
+    double r = 0.;
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) r += d[a][j][i] * R[i][j];
+    g[3 + a] = r;
+  }
+}
+
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t cap = 0;
+  hipError_t reserve(size_t n) {
+    if (n <= cap && p) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T));
+    if (e == hipSuccess) cap = std::max<size_t>(n, 1);
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct Cloud {
+  size_t n = 0;
+  bool dirty = false;      // grid must be rebuilt
+  bool have_cov = false;   // covariances valid for [cov_p0, cov_p1)
+  size_t cov_p0 = 0, cov_p1 = 0;
+  DevBuf<unsigned char> raw;  // staging of strided records
+  DevBuf<float4> orig;        // original order, w = index
+  DevBuf<float4> pts;         // grid-sorted
+  DevBuf<uint32_t> perm;      // sorted pos -> original index
+  DevBuf<uint32_t> cell_start;
+  DevBuf<double2> cov;        // 3 * n
+  GridView view{};
+  size_t ncells = 0;
+  Cov3 cov3() const { return Cov3{cov.p, cov.p + n, cov.p + 2 * n}; }
+};
+
+enum { kFamCov = 0, kFamCorr = 1, kFamFdf = 2, kFamRed = 3 };
+
+}  // namespace
+
+struct mgicp_ctx {
+  mgicp_params prm{};
+  std::string err;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  Cloud src, tgt;
+  double ms_upload_pending = 0;
+  // per source point (sorted), rank shard only
+  DevBuf<float4> src_out;  // guess-applied source (only when guess != I)
+  const float4* d_out = nullptr;
+  DevBuf<float4> qbuf;
+  DevBuf<double2> mahal;   // 3 * n
+  DevBuf<int> dbg_nn;
+  DevBuf<double> partial;
+  DevBuf<double> red;      // kRedVals
+  double* h_red = nullptr; // pinned
+  // build scratch
+  DevBuf<uint32_t> counts, keys, keys_sorted, vals;
+  DevBuf<unsigned char> scratch;
+  DevBuf<unsigned long long> u64;
+  DevBuf<float> fpartial;
+  // multi-GPU
+  int nranks = 1, rank = 0;
+  ncclComm_t comm = nullptr;
+  // state of the last correspondence sweep
+  bool have_corr = false;
+  Mat4 last_guess = Mat4::identity();
+  std::vector<float> trace;
+  int n_evals = 0;
+  // profiling
+  bool profiling = false;
+  struct EvPair { hipEvent_t a, b; int fam; };
+  std::vector<EvPair> pending;
+  std::vector<hipEvent_t> pool;
+  double fam_ms[4] = {0, 0, 0, 0};
+  int fam_cnt[4] = {0, 0, 0, 0};
+
+  size_t shard_p0() const { return src.n * static_cast<size_t>(rank) / nranks; }
+  size_t shard_p1() const { return src.n * static_cast<size_t>(rank + 1) / nranks; }
+};
+
+namespace {
+
+int fail(mgicp_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+#define HIPCK(expr)                                                                    \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess)                                                              \
+      return fail(ctx, (e_ == hipErrorOutOfMemory) ? MGICP_E_NOMEM : MGICP_E_HIP,      \
+                  std::string(#expr) + ": " + hipGetErrorString(e_));                  \
+  } while (0)
+
+#define NCCLCK(expr)                                                                   \
+  do {                                                                                 \
+    ncclResult_t r_ = (expr);                                                          \
+    if (r_ != ncclSuccess)                                                             \
+      return fail(ctx, MGICP_E_COMM, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+  } while (0)
+
+hipEvent_t ev_get(mgicp_ctx* ctx) {
+  if (!ctx->pool.empty()) {
+    hipEvent_t e = ctx->pool.back();
+    ctx->pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+struct ProfScope {
+  mgicp_ctx* ctx;
+  int fam;
+  hipEvent_t a = nullptr;
+  ProfScope(mgicp_ctx* c, int f) : ctx(c), fam(f) {
+    if (ctx->profiling) {
+      a = ev_get(ctx);
+      (void)hipEventRecord(a, ctx->stream);
+    }
+  }
+  ~ProfScope() {
+    if (a) {
+      hipEvent_t b = ev_get(ctx);
+      (void)hipEventRecord(b, ctx->stream);
+      ctx->pending.push_back({a, b, fam});
+    }
+  }
+};
+
+void prof_resolve(mgicp_ctx* ctx) {
+  for (auto& p : ctx->pending) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+      ctx->fam_ms[p.fam] += ms;
+      ctx->fam_cnt[p.fam] += 1;
+    }
+    ctx->pool.push_back(p.a);
+    ctx->pool.push_back(p.b);
+  }
+  ctx->pending.clear();
+}
+
+int sync(mgicp_ctx* ctx) {
+  HIPCK(hipStreamSynchronize(ctx->stream));
+  if (ctx->profiling) prof_resolve(ctx);
+  return MGICP_OK;
+}
+
+// Upload strided host records (or copy device records) and pack to float4 (original order).
+int upload_cloud(mgicp_ctx* ctx, Cloud& cl, const float* xyz, size_t n, size_t stride,
+                 bool device_ptr) {
+  if (n == 0 || !xyz || stride < 12 || (stride % 4) != 0)
+    return fail(ctx, MGICP_E_INVALID, "invalid cloud (null, empty or stride not a multiple of 4 >= 12)");
+  const double t0 = now_ms();
+  HIPCK(cl.orig.reserve(n));
+  if (device_ptr) {
+    HIPCK(launch_pack_points(xyz, n, stride, cl.orig.p, ctx->stream));
+  } else {
+    HIPCK(cl.raw.reserve(n * stride));
+    HIPCK(hipMemcpyAsync(cl.raw.p, xyz, n * stride, hipMemcpyHostToDevice, ctx->stream));
+    HIPCK(launch_pack_points(cl.raw.p, n, stride, cl.orig.p, ctx->stream));
+  }
+  int rc = sync(ctx);
+  if (rc) return rc;
+  cl.raw.release();
+  cl.n = n;
+  cl.dirty = true;
+  cl.have_cov = false;
+  ctx->have_corr = false;
+  ctx->ms_upload_pending += now_ms() - t0;
+  return MGICP_OK;
+}
+
+// Build the row-sorted uniform grid of a cloud (one-time per set_*).
+int build_grid(mgicp_ctx* ctx, Cloud& cl) {
+  const size_t n = cl.n;
+  hipStream_t s = ctx->stream;
+  // 1. bounding box + finiteness
+  const int nb = static_cast<int>(std::min<size_t>((n + 255) / 256, 1024));
+  HIPCK(ctx->fpartial.reserve(static_cast<size_t>(nb) * 8));
+  HIPCK(launch_bbox(cl.orig.p, n, ctx->fpartial.p, nb, s));
+  std::vector<float> hp(static_cast<size_t>(nb) * 8);
+  HIPCK(hipMemcpyAsync(hp.data(), ctx->fpartial.p, hp.size() * sizeof(float),
+                       hipMemcpyDeviceToHost, s));
+  int rc = sync(ctx);
+  if (rc) return rc;
+  float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+  double bad = 0;
+  for (int b = 0; b < nb; ++b) {
+    for (int d = 0; d < 3; ++d) {
+      mn[d] = std::min(mn[d], hp[b * 8 + d]);
+      mx[d] = std::max(mx[d], hp[b * 8 + 3 + d]);
+    }
+    bad += hp[b * 8 + 6];
+  }
+  if (bad > 0) return fail(ctx, MGICP_E_NONFINITE, "cloud contains NaN/Inf coordinates");
+  float ext[3];
+  float maxext = 0.f, maxabs = 0.f;
+  for (int d = 0; d < 3; ++d) {
+    ext[d] = mx[d] - mn[d];
+    maxext = std::max(maxext, ext[d]);
+    maxabs = std::max(maxabs, std::max(std::fabs(mn[d]), std::fabs(mx[d])));
+  }
+  // 2. cell size: aim at kOccupancyTarget points per non-empty cell
+  auto dims = [&](double h, int* nd) {
+    size_t nc = 1;
+    for (int d = 0; d < 3; ++d) {
+      const float inv_h = static_cast<float>(1.0 / h);
+      nd[d] = static_cast<int>(std::floor(static_cast<double>(ext[d]) * inv_h)) + 1;
+      nc *= static_cast<size_t>(nd[d]);
+    }
+    return nc;
+  };
+  double h = maxext > 0.f ? static_cast<double>(maxext) / std::cbrt(static_cast<double>(n)) : 1.0;
+  h = std::max(h, 1e-6);
+  int nd[3];
+  double h_prev = 0, occ_prev = 0;
+  HIPCK(ctx->u64.reserve(1));
+  for (int it = 0; it < 6 && maxext > 0.f; ++it) {
+    size_t nc = dims(h, nd);
+    int guard = 0;
+    while (nc > kMaxCells && guard++ < 64) {
+      h *= std::cbrt(static_cast<double>(nc) / kMaxCells) * 1.01;
+      nc = dims(h, nd);
+    }
+    HIPCK(ctx->counts.reserve(nc + 1));
+    HIPCK(hipMemsetAsync(ctx->counts.p, 0, (nc + 1) * sizeof(uint32_t), s));
+    HIPCK(hipMemsetAsync(ctx->u64.p, 0, sizeof(unsigned long long), s));
+    HIPCK(launch_cell_hist(cl.orig.p, n, mn[0], mn[1], mn[2], static_cast<float>(1.0 / h), nd[0],
+                           nd[1], nd[2], ctx->counts.p, nullptr, s));
+    HIPCK(launch_count_nonzero(ctx->counts.p, nc, ctx->u64.p, s));
+    unsigned long long nonempty = 0;
+    HIPCK(hipMemcpyAsync(&nonempty, ctx->u64.p, sizeof(nonempty), hipMemcpyDeviceToHost, s));
+    rc = sync(ctx);
+    if (rc) return rc;
+    const double occ = static_cast<double>(n) / std::max<unsigned long long>(nonempty, 1);
+    if ((occ > 0.6 * kOccupancyTarget && occ < 1.6 * kOccupancyTarget) || nc >= kMaxCells / 2)
+      break;
+    if (nonempty <= 1 && occ < kOccupancyTarget) break;  // everything in one cell already
+    double dim = 2.0;
+    if (h_prev > 0 && occ_prev > 0 && std::fabs(std::log(h / h_prev)) > 1e-3) {
+      dim = std::log(occ / occ_prev) / std::log(h / h_prev);
+      dim = std::min(3.0, std::max(1.0, dim));
+    }
+    h_prev = h;
+    occ_prev = occ;
+    h = h * std::pow(kOccupancyTarget / occ, 1.0 / dim);
+    h = std::max(h, 1e-6);
+  }
+  size_t nc = dims(h, nd);
+  while (nc > kMaxCells) {
+    h *= std::cbrt(static_cast<double>(nc) / kMaxCells) * 1.01;
+    nc = dims(h, nd);
+  }
+  const float inv_h = static_cast<float>(1.0 / h);
+  // 3. final histogram with keys, scan -> cell_start, stable radix sort -> permutation
+  HIPCK(ctx->counts.reserve(nc + 1));
+  HIPCK(ctx->keys.reserve(n));
+  HIPCK(ctx->keys_sorted.reserve(n));
+  HIPCK(ctx->vals.reserve(n));
+  HIPCK(cl.perm.reserve(n));
+  HIPCK(cl.cell_start.reserve(nc + 1));
+  HIPCK(cl.pts.reserve(n));
+  HIPCK(hipMemsetAsync(ctx->counts.p, 0, (nc + 1) * sizeof(uint32_t), s));
+  HIPCK(launch_cell_hist(cl.orig.p, n, mn[0], mn[1], mn[2], inv_h, nd[0], nd[1], nd[2],
+                         ctx->counts.p, ctx->keys.p, s));
+  int bits = 1;
+  while ((size_t(1) << bits) < nc && bits < 32) ++bits;
+  const size_t sb = std::max(sort_scratch_bytes(n, bits), scan_scratch_bytes(nc + 1));
+  HIPCK(ctx->scratch.reserve(sb));
+  HIPCK(launch_exclusive_scan(ctx->scratch.p, sb, ctx->counts.p, cl.cell_start.p, nc + 1, s));
+  HIPCK(launch_iota(ctx->vals.p, n, s));
+  HIPCK(launch_sort_pairs(ctx->scratch.p, sb, ctx->keys.p, ctx->keys_sorted.p, ctx->vals.p,
+                          cl.perm.p, n, bits, s));
+  HIPCK(launch_gather_sorted(cl.orig.p, cl.perm.p, n, cl.pts.p, s));
+  rc = sync(ctx);
+  if (rc) return rc;
+  ctx->counts.release();
+  ctx->keys.release();
+  ctx->keys_sorted.release();
+  ctx->vals.release();
+  GridView& g = cl.view;
+  g.ox = mn[0];
+  g.oy = mn[1];
+  g.oz = mn[2];
+  g.h = static_cast<float>(h);
+  g.inv_h = inv_h;
+  // rounding slack: a few ulps of the largest coordinate plus a sliver of a cell
+  g.slop = 8.f * maxabs * 1.1920929e-7f + 1e-6f * static_cast<float>(h);
+  g.nx = nd[0];
+  g.ny = nd[1];
+  g.nz = nd[2];
+  g.cell_start = cl.cell_start.p;
+  g.pts = cl.pts.p;
+  cl.ncells = nc;
+  cl.dirty = false;
+  cl.have_cov = false;
+  return MGICP_OK;
+}
+
+int compute_cov(mgicp_ctx* ctx, Cloud& cl, size_t p0, size_t p1) {
+  HIPCK(cl.cov.reserve(3 * cl.n));
+  {
+    ProfScope ps(ctx, kFamCov);
+    HIPCK(launch_knn_cov(cl.view, ctx->prm.k, ctx->prm.gicp_eps, p0, p1, cl.cov3(), ctx->stream));
+  }
+  int rc = sync(ctx);
+  if (rc) return rc;
+  cl.have_cov = true;
+  cl.cov_p0 = p0;
+  cl.cov_p1 = p1;
+  return MGICP_OK;
+}
+
+// Registration::initCompute + initComputeReciprocal + computeCovariances (both clouds)
+int prepare(mgicp_ctx* ctx, bool need_cov) {
+  if (ctx->src.n == 0 || ctx->tgt.n == 0)
+    return fail(ctx, MGICP_E_INVALID, "source and target clouds must be set before align");
+  const int k = ctx->prm.k;
+  if (static_cast<size_t>(k) > ctx->src.n || static_cast<size_t>(k) > ctx->tgt.n)
+    return fail(ctx, MGICP_E_TOO_FEW_POINTS,
+                "a cloud has fewer points than k_correspondences (PCL computeCovariances)");
+  int rc;
+  if (ctx->tgt.dirty && (rc = build_grid(ctx, ctx->tgt))) return rc;
+  if (ctx->src.dirty && (rc = build_grid(ctx, ctx->src))) return rc;
+  if (!need_cov) return MGICP_OK;
+  if (!ctx->tgt.have_cov && (rc = compute_cov(ctx, ctx->tgt, 0, ctx->tgt.n))) return rc;
+  if (!ctx->src.have_cov || ctx->src.cov_p0 != ctx->shard_p0() || ctx->src.cov_p1 != ctx->shard_p1())
+    if ((rc = compute_cov(ctx, ctx->src, ctx->shard_p0(), ctx->shard_p1()))) return rc;
+  return MGICP_OK;
+}
+
+int ensure_iter_buffers(mgicp_ctx* ctx) {
+  const size_t n = ctx->src.n;
+  HIPCK(ctx->qbuf.reserve(n));
+  HIPCK(ctx->mahal.reserve(3 * n));
+  const int nb = std::max(fdf_grid_blocks(n), static_cast<int>((n + 255) / 256));
+  HIPCK(ctx->partial.reserve(static_cast<size_t>(nb) * kRedVals));
+  HIPCK(ctx->red.reserve(kRedVals));
+  if (!ctx->h_red) HIPCK(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_red), kRedVals * sizeof(double)));
+  return MGICP_OK;
+}
+
+Cov3 mahal3(mgicp_ctx* ctx) {
+  const size_t n = ctx->src.n;
+  return Cov3{ctx->mahal.p, ctx->mahal.p + n, ctx->mahal.p + 2 * n};
+}
+
+// guess-applied source cloud ("output" after transformPointCloud(output, output, guess))
+int set_output(mgicp_ctx* ctx, const Mat4& G) {
+  if (G.is_identity()) {
+    ctx->d_out = ctx->src.pts.p;  // x*1 + y*0 + z*0 + 0 == x: identity leaves points intact
+  } else {
+    HIPCK(ctx->src_out.reserve(ctx->src.n));
+    HIPCK(launch_xform_points(ctx->src.pts.p, ctx->src.n, G.xf(), ctx->src_out.p, ctx->stream));
+    ctx->d_out = ctx->src_out.p;
+  }
+  ctx->last_guess = G;
+  return MGICP_OK;
+}
+
+// transform_R(i,j) = sum_k double(T(i,k)) * double(G(k,j)), top-left 3x3
+Rot33d rot_of(const Mat4& T, const Mat4& G) {
+  Rot33d R;
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      double a = 0.0;
+      for (int k = 0; k < 4; ++k) a += static_cast<double>(T.m[i][k]) * static_cast<double>(G.m[k][j]);
+      R.m[3 * i + j] = a;
+    }
+  return R;
+}
+
+int correspond(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, int* dbg) {
+  const double thr = ctx->prm.max_corr_dist * ctx->prm.max_corr_dist;
+  ProfScope ps(ctx, kFamCorr);
+  HIPCK(launch_correspond(ctx->tgt.view, ctx->tgt.cov3(), ctx->d_out, ctx->src.cov3(),
+                          ctx->shard_p0(), ctx->shard_p1(), T.xf(), rot_of(T, G), thr,
+                          ctx->qbuf.p, mahal3(ctx), dbg, ctx->stream));
+  ctx->have_corr = true;
+  return MGICP_OK;
+}
+
+// finish the block partials (fixed order), all-reduce across ranks, copy to host
+int reduce_to_host(mgicp_ctx* ctx, int nb) {
+  {
+    ProfScope ps(ctx, kFamRed);
+    HIPCK(launch_reduce_finish(ctx->partial.p, nb, ctx->red.p, ctx->stream));
+  }
+  if (ctx->nranks > 1)
+    NCCLCK(ncclAllReduce(ctx->red.p, ctx->red.p, kRedVals, ncclDouble, ncclSum, ctx->comm,
+                         ctx->stream));
+  HIPCK(hipMemcpyAsync(ctx->h_red, ctx->red.p, kRedVals * sizeof(double), hipMemcpyDeviceToHost,
+                       ctx->stream));
+  return sync(ctx);
+}
+
+// OptimizationFunctorWithIndices::fdf on the device; memoises the last state
+struct DeviceFunctor {
+  mgicp_ctx* ctx;
+  bool have_memo = false;
+  Vec6 memo_x{};
+  double memo_f = 0;
+  Vec6 memo_g{};
+  double m = 0;  // correspondences of this sweep (all ranks)
+
+  int pass(const Vec6& x, double sums[kRedVals]) {
+    const Mat4 A = apply_state(x);
+    const size_t p0 = ctx->shard_p0(), p1 = ctx->shard_p1();
+    const int nb = fdf_grid_blocks(p1 - p0);
+    {
+      ProfScope ps(ctx, kFamFdf);
+      HIPCK(launch_fdf(ctx->d_out, ctx->qbuf.p, mahal3(ctx), p0, p1, A.xf(), ctx->partial.p, nb,
+                       ctx->stream));
+    }
+    int rc = reduce_to_host(ctx, nb);
+    if (rc) return rc;
+    std::memcpy(sums, ctx->h_red, kRedVals * sizeof(double));
+    ctx->n_evals++;
+    return MGICP_OK;
+  }
+
+  int eval(const Vec6& x, double& f, Vec6& g) {
+    if (have_memo && std::memcmp(x.v, memo_x.v, sizeof(x.v)) == 0) {
+      f = memo_f;
+      g = memo_g;
+      return 0;
+    }
+    double s[kRedVals];
+    int rc = pass(x, s);
+    if (rc) return rc;
+    m = s[13];
+    f = s[0] / m;
+    const double sc = 2.0 / m;
+    g[0] = s[1] * sc;
+    g[1] = s[2] * sc;
+    g[2] = s[3] * sc;
+    double R[3][3];
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) R[a][b] = s[4 + 3 * a + b] * sc;
+    r_derivative(x, R, g);
+    have_memo = true;
+    memo_x = x;
+    memo_f = f;
+    memo_g = g;
+    return 0;
+  }
+};
+
+// GICP::estimateRigidTransformationBFGS: 0 = accepted, MGICP_E_SOLVER = PCL would throw
+int estimate_bfgs(mgicp_ctx* ctx, Mat4& T, int* n_corr) {
+  Vec6 x;
+  x[0] = T.m[0][3];
+  x[1] = T.m[1][3];
+  x[2] = T.m[2][3];
+  x[3] = std::atan2(static_cast<double>(T.m[2][1]), static_cast<double>(T.m[2][2]));
+  x[4] = std::asin(-static_cast<double>(T.m[2][0]));
+  x[5] = std::atan2(static_cast<double>(T.m[1][0]), static_cast<double>(T.m[0][0]));
+  DeviceFunctor fn{ctx};
+  // the correspondence count arrives with the first objective pass (its count lane)
+  double s[kRedVals];
+  int rc = fn.pass(x, s);
+  if (rc) return rc;
+  *n_corr = static_cast<int>(s[13]);
+  if (s[13] < 4) return MGICP_E_SOLVER;  // NotEnoughPointsException
+  {
+    // seed the memo with this pass so minimizeInit reuses it
+    fn.m = s[13];
+    fn.memo_x = x;
+    fn.memo_f = s[0] / fn.m;
+    const double sc = 2.0 / fn.m;
+    fn.memo_g[0] = s[1] * sc;
+    fn.memo_g[1] = s[2] * sc;
+    fn.memo_g[2] = s[3] * sc;
+    double R[3][3];
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) R[a][b] = s[4 + 3 * a + b] * sc;
+    r_derivative(x, R, fn.memo_g);
+    fn.have_memo = true;
+  }
+  PclBfgs<DeviceFunctor> bfgs(fn);
+  const double gradient_tol = 1e-2;
+  int inner = 0;
+  int result = bfgs.init(x);
+  result = kRunning;
+  do {
+    inner++;
+    result = bfgs.step(x);
+    if (bfgs.error) return bfgs.error;
+    if (result) break;
+    result = bfgs.test_gradient(gradient_tol);
+  } while (result == kRunning && inner < ctx->prm.max_inner_iter);
+  if (bfgs.error) return bfgs.error;
+  if (result == kNoProgress || result == kSuccess || inner == ctx->prm.max_inner_iter) {
+    T = apply_state(x);
+    return MGICP_OK;
+  }
+  return MGICP_E_SOLVER;  // SolverDidntConvergeException
+}
+
+int check_params(mgicp_ctx* ctx, const mgicp_params& p) {
+  const int k = p.k;
+  if (!(k == 5 || k == 10 || k == 15 || k == 20 || k == 25 || k == 30))
+    return fail(ctx, MGICP_E_INVALID, "k must be one of 5, 10, 15, 20, 25, 30");
+  if (p.max_iter < 1 || p.max_inner_iter < 1 || !(p.max_corr_dist >= 0) || !(p.rot_eps > 0) ||
+      !(p.tf_eps >= 0) || p.solver != MGICP_SOLVER_PCL_BFGS)
+    return fail(ctx, MGICP_E_INVALID, "invalid GICP parameters");
+  return MGICP_OK;
+}
+
+}  // namespace
+
+// =====================================================================================
+// C-ABI
+// =====================================================================================
+extern "C" {
+
+void mgicp_default_params(mgicp_params* p) {
+  if (!p) return;
+  p->max_iter = 100;        // GICPAlignment.cpp:30
+  p->tf_eps = 4e-3;         // GICPAlignment.cpp:29
+  p->rot_eps = 2e-3;        // PCL GICP rotation_epsilon_
+  p->max_corr_dist = 4e-2;  // GICPAlignment.cpp:31
+  p->gicp_eps = 1e-3;       // PCL GICP gicp_epsilon_
+  p->k = 20;                // PCL GICP k_correspondences_
+  p->max_inner_iter = 20;   // PCL GICP max_inner_iterations_
+  p->solver = MGICP_SOLVER_PCL_BFGS;
+  p->device = -1;
+  p->fixed_iterations = 0;
+}
+
+int mgicp_device_count(int* n) {
+  if (!n) return MGICP_E_INVALID;
+  return hipGetDeviceCount(n) == hipSuccess ? MGICP_OK : MGICP_E_HIP;
+}
+
+int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
+  if (!out) return MGICP_E_INVALID;
+  *out = nullptr;
+  mgicp_ctx* ctx = new mgicp_ctx();
+  if (p) ctx->prm = *p;
+  else mgicp_default_params(&ctx->prm);
+  int rc = check_params(ctx, ctx->prm);
+  if (rc) {
+    delete ctx;
+    return rc;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+    delete ctx;
+    return MGICP_E_HIP;
+  }
+  if (ctx->prm.device >= 0) {
+    if (ctx->prm.device >= ndev || hipSetDevice(ctx->prm.device) != hipSuccess) {
+      delete ctx;
+      return MGICP_E_INVALID;
+    }
+    ctx->device = ctx->prm.device;
+  } else if (hipGetDevice(&ctx->device) != hipSuccess) {
+    delete ctx;
+    return MGICP_E_HIP;
+  }
+  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete ctx;
+    return MGICP_E_HIP;
+  }
+  *out = ctx;
+  return MGICP_OK;
+}
+
+int mgicp_set_params(mgicp_ctx* ctx, const mgicp_params* p) {
+  if (!ctx || !p) return MGICP_E_INVALID;
+  int rc = check_params(ctx, *p);
+  if (rc) return rc;
+  const bool cov_change = p->k != ctx->prm.k || p->gicp_eps != ctx->prm.gicp_eps;
+  const int dev = ctx->device;
+  ctx->prm = *p;
+  ctx->prm.device = dev;
+  if (cov_change) {
+    ctx->src.have_cov = false;
+    ctx->tgt.have_cov = false;
+  }
+  return MGICP_OK;
+}
+
+const char* mgicp_last_error(const mgicp_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+void mgicp_destroy(mgicp_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  for (Cloud* c : {&ctx->src, &ctx->tgt}) {
+    c->raw.release(); c->orig.release(); c->pts.release(); c->perm.release();
+    c->cell_start.release(); c->cov.release();
+  }
+  ctx->src_out.release(); ctx->qbuf.release(); ctx->mahal.release(); ctx->dbg_nn.release();
+  ctx->partial.release(); ctx->red.release(); ctx->counts.release(); ctx->keys.release();
+  ctx->keys_sorted.release(); ctx->vals.release(); ctx->scratch.release(); ctx->u64.release();
+  ctx->fpartial.release();
+  if (ctx->h_red) (void)hipHostFree(ctx->h_red);
+  prof_resolve(ctx);
+  for (hipEvent_t e : ctx->pool) (void)hipEventDestroy(e);
+  if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+int mgicp_set_target(mgicp_ctx* ctx, const float* xyz, size_t n, size_t stride) {
+  if (!ctx) return MGICP_E_INVALID;
+  HIPCK(hipSetDevice(ctx->device));
+  return upload_cloud(ctx, ctx->tgt, xyz, n, stride, false);
+}
+int mgicp_set_source(mgicp_ctx* ctx, const float* xyz, size_t n, size_t stride) {
+  if (!ctx) return MGICP_E_INVALID;
+  HIPCK(hipSetDevice(ctx->device));
+  return upload_cloud(ctx, ctx->src, xyz, n, stride, false);
+}
+int mgicp_set_target_device(mgicp_ctx* ctx, const float* d_xyz, size_t n, size_t stride) {
+  if (!ctx) return MGICP_E_INVALID;
+  HIPCK(hipSetDevice(ctx->device));
+  return upload_cloud(ctx, ctx->tgt, d_xyz, n, stride, true);
+}
+int mgicp_set_source_device(mgicp_ctx* ctx, const float* d_xyz, size_t n, size_t stride) {
+  if (!ctx) return MGICP_E_INVALID;
+  HIPCK(hipSetDevice(ctx->device));
+  return upload_cloud(ctx, ctx->src, d_xyz, n, stride, true);
+}
+
+int mgicp_align(mgicp_ctx* ctx, const float guess_cm[16], float out_T_cm[16], mgicp_result* res) {
+  if (!ctx || !out_T_cm) return MGICP_E_INVALID;
+  HIPCK(hipSetDevice(ctx->device));
+  mgicp_result r;
+  std::memset(&r, 0, sizeof(r));
+  const double t0 = now_ms();
+  int rc = prepare(ctx, true);
+  if (rc) return rc;
+  rc = ensure_iter_buffers(ctx);
+  if (rc) return rc;
+  const double t1 = now_ms();
+  const Mat4 G = guess_cm ? Mat4::from_cm(guess_cm) : Mat4::identity();
+  if ((rc = set_output(ctx, G))) return rc;
+
+  Mat4 T = Mat4::identity(), prev = Mat4::identity();
+  ctx->trace.clear();
+  ctx->n_evals = 0;
+  int nr_iterations = 0;
+  bool converged = false;
+  int solver_rc = MGICP_OK;
+  while (!converged) {
+    if ((rc = correspond(ctx, T, G, nullptr))) return rc;
+    prev = T;
+    int ncorr = 0;
+    rc = estimate_bfgs(ctx, T, &ncorr);
+    r.n_corr = ncorr;
+    if (rc == MGICP_E_SOLVER) {  // PCLException caught: converged_ stays false
+      T = prev;
+      solver_rc = rc;
+      break;
+    }
+    if (rc) return rc;
+    double delta = 0.;
+    for (int k = 0; k < 4; ++k)
+      for (int l = 0; l < 4; ++l) {
+        const double ratio = (k < 3 && l < 3) ? 1. / ctx->prm.rot_eps : 1. / ctx->prm.tf_eps;
+        const double c_delta = ratio * static_cast<double>(std::fabs(prev.m[k][l] - T.m[k][l]));
+        if (c_delta > delta) delta = c_delta;
+      }
+    float tcm[16];
+    T.to_cm(tcm);
+    ctx->trace.insert(ctx->trace.end(), tcm, tcm + 16);
+    nr_iterations++;
+    const bool stop = ctx->prm.fixed_iterations
+                          ? nr_iterations >= ctx->prm.max_iter
+                          : (nr_iterations >= ctx->prm.max_iter || delta < 1);
+    if (stop) {
+      converged = true;
+      prev = T;
+    }
+  }
+  // final_transformation_ = previous_transformation_ (3x3) * guess (3x3); t = prev t + guess t
+  Mat4 F = Mat4::identity();
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      float a = prev.m[i][0] * G.m[0][j];
+      a = a + prev.m[i][1] * G.m[1][j];
+      a = a + prev.m[i][2] * G.m[2][j];
+      F.m[i][j] = a;
+    }
+  for (int i = 0; i < 3; ++i) F.m[i][3] = prev.m[i][3] + G.m[i][3];
+  F.to_cm(out_T_cm);
+  const double t2 = now_ms();
+  r.converged = converged ? 1 : 0;
+  r.iterations = nr_iterations;
+  r.n_evals = ctx->n_evals;
+  r.ms_upload = ctx->ms_upload_pending;
+  ctx->ms_upload_pending = 0;
+  r.ms_prep = t1 - t0;
+  r.ms_loop = t2 - t1;
+  r.ms_total = t2 - t0 + r.ms_upload;
+  if (res) *res = r;
+  if (solver_rc) return fail(ctx, solver_rc, "GICP solver threw (fewer than 4 correspondences or BFGS failure)");
+  return MGICP_OK;
+}
+
+int mgicp_fitness(mgicp_ctx* ctx, const float T_cm[16], double max_range, double* out) {
+  if (!ctx || !T_cm || !out) return MGICP_E_INVALID;
+  HIPCK(hipSetDevice(ctx->device));
+  int rc = prepare(ctx, false);
+  if (rc) return rc;
+  if ((rc = ensure_iter_buffers(ctx))) return rc;
+  if (!(max_range > 0)) max_range = 1.7976931348623157e308;
+  const Mat4 T = Mat4::from_cm(T_cm);
+  const size_t p0 = ctx->shard_p0(), p1 = ctx->shard_p1();
+  const int nb = static_cast<int>(std::max<size_t>(1, (p1 - p0 + 255) / 256));
+  HIPCK(ctx->partial.reserve(static_cast<size_t>(nb) * kRedVals));
+  HIPCK(launch_fitness(ctx->tgt.view, ctx->src.pts.p, p0, p1, T.xf(), max_range, ctx->partial.p,
+                       nb, ctx->stream));
+  if ((rc = reduce_to_host(ctx, nb))) return rc;
+  const double nr = ctx->h_red[13];
+  *out = nr > 0 ? ctx->h_red[0] / nr : 1.7976931348623157e308;
+  return MGICP_OK;
+}
+
+int mgicp_transform_source(mgicp_ctx* ctx, const float T_cm[16], float* out, size_t out_stride) {
+  if (!ctx || !T_cm || !out || out_stride < 12 || ctx->src.n == 0) return MGICP_E_INVALID;
+  HIPCK(hipSetDevice(ctx->device));
+  const size_t n = ctx->src.n;
+  DevBuf<float4> tmp;
+  HIPCK(tmp.reserve(n));
+  HIPCK(launch_xform_points(ctx->src.orig.p, n, Mat4::from_cm(T_cm).xf(), tmp.p, ctx->stream));
+  std::vector<float4> h(n);
+  HIPCK(hipMemcpyAsync(h.data(), tmp.p, n * sizeof(float4), hipMemcpyDeviceToHost, ctx->stream));
+  int rc = sync(ctx);
+  tmp.release();
+  if (rc) return rc;
+  unsigned char* base = reinterpret_cast<unsigned char*>(out);
+  for (size_t i = 0; i < n; ++i) {
+    float* o = reinterpret_cast<float*>(base + i * out_stride);
+    o[0] = h[i].x;
+    o[1] = h[i].y;
+    o[2] = h[i].z;
+  }
+  return MGICP_OK;
+}
+
+int mgicp_get_unique_id(unsigned char id[128]) {
+  if (!id) return MGICP_E_INVALID;
+  ncclUniqueId uid;
+  if (ncclGetUniqueId(&uid) != ncclSuccess) return MGICP_E_COMM;
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
+  std::memcpy(id, &uid, 128);
+  return MGICP_OK;
+}
+
+int mgicp_comm_init(mgicp_ctx* ctx, int nranks, int rank, const unsigned char id[128]) {
+  if (!ctx || nranks < 1 || rank < 0 || rank >= nranks || (nranks > 1 && !id)) return MGICP_E_INVALID;
+  HIPCK(hipSetDevice(ctx->device));
+  if (ctx->comm) {
+    (void)ncclCommDestroy(ctx->comm);
+    ctx->comm = nullptr;
+  }
+  ctx->nranks = nranks;
+  ctx->rank = rank;
+  ctx->src.have_cov = false;
+  ctx->have_corr = false;
+  if (nranks == 1) return MGICP_OK;
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, 128);
+  NCCLCK(ncclCommInitRank(&ctx->comm, nranks, uid, rank));
+  return MGICP_OK;
+}
+
+int mgicp_debug_covariances(mgicp_ctx* ctx, int which, double* out_c6) {
+  if (!ctx || !out_c6 || (which != 0 && which != 1)) return MGICP_E_INVALID;
+  HIPCK(hipSetDevice(ctx->device));
+  int rc = prepare(ctx, true);
+  if (rc) return rc;
+  Cloud& cl = which ? ctx->tgt : ctx->src;
+  const size_t n = cl.n;
+  std::vector<double2> h(3 * n);
+  std::vector<uint32_t> perm(n);
+  HIPCK(hipMemcpyAsync(h.data(), cl.cov.p, 3 * n * sizeof(double2), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCK(hipMemcpyAsync(perm.data(), cl.perm.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+  if ((rc = sync(ctx))) return rc;
+  for (size_t p = 0; p < n; ++p) {
+    double* o = out_c6 + 6 * static_cast<size_t>(perm[p]);
+    o[0] = h[p].x; o[1] = h[p].y;
+    o[2] = h[n + p].x; o[3] = h[n + p].y;
+    o[4] = h[2 * n + p].x; o[5] = h[2 * n + p].y;
+  }
+  return MGICP_OK;
+}
+
+int mgicp_debug_correspondences(mgicp_ctx* ctx, const float T_cm[16], int* out_tgt, double* out_M6) {
+  if (!ctx || !T_cm) return MGICP_E_INVALID;
+  HIPCK(hipSetDevice(ctx->device));
+  int rc = prepare(ctx, true);
+  if (rc) return rc;
+  if ((rc = ensure_iter_buffers(ctx))) return rc;
+  const size_t n = ctx->src.n;
+  HIPCK(ctx->dbg_nn.reserve(n));
+  HIPCK(hipMemsetAsync(ctx->dbg_nn.p, 0xff, n * sizeof(int), ctx->stream));
+  const Mat4 G = Mat4::identity();
+  if ((rc = set_output(ctx, G))) return rc;
+  if ((rc = correspond(ctx, Mat4::from_cm(T_cm), G, ctx->dbg_nn.p))) return rc;
+  std::vector<int> nn(n);
+  std::vector<double2> M(3 * n);
+  std::vector<uint32_t> perm(n);
+  HIPCK(hipMemcpyAsync(nn.data(), ctx->dbg_nn.p, n * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCK(hipMemcpyAsync(M.data(), ctx->mahal.p, 3 * n * sizeof(double2), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCK(hipMemcpyAsync(perm.data(), ctx->src.perm.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+  if ((rc = sync(ctx))) return rc;
+  int cnt = 0;
+  const size_t p0 = ctx->shard_p0(), p1 = ctx->shard_p1();
+  for (size_t p = p0; p < p1; ++p) {
+    const size_t i = perm[p];
+    if (out_tgt) out_tgt[i] = nn[p];
+    if (nn[p] >= 0) cnt++;
+    if (out_M6) {
+      double* o = out_M6 + 6 * i;
+      o[0] = M[p].x; o[1] = M[p].y;
+      o[2] = M[n + p].x; o[3] = M[n + p].y;
+      o[4] = M[2 * n + p].x; o[5] = M[2 * n + p].y;
+    }
+  }
+  return cnt;
+}
+
+int mgicp_debug_fdf(mgicp_ctx* ctx, const double x[6], double* f, double g6[6]) {
+  if (!ctx || !x || !ctx->have_corr) return MGICP_E_INVALID;
+  HIPCK(hipSetDevice(ctx->device));
+  DeviceFunctor fn{ctx};
+  Vec6 xv, gv;
+  for (int i = 0; i < 6; ++i) xv[i] = x[i];
+  double fv = 0;
+  int rc = fn.eval(xv, fv, gv);
+  if (rc) return rc;
+  if (f) *f = fv;
+  if (g6)
+    for (int i = 0; i < 6; ++i) g6[i] = gv[i];
+  return MGICP_OK;
+}
+
+int mgicp_debug_trace(mgicp_ctx* ctx, float* out, int max_iters) {
+  if (!ctx || !out || max_iters < 0) return MGICP_E_INVALID;
+  const int n = static_cast<int>(ctx->trace.size() / 16);
+  const int m = std::min(n, max_iters);
+  std::memcpy(out, ctx->trace.data(), static_cast<size_t>(m) * 16 * sizeof(float));
+  return n;
+}
+
+int mgicp_debug_kernel_times(mgicp_ctx* ctx, double out_ms[4], int out_counts[4]) {
+  if (!ctx || !out_ms) return MGICP_E_INVALID;
+  prof_resolve(ctx);
+  for (int i = 0; i < 4; ++i) {
+    out_ms[i] = ctx->fam_cnt[i] ? ctx->fam_ms[i] / ctx->fam_cnt[i] : 0.0;
+    if (out_counts) out_counts[i] = ctx->fam_cnt[i];
+  }
+  return MGICP_OK;
+}
+
+int mgicp_set_profiling(mgicp_ctx* ctx, int on) {
+  if (!ctx) return MGICP_E_INVALID;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  prof_resolve(ctx);
+  ctx->profiling = on != 0;
+  for (int i = 0; i < 4; ++i) {
+    ctx->fam_ms[i] = 0;
+    ctx->fam_cnt[i] = 0;
+  }
+  return MGICP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,80 @@
+// mgicp_internal.hpp -- shared device-side layouts and kernel launchers of libmgicp.so.
+//
+// HBM layout (DESIGN.md "Data layout"): every cloud lives in a uniform grid sorted by
+// linear cell index (z-major, then y, then x; stable in the original point index), so a
+// row of cells is one contiguous range of the point array:
+//   pts        float4[n]      (x, y, z, bit_cast<float>(original index))
+//   cell_start uint32[nc + 1] exclusive prefix of per-cell counts (dense over the bbox)
+//   cov        3 x double2[n] symmetric covariance {c00,c01},{c02,c11},{c12,c22}
+// Per source point (sorted order), rewritten every outer iteration:
+//   qbuf       float4[n]      matched target xyz, w = 1 if the correspondence is accepted
+//   mahal      3 x double2[n] Mahalanobis matrix (R Cs R' + Ct)^-1, upper triangle
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstddef>
+#include <cstdint>
+
+namespace mgicp {
+
+struct GridView {
+  float ox, oy, oz;   // grid origin (bbox min)
+  float h, inv_h;     // cell edge and its reciprocal
+  float slop;         // absolute rounding slack for ring lower bounds (metres)
+  int nx, ny, nz;
+  const uint32_t* cell_start;  // nx*ny*nz + 1
+  const float4* pts;           // sorted points
+};
+
+struct Cov3 {  // SoA triple of double2 arrays
+  double2* a;  // {m00, m01}
+  double2* b;  // {m02, m11}
+  double2* c;  // {m12, m22}
+};
+
+// Number of values reduced per objective pass:
+//   [0] f-sum  [1..3] g_t sum  [4..12] Rsum (row-major)  [13] count  [14..15] pad
+constexpr int kRedVals = 16;
+constexpr int kRedThreads = 256;
+
+// Xform as 3x4 row-major float (the top three rows of an Eigen::Matrix4f).
+struct Xf34 { float m[12]; };
+struct Rot33d { double m[9]; };
+
+// ---- launchers (mgicp_kernels.hip); all asynchronous on `s` ----
+hipError_t launch_pack_points(const void* raw, size_t n, size_t stride, float4* out,
+                              hipStream_t s);
+hipError_t launch_bbox(const float4* pts, size_t n, float* partial /*nb*8*/, int nb,
+                       hipStream_t s);
+hipError_t launch_cell_hist(const float4* pts, size_t n, float ox, float oy, float oz,
+                            float inv_h, int nx, int ny, int nz, uint32_t* counts,
+                            uint32_t* keys /*nullable*/, hipStream_t s);
+hipError_t launch_count_nonzero(const uint32_t* counts, size_t nc, unsigned long long* out,
+                                hipStream_t s);
+hipError_t launch_gather_sorted(const float4* pts, const uint32_t* perm, size_t n,
+                                float4* out, hipStream_t s);
+hipError_t launch_xform_points(const float4* in, size_t n, Xf34 T, float4* out,
+                               hipStream_t s);
+hipError_t launch_knn_cov(const GridView& g, int k, double eps, size_t p0, size_t p1,
+                          Cov3 cov, hipStream_t s);
+hipError_t launch_correspond(const GridView& tgt, const Cov3& cov_t, const float4* src,
+                             const Cov3& cov_s, size_t p0, size_t p1, Xf34 T, Rot33d R,
+                             double thr, float4* qbuf, Cov3 mahal, int* dbg_nn,
+                             hipStream_t s);
+int        fdf_grid_blocks(size_t n);
+hipError_t launch_fdf(const float4* src, const float4* qbuf, const Cov3& mahal, size_t p0,
+                      size_t p1, Xf34 A, double* partial, int nb, hipStream_t s);
+hipError_t launch_fitness(const GridView& tgt, const float4* src, size_t p0, size_t p1,
+                          Xf34 T, double max_range, double* partial, int nb, hipStream_t s);
+hipError_t launch_reduce_finish(const double* partial, int nb, double* out, hipStream_t s);
+
+// radix sort / scan scratch (hipcub)
+size_t sort_scratch_bytes(size_t n, int bits);
+hipError_t launch_sort_pairs(void* scratch, size_t scratch_bytes, const uint32_t* keys_in,
+                             uint32_t* keys_out, const uint32_t* vals_in, uint32_t* vals_out,
+                             size_t n, int bits, hipStream_t s);
+size_t scan_scratch_bytes(size_t n);
+hipError_t launch_exclusive_scan(void* scratch, size_t scratch_bytes, const uint32_t* in,
+                                 uint32_t* out, size_t n, hipStream_t s);
+hipError_t launch_iota(uint32_t* v, size_t n, hipStream_t s);
+
+}  // namespace mgicp

@@ -1,0 +1,694 @@
+// mgicp_kernels.hip -- hand-written CDNA4 (gfx950, wave64) kernels of the GICP engine.
+//
+// Kernel families (DESIGN.md "Kernels"):
+//   knn_cov      exact k-NN (k = 20) over the Morton-free row-sorted uniform grid + PCL's
+//                raw-moment covariance + fp64 Jacobi SVD regularisation
+//                (PCL GICP::computeCovariances, registration/impl/gicp.hpp)
+//   correspond   T * p, radius-bounded exact 1-NN, Mahalanobis (R Cs R' + Ct)^-1
+//                (the correspondence loop of GICP::computeTransformation)
+//   fdf          one objective pass of OptimizationFunctorWithIndices::fdf:
+//                f, grad_t and Rsum in fp64, 64-lane __shfl_down + LDS block reduction,
+//                deterministic fixed-order finish
+//   fitness      Registration::getFitnessScore 1-NN mean d^2
+//
+// Numerics: the file is compiled with -ffp-contract=off (and the pragma below) so every fp32
+// expression rounds exactly like PCL's non-FMA SSE2 Eigen code and like oracle/gicp_ref.c.
+#pragma clang fp contract(off)
+
+#include "mgicp_internal.hpp"
+
+#include <hipcub/hipcub.hpp>
+
+namespace mgicp {
+
+// ------------------------------------------------------------------------------------
+// common device helpers
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ float dist2(float qx, float qy, float qz, const float4& p) {
+  // FLANN L2_Simple: ((0 + dx^2) + dy^2) + dz^2 in float, dx = query - point
+  const float dx = qx - p.x, dy = qy - p.y, dz = qz - p.z;
+  float r = dx * dx;
+  r = r + dy * dy;
+  r = r + dz * dz;
+  return r;
+}
+
+// (d2, original index) packed so that one u64 compare is the lexicographic order
+__device__ __forceinline__ unsigned long long mkkey(float d2, float w) {
+  return (static_cast<unsigned long long>(__float_as_uint(d2)) << 32) |
+         static_cast<unsigned long long>(__float_as_uint(w));
+}
+
+// Eigen Matrix4f * Vector4f (w = 1): ((c0 x + c1 y) + c2 z) + c3
+__device__ __forceinline__ void xform(const Xf34& T, float x, float y, float z, float& ox,
+                                      float& oy, float& oz) {
+  float a = T.m[0] * x;
+  a = a + T.m[1] * y;
+  a = a + T.m[2] * z;
+  ox = a + T.m[3];
+  float b = T.m[4] * x;
+  b = b + T.m[5] * y;
+  b = b + T.m[6] * z;
+  oy = b + T.m[7];
+  float c = T.m[8] * x;
+  c = c + T.m[9] * y;
+  c = c + T.m[10] * z;
+  oz = c + T.m[11];
+}
+
+__device__ __forceinline__ int qcell(float v, float o, float inv_h) {
+  float f = floorf((v - o) * inv_h);
+  f = fminf(fmaxf(f, -1048576.f), 1048576.f);
+  return static_cast<int>(f);
+}
+
+__device__ __forceinline__ int bcell(float v, float o, float inv_h, int n) {
+  int c = qcell(v, o, inv_h);
+  return c < 0 ? 0 : (c > n - 1 ? n - 1 : c);
+}
+
+// distance from q to the nearest face of the cell box [c-r, c+r] beyond which grid cells
+// remain unvisited along this axis (INF when none remain)
+__device__ __forceinline__ float axis_bound(float q, float o, float h, int c, int r, int n) {
+  const float dlo = (c - r > 0) ? q - (o + static_cast<float>(c - r) * h) : INFINITY;
+  const float dhi = (c + r < n - 1) ? (o + static_cast<float>(c + r + 1) * h) - q : INFINITY;
+  return fminf(dlo, dhi);
+}
+
+__device__ __forceinline__ int dist_out(int c, int n) {
+  return c < 0 ? -c : (c > n - 1 ? c - (n - 1) : 0);
+}
+
+// Visit grid rings (Chebyshev shells of cells) around q in increasing order until the
+// visitor proves that no unvisited point can enter its result.  A ring's rows of cells
+// are contiguous ranges of the sorted point array.
+template <class V>
+__device__ __forceinline__ void ring_search(const GridView& g, float qx, float qy, float qz,
+                                            V& vis) {
+  const int cx = qcell(qx, g.ox, g.inv_h), cy = qcell(qy, g.oy, g.inv_h),
+            cz = qcell(qz, g.oz, g.inv_h);
+  const int rmin = max(max(dist_out(cx, g.nx), dist_out(cy, g.ny)), dist_out(cz, g.nz));
+  for (int r = rmin; r < (1 << 22); ++r) {
+    if (r > 0) {
+      const float L = fminf(fminf(axis_bound(qx, g.ox, g.h, cx, r - 1, g.nx),
+                                  axis_bound(qy, g.oy, g.h, cy, r - 1, g.ny)),
+                            axis_bound(qz, g.oz, g.h, cz, r - 1, g.nz));
+      if (L == INFINITY) return;  // every cell visited
+      const float Ls = L * 0.99999f - g.slop;
+      if (vis.done(Ls)) return;
+    }
+    const int x0 = cx - r, x1 = cx + r, y0 = cy - r, y1 = cy + r, z0 = cz - r, z1 = cz + r;
+    const int xlo = max(x0, 0), xhi = min(x1, g.nx - 1);
+    const int ylo = max(y0, 0), yhi = min(y1, g.ny - 1);
+    const int zlo = max(z0, 0), zhi = min(z1, g.nz - 1);
+    for (int z = zlo; z <= zhi; ++z) {
+      const bool zf = (z == z0) || (z == z1);
+      for (int y = ylo; y <= yhi; ++y) {
+        const uint32_t* row = g.cell_start + (static_cast<size_t>(z) * g.ny + y) * g.nx;
+        if (zf || y == y0 || y == y1) {
+          if (xlo <= xhi) vis.range(g, row[xlo], row[xhi + 1]);
+        } else {
+          if (x0 >= 0) vis.range(g, row[x0], row[x0 + 1]);
+          if (x1 < g.nx) vis.range(g, row[x1], row[x1 + 1]);
+        }
+      }
+    }
+  }
+}
+
+// exact k-NN visitor: register-resident sorted list of (d2, index) keys
+template <int K>
+struct KnnVisitor {
+  float qx, qy, qz;
+  unsigned long long key[K];
+  uint32_t pos[K];
+
+  __device__ __forceinline__ void init(float x, float y, float z) {
+    qx = x; qy = y; qz = z;
+#pragma unroll
+    for (int k = 0; k < K; ++k) { key[k] = ~0ull; pos[k] = 0u; }
+  }
+  __device__ __forceinline__ bool done(float Ls) const {
+    if (key[K - 1] == ~0ull || !(Ls > 0.f)) return false;
+    return __uint_as_float(static_cast<uint32_t>(key[K - 1] >> 32)) < Ls * Ls;
+  }
+  __device__ __forceinline__ void insert(unsigned long long c, uint32_t cp) {
+#pragma unroll
+    for (int k = K - 1; k > 0; --k) {
+      const bool sh = c < key[k - 1];
+      const bool here = !sh && c < key[k];
+      const unsigned long long nk = sh ? key[k - 1] : (here ? c : key[k]);
+      const uint32_t np = sh ? pos[k - 1] : (here ? cp : pos[k]);
+      key[k] = nk;
+      pos[k] = np;
+    }
+    if (c < key[0]) { key[0] = c; pos[0] = cp; }
+  }
+  __device__ __forceinline__ void range(const GridView& g, uint32_t a, uint32_t b) {
+    for (uint32_t j = a; j < b; ++j) {
+      const float4 p = g.pts[j];
+      const unsigned long long c = mkkey(dist2(qx, qy, qz, p), p.w);
+      if (c < key[K - 1]) insert(c, j);
+    }
+  }
+};
+
+// exact 1-NN visitor, optionally bounded by an acceptance threshold thr on d2
+struct NnVisitor {
+  float qx, qy, qz;
+  double thr;
+  unsigned long long best;
+  uint32_t pos;
+
+  __device__ __forceinline__ void init(float x, float y, float z, double t) {
+    qx = x; qy = y; qz = z; thr = t; best = ~0ull; pos = 0u;
+  }
+  __device__ __forceinline__ bool done(float Ls) const {
+    if (!(Ls > 0.f)) return false;
+    if (static_cast<double>(Ls) * static_cast<double>(Ls) >= thr) return true;
+    if (best == ~0ull) return false;
+    return __uint_as_float(static_cast<uint32_t>(best >> 32)) < Ls * Ls;
+  }
+  __device__ __forceinline__ void range(const GridView& g, uint32_t a, uint32_t b) {
+    for (uint32_t j = a; j < b; ++j) {
+      const float4 p = g.pts[j];
+      const unsigned long long c = mkkey(dist2(qx, qy, qz, p), p.w);
+      if (c < best) { best = c; pos = j; }
+    }
+  }
+};
+
+// ------------------------------------------------------------------------------------
+// grid build
+// ------------------------------------------------------------------------------------
+__global__ void pack_points_kernel(const unsigned char* raw, size_t n, size_t stride,
+                                   float4* out) {
+  const size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float* p = reinterpret_cast<const float*>(raw + i * stride);
+  out[i] = make_float4(p[0], p[1], p[2], __uint_as_float(static_cast<uint32_t>(i)));
+}
+
+__global__ __launch_bounds__(256) void bbox_kernel(const float4* pts, size_t n, float* partial) {
+  float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+  float bad = 0.f;
+  for (size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<size_t>(gridDim.x) * blockDim.x) {
+    const float4 p = pts[i];
+    if (!isfinite(p.x) || !isfinite(p.y) || !isfinite(p.z)) { bad += 1.f; continue; }
+    mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
+    mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
+  }
+  __shared__ float sm[7][256];
+  for (int d = 0; d < 3; ++d) { sm[d][threadIdx.x] = mn[d]; sm[3 + d][threadIdx.x] = mx[d]; }
+  sm[6][threadIdx.x] = bad;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      for (int d = 0; d < 3; ++d) {
+        sm[d][threadIdx.x] = fminf(sm[d][threadIdx.x], sm[d][threadIdx.x + s]);
+        sm[3 + d][threadIdx.x] = fmaxf(sm[3 + d][threadIdx.x], sm[3 + d][threadIdx.x + s]);
+      }
+      sm[6][threadIdx.x] += sm[6][threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < 7) partial[blockIdx.x * 8 + threadIdx.x] = sm[threadIdx.x][0];
+}
+
+__global__ void cell_hist_kernel(const float4* pts, size_t n, float ox, float oy, float oz,
+                                 float inv_h, int nx, int ny, int nz, uint32_t* counts,
+                                 uint32_t* keys) {
+  const size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float4 p = pts[i];
+  const uint32_t cx = bcell(p.x, ox, inv_h, nx), cy = bcell(p.y, oy, inv_h, ny),
+                 cz = bcell(p.z, oz, inv_h, nz);
+  const uint32_t lin = cx + static_cast<uint32_t>(nx) * (cy + static_cast<uint32_t>(ny) * cz);
+  atomicAdd(&counts[lin], 1u);
+  if (keys) keys[i] = lin;
+}
+
+__global__ __launch_bounds__(256) void count_nonzero_kernel(const uint32_t* c, size_t n,
+                                                            unsigned long long* out) {
+  unsigned long long cnt = 0;
+  for (size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<size_t>(gridDim.x) * blockDim.x)
+    cnt += (c[i] != 0u);
+  for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off);
+  __shared__ unsigned long long sm[4];
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(out, sm[0] + sm[1] + sm[2] + sm[3]);
+}
+
+__global__ void gather_sorted_kernel(const float4* pts, const uint32_t* perm, size_t n,
+                                     float4* out) {
+  const size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  out[i] = pts[perm[i]];
+}
+
+__global__ void xform_points_kernel(const float4* in, size_t n, Xf34 T, float4* out) {
+  const size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float4 p = in[i];
+  float x, y, z;
+  xform(T, p.x, p.y, p.z, x, y, z);
+  out[i] = make_float4(x, y, z, p.w);
+}
+
+__global__ void iota_kernel(uint32_t* v, size_t n) {
+  const size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < n) v[i] = static_cast<uint32_t>(i);
+}
+
+// ------------------------------------------------------------------------------------
+// covariance: exact kNN + PCL raw moments + fp64 Jacobi (bit-identical to the oracle)
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ void jacobi3(double a[3][3], double v[3][3]) {
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) v[r][c] = (r == c) ? 1.0 : 0.0;
+  for (int sweep = 0; sweep < 50; ++sweep) {
+    bool rotated = false;
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+      const int p = (e == 2) ? 1 : 0, q = (e == 0) ? 1 : 2, o = 3 - p - q;
+      const double apq = a[p][q];
+      const double app = a[p][p], aqq = a[q][q];
+      if (fabs(apq) <= 1e-18 * (fabs(app) + fabs(aqq))) {
+        a[p][q] = a[q][p] = 0.0;
+        continue;
+      }
+      rotated = true;
+      const double theta = (aqq - app) / (2.0 * apq);
+      double t;
+      if (fabs(theta) > 1e150) t = 0.5 / theta;
+      else t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+      const double c = 1.0 / sqrt(t * t + 1.0);
+      const double s = t * c;
+      a[p][p] = app - t * apq;
+      a[q][q] = aqq + t * apq;
+      a[p][q] = a[q][p] = 0.0;
+      const double aop = a[o][p], aoq = a[o][q];
+      a[o][p] = a[p][o] = c * aop - s * aoq;
+      a[o][q] = a[q][o] = s * aop + c * aoq;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const double vp = v[r][p], vq = v[r][q];
+        v[r][p] = c * vp - s * vq;
+        v[r][q] = s * vp + c * vq;
+      }
+    }
+    if (!rotated) break;
+  }
+}
+
+__device__ __forceinline__ double sel3(int i, double a, double b, double c) {
+  return i == 0 ? a : (i == 1 ? b : c);
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void knn_cov_kernel(GridView g, double eps, size_t p0,
+                                                      size_t p1, Cov3 cov) {
+  const size_t p = p0 + static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (p >= p1) return;
+  const float4 q = g.pts[p];
+  KnnVisitor<K> vis;
+  vis.init(q.x, q.y, q.z);
+  ring_search(g, q.x, q.y, q.z, vis);
+
+  double m0 = 0.0, m1 = 0.0, m2 = 0.0;
+  double a[3][3] = {{0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}};
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const float4 pt = g.pts[vis.pos[k]];
+    m0 += pt.x;
+    m1 += pt.y;
+    m2 += pt.z;
+    a[0][0] += static_cast<double>(pt.x * pt.x);
+    a[1][0] += static_cast<double>(pt.y * pt.x);
+    a[1][1] += static_cast<double>(pt.y * pt.y);
+    a[2][0] += static_cast<double>(pt.z * pt.x);
+    a[2][1] += static_cast<double>(pt.z * pt.y);
+    a[2][2] += static_cast<double>(pt.z * pt.z);
+  }
+  const double kd = static_cast<double>(K);
+  double mean[3] = {m0 / kd, m1 / kd, m2 / kd};
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j <= i; ++j) {
+      a[i][j] /= kd;
+      a[i][j] -= mean[i] * mean[j];
+      a[j][i] = a[i][j];
+    }
+  double v[3][3];
+  jacobi3(a, v);
+  const double sv0 = fabs(a[0][0]), sv1 = fabs(a[1][1]), sv2 = fabs(a[2][2]);
+  int ord[3] = {0, 1, 2};
+  // descending selection sort, no swap on ties (identical to the oracle)
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = i + 1; j < 3; ++j) {
+      const double sj = sel3(ord[j], sv0, sv1, sv2), si = sel3(ord[i], sv0, sv1, sv2);
+      if (sj > si) { const int t = ord[i]; ord[i] = ord[j]; ord[j] = t; }
+    }
+  double C00 = 0.0, C01 = 0.0, C02 = 0.0, C11 = 0.0, C12 = 0.0, C22 = 0.0;
+#pragma unroll
+  for (int kk = 0; kk < 3; ++kk) {
+    const int col = ord[kk];
+    const double w = (kk == 2) ? eps : 1.0;
+    const double v0 = sel3(col, v[0][0], v[0][1], v[0][2]);
+    const double v1 = sel3(col, v[1][0], v[1][1], v[1][2]);
+    const double v2 = sel3(col, v[2][0], v[2][1], v[2][2]);
+    const double u0 = w * v0, u1 = w * v1, u2 = w * v2;
+    C00 += u0 * v0;
+    C01 += u0 * v1;
+    C02 += u0 * v2;
+    C11 += u1 * v1;
+    C12 += u1 * v2;
+    C22 += u2 * v2;
+  }
+  cov.a[p] = make_double2(C00, C01);
+  cov.b[p] = make_double2(C02, C11);
+  cov.c[p] = make_double2(C12, C22);
+}
+
+// ------------------------------------------------------------------------------------
+// correspondence + Mahalanobis
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ void load_cov(const Cov3& c, size_t i, double M[3][3]) {
+  const double2 a = c.a[i], b = c.b[i], d = c.c[i];
+  M[0][0] = a.x; M[0][1] = a.y; M[0][2] = b.x;
+  M[1][0] = a.y; M[1][1] = b.y; M[1][2] = d.x;
+  M[2][0] = b.x; M[2][1] = d.x; M[2][2] = d.y;
+}
+
+__global__ __launch_bounds__(256) void correspond_kernel(GridView tg, Cov3 cov_t,
+                                                         const float4* __restrict__ src,
+                                                         Cov3 cov_s, size_t p0, size_t p1,
+                                                         Xf34 T, Rot33d R, double thr,
+                                                         float4* __restrict__ qbuf, Cov3 mahal,
+                                                         int* dbg_nn) {
+  const size_t p = p0 + static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (p >= p1) return;
+  const float4 s = src[p];
+  float qx, qy, qz;
+  xform(T, s.x, s.y, s.z, qx, qy, qz);
+  NnVisitor vis;
+  vis.init(qx, qy, qz, thr);
+  ring_search(tg, qx, qy, qz, vis);
+  const bool ok = vis.best != ~0ull &&
+                  static_cast<double>(__uint_as_float(static_cast<uint32_t>(vis.best >> 32))) < thr;
+  if (!ok) {
+    qbuf[p] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (dbg_nn) {
+      dbg_nn[p] = -1;
+      mahal.a[p] = make_double2(0.0, 0.0);
+      mahal.b[p] = make_double2(0.0, 0.0);
+      mahal.c[p] = make_double2(0.0, 0.0);
+    }
+    return;
+  }
+  const float4 t = tg.pts[vis.pos];
+  double C1[3][3], C2[3][3], RC[3][3], tm[3][3];
+  load_cov(cov_s, p, C1);
+  load_cov(cov_t, vis.pos, C2);
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      double a = R.m[3 * i + 0] * C1[0][j];
+      a = a + R.m[3 * i + 1] * C1[1][j];
+      a = a + R.m[3 * i + 2] * C1[2][j];
+      RC[i][j] = a;
+    }
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      double a = RC[i][0] * R.m[3 * j + 0];
+      a = a + RC[i][1] * R.m[3 * j + 1];
+      a = a + RC[i][2] * R.m[3 * j + 2];
+      tm[i][j] = a + C2[i][j];
+    }
+#define COF(i, j) (tm[((i) + 1) % 3][((j) + 1) % 3] * tm[((i) + 2) % 3][((j) + 2) % 3] - \
+                   tm[((i) + 1) % 3][((j) + 2) % 3] * tm[((i) + 2) % 3][((j) + 1) % 3])
+  const double c00 = COF(0, 0), c10 = COF(1, 0), c20 = COF(2, 0);
+  double det = c00 * tm[0][0];
+  det = det + c10 * tm[1][0];
+  det = det + c20 * tm[2][0];
+  const double inv = 1.0 / det;
+  // Eigen: result(i, j) = cofactor(j, i) / det; keep the upper triangle
+  const double m00 = c00 * inv, m01 = c10 * inv, m02 = c20 * inv;
+  const double m11 = COF(1, 1) * inv, m12 = COF(2, 1) * inv, m22 = COF(2, 2) * inv;
+#undef COF
+  qbuf[p] = make_float4(t.x, t.y, t.z, 1.f);
+  mahal.a[p] = make_double2(m00, m01);
+  mahal.b[p] = make_double2(m02, m11);
+  mahal.c[p] = make_double2(m12, m22);
+  if (dbg_nn) dbg_nn[p] = static_cast<int>(__float_as_uint(t.w));
+}
+
+// ------------------------------------------------------------------------------------
+// objective pass (fdf) and reductions
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  return v;
+}
+
+// reduce kRedVals doubles across a 256-thread block; thread 0 writes dst[0..15]
+__device__ __forceinline__ void block_reduce_store(double (&acc)[kRedVals], double* dst) {
+  __shared__ double sm[4][kRedVals];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int v = 0; v < kRedVals; ++v) {
+    const double w = wave_sum(acc[v]);
+    if (lane == 0) sm[wid][v] = w;
+  }
+  __syncthreads();
+  if (threadIdx.x < kRedVals) {
+    const int v = threadIdx.x;
+    double s = sm[0][v];
+    s = s + sm[1][v];
+    s = s + sm[2][v];
+    s = s + sm[3][v];
+    dst[v] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void fdf_kernel(const float4* __restrict__ src,
+                                                  const float4* __restrict__ qbuf, Cov3 mahal,
+                                                  size_t p0, size_t p1, Xf34 A,
+                                                  double* __restrict__ partial) {
+  double acc[kRedVals];
+#pragma unroll
+  for (int v = 0; v < kRedVals; ++v) acc[v] = 0.0;
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  for (size_t p = p0 + static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; p < p1;
+       p += stride) {
+    const float4 q = qbuf[p];
+    if (q.w == 0.f) continue;
+    const float4 s = src[p];
+    const double2 ma = mahal.a[p], mb = mahal.b[p], mc = mahal.c[p];
+    float px, py, pz;
+    xform(A, s.x, s.y, s.z, px, py, pz);
+    const double r0 = static_cast<double>(px - q.x);
+    const double r1 = static_cast<double>(py - q.y);
+    const double r2 = static_cast<double>(pz - q.z);
+    const double m00 = ma.x, m01 = ma.y, m02 = mb.x, m11 = mb.y, m12 = mc.x, m22 = mc.y;
+    double t0 = m00 * r0; t0 = t0 + m01 * r1; t0 = t0 + m02 * r2;
+    double t1 = m01 * r0; t1 = t1 + m11 * r1; t1 = t1 + m12 * r2;
+    double t2 = m02 * r0; t2 = t2 + m12 * r1; t2 = t2 + m22 * r2;
+    double d = r0 * t0; d = d + r1 * t1; d = d + r2 * t2;
+    const double sx = s.x, sy = s.y, sz = s.z;
+    acc[0] += d;
+    acc[1] += t0; acc[2] += t1; acc[3] += t2;
+    acc[4] += sx * t0; acc[5] += sx * t1; acc[6] += sx * t2;
+    acc[7] += sy * t0; acc[8] += sy * t1; acc[9] += sy * t2;
+    acc[10] += sz * t0; acc[11] += sz * t1; acc[12] += sz * t2;
+    acc[13] += 1.0;
+  }
+  block_reduce_store(acc, partial + static_cast<size_t>(blockIdx.x) * kRedVals);
+}
+
+__global__ __launch_bounds__(256) void fitness_kernel(GridView tg, const float4* __restrict__ src,
+                                                      size_t p0, size_t p1, Xf34 T,
+                                                      double max_range,
+                                                      double* __restrict__ partial) {
+  double acc[kRedVals];
+#pragma unroll
+  for (int v = 0; v < kRedVals; ++v) acc[v] = 0.0;
+  const size_t p = p0 + static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (p < p1) {
+    const float4 s = src[p];
+    float qx, qy, qz;
+    xform(T, s.x, s.y, s.z, qx, qy, qz);
+    NnVisitor vis;
+    vis.init(qx, qy, qz, INFINITY);
+    ring_search(tg, qx, qy, qz, vis);
+    if (vis.best != ~0ull) {
+      const float d2 = __uint_as_float(static_cast<uint32_t>(vis.best >> 32));
+      if (static_cast<double>(d2) <= max_range) {
+        acc[0] = d2;
+        acc[13] = 1.0;
+      }
+    }
+  }
+  block_reduce_store(acc, partial + static_cast<size_t>(blockIdx.x) * kRedVals);
+}
+
+__global__ __launch_bounds__(256) void reduce_finish_kernel(const double* __restrict__ partial,
+                                                            int nb, double* __restrict__ out) {
+  double acc[kRedVals];
+#pragma unroll
+  for (int v = 0; v < kRedVals; ++v) acc[v] = 0.0;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+#pragma unroll
+    for (int v = 0; v < kRedVals; ++v) acc[v] += partial[static_cast<size_t>(b) * kRedVals + v];
+  }
+  block_reduce_store(acc, out);
+}
+
+// ------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------
+static inline unsigned nblk(size_t n, unsigned t = 256) {
+  return static_cast<unsigned>((n + t - 1) / t);
+}
+
+hipError_t launch_pack_points(const void* raw, size_t n, size_t stride, float4* out,
+                              hipStream_t s) {
+  if (!n) return hipSuccess;
+  pack_points_kernel<<<nblk(n), 256, 0, s>>>(static_cast<const unsigned char*>(raw), n, stride,
+                                             out);
+  return hipGetLastError();
+}
+
+hipError_t launch_bbox(const float4* pts, size_t n, float* partial, int nb, hipStream_t s) {
+  bbox_kernel<<<nb, 256, 0, s>>>(pts, n, partial);
+  return hipGetLastError();
+}
+
+hipError_t launch_cell_hist(const float4* pts, size_t n, float ox, float oy, float oz,
+                            float inv_h, int nx, int ny, int nz, uint32_t* counts,
+                            uint32_t* keys, hipStream_t s) {
+  if (!n) return hipSuccess;
+  cell_hist_kernel<<<nblk(n), 256, 0, s>>>(pts, n, ox, oy, oz, inv_h, nx, ny, nz, counts, keys);
+  return hipGetLastError();
+}
+
+hipError_t launch_count_nonzero(const uint32_t* counts, size_t nc, unsigned long long* out,
+                                hipStream_t s) {
+  const unsigned nb = static_cast<unsigned>(std::min<size_t>(nblk(nc), 4096));
+  count_nonzero_kernel<<<nb, 256, 0, s>>>(counts, nc, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_sorted(const float4* pts, const uint32_t* perm, size_t n, float4* out,
+                                hipStream_t s) {
+  if (!n) return hipSuccess;
+  gather_sorted_kernel<<<nblk(n), 256, 0, s>>>(pts, perm, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_xform_points(const float4* in, size_t n, Xf34 T, float4* out, hipStream_t s) {
+  if (!n) return hipSuccess;
+  xform_points_kernel<<<nblk(n), 256, 0, s>>>(in, n, T, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_iota(uint32_t* v, size_t n, hipStream_t s) {
+  if (!n) return hipSuccess;
+  iota_kernel<<<nblk(n), 256, 0, s>>>(v, n);
+  return hipGetLastError();
+}
+
+template <int K>
+static hipError_t knn_cov_k(const GridView& g, double eps, size_t p0, size_t p1, Cov3 cov,
+                            hipStream_t s) {
+  knn_cov_kernel<K><<<nblk(p1 - p0), 256, 0, s>>>(g, eps, p0, p1, cov);
+  return hipGetLastError();
+}
+
+hipError_t launch_knn_cov(const GridView& g, int k, double eps, size_t p0, size_t p1, Cov3 cov,
+                          hipStream_t s) {
+  if (p1 <= p0) return hipSuccess;
+  switch (k) {
+    case 5: return knn_cov_k<5>(g, eps, p0, p1, cov, s);
+    case 10: return knn_cov_k<10>(g, eps, p0, p1, cov, s);
+    case 15: return knn_cov_k<15>(g, eps, p0, p1, cov, s);
+    case 20: return knn_cov_k<20>(g, eps, p0, p1, cov, s);
+    case 25: return knn_cov_k<25>(g, eps, p0, p1, cov, s);
+    case 30: return knn_cov_k<30>(g, eps, p0, p1, cov, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_correspond(const GridView& tgt, const Cov3& cov_t, const float4* src,
+                             const Cov3& cov_s, size_t p0, size_t p1, Xf34 T, Rot33d R,
+                             double thr, float4* qbuf, Cov3 mahal, int* dbg_nn, hipStream_t s) {
+  if (p1 <= p0) return hipSuccess;
+  correspond_kernel<<<nblk(p1 - p0), 256, 0, s>>>(tgt, cov_t, src, cov_s, p0, p1, T, R, thr,
+                                                  qbuf, mahal, dbg_nn);
+  return hipGetLastError();
+}
+
+int fdf_grid_blocks(size_t n) {
+  // ~8 points per thread keeps >= 8 waves per CU resident on 256 CUs at 5M points
+  const size_t want = (n + 256 * 8 - 1) / (256 * 8);
+  return static_cast<int>(std::max<size_t>(1, std::min<size_t>(want, 2048)));
+}
+
+hipError_t launch_fdf(const float4* src, const float4* qbuf, const Cov3& mahal, size_t p0,
+                      size_t p1, Xf34 A, double* partial, int nb, hipStream_t s) {
+  fdf_kernel<<<nb, 256, 0, s>>>(src, qbuf, mahal, p0, p1, A, partial);
+  return hipGetLastError();
+}
+
+hipError_t launch_fitness(const GridView& tgt, const float4* src, size_t p0, size_t p1, Xf34 T,
+                          double max_range, double* partial, int nb, hipStream_t s) {
+  fitness_kernel<<<nb, 256, 0, s>>>(tgt, src, p0, p1, T, max_range, partial);
+  return hipGetLastError();
+}
+
+hipError_t launch_reduce_finish(const double* partial, int nb, double* out, hipStream_t s) {
+  reduce_finish_kernel<<<1, kRedThreads, 0, s>>>(partial, nb, out);
+  return hipGetLastError();
+}
+
+size_t sort_scratch_bytes(size_t n, int bits) {
+  size_t bytes = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, static_cast<const uint32_t*>(nullptr),
+                                     static_cast<uint32_t*>(nullptr),
+                                     static_cast<const uint32_t*>(nullptr),
+                                     static_cast<uint32_t*>(nullptr), static_cast<int>(n), 0, bits);
+  return bytes;
+}
+
+hipError_t launch_sort_pairs(void* scratch, size_t scratch_bytes, const uint32_t* keys_in,
+                             uint32_t* keys_out, const uint32_t* vals_in, uint32_t* vals_out,
+                             size_t n, int bits, hipStream_t s) {
+  return hipcub::DeviceRadixSort::SortPairs(scratch, scratch_bytes, keys_in, keys_out, vals_in,
+                                            vals_out, static_cast<int>(n), 0, bits, s);
+}
+
+size_t scan_scratch_bytes(size_t n) {
+  size_t bytes = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, static_cast<const uint32_t*>(nullptr),
+                                   static_cast<uint32_t*>(nullptr), static_cast<int>(n));
+  return bytes;
+}
+
+hipError_t launch_exclusive_scan(void* scratch, size_t scratch_bytes, const uint32_t* in,
+                                 uint32_t* out, size_t n, hipStream_t s) {
+  return hipcub::DeviceScan::ExclusiveSum(scratch, scratch_bytes, in, out, static_cast<int>(n), s);
+}
+
+}  // namespace mgicp

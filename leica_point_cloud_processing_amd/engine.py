@@ -1,0 +1,220 @@
+"""GICPEngine: the MI355X GICP behind pcl::GeneralizedIterativeClosestPoint's API surface.
+
+Mirrors the subset of pcl::GeneralizedIterativeClosestPoint<PointXYZRGB,PointXYZRGB> that
+GICPAlignment uses (/root/reference/src/GICPAlignment.cpp:48-54, 89-105, 116-123):
+setMaximumIterations, setMaxCorrespondenceDistance, setTransformationEpsilon,
+setRANSACOutlierRejectionThreshold (stored, unused by GICP), setInputSource, setInputTarget,
+align, hasConverged, getFinalTransformation, getFitnessScore, getMaximumIterations.
+All compute goes through libmgicp.so (include/mi355x_gicp.h); nothing runs on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .cloud import PointCloudRGB
+
+DBL_MAX = float(np.finfo(np.float64).max)
+
+
+def _cm(T) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(T, dtype=np.float32).T).reshape(16)
+
+
+def _from_cm(buf) -> np.ndarray:
+    return np.asarray(buf, dtype=np.float32).reshape(4, 4).T.copy()
+
+
+def _fp(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+def _dp(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+class GICPEngine:
+    def __init__(self, device: int = -1, **params):
+        self._lib = _lib.load()
+        self.params = _lib.default_params()
+        self.params.device = device
+        for k, v in params.items():
+            setattr(self.params, k, v)
+        h = ctypes.c_void_p()
+        rc = self._lib.mgicp_create(ctypes.byref(h), ctypes.byref(self.params))
+        if rc != 0:
+            raise _lib.MgicpError(rc, "mgicp_create failed (no HIP device or invalid parameters)")
+        self._h = h
+        self.ransac_outlier_threshold = 0.05
+        self._input = None
+        self._converged = False
+        self._final = np.eye(4, dtype=np.float32)
+        self.last_result = None
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.mgicp_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    # -- helpers -------------------------------------------------------------------------
+    def _check(self, rc: int, what: str):
+        if rc < 0:
+            raise _lib.MgicpError(rc, f"{what}: {self._lib.mgicp_last_error(self._h).decode()}")
+        return rc
+
+    def _push_params(self):
+        self._check(self._lib.mgicp_set_params(self._h, ctypes.byref(self.params)), "mgicp_set_params")
+
+    # -- pcl::Registration setters -----------------------------------------------------------
+    def setMaximumIterations(self, n: int):
+        self.params.max_iter = int(n)
+        self._push_params()
+
+    def getMaximumIterations(self) -> int:
+        return int(self.params.max_iter)
+
+    def setMaxCorrespondenceDistance(self, d: float):
+        self.params.max_corr_dist = float(d)
+        self._push_params()
+
+    def setTransformationEpsilon(self, eps: float):
+        self.params.tf_eps = float(eps)
+        self._push_params()
+
+    def setRotationEpsilon(self, eps: float):
+        self.params.rot_eps = float(eps)
+        self._push_params()
+
+    def setRANSACOutlierRejectionThreshold(self, th: float):
+        self.ransac_outlier_threshold = float(th)  # stored; GICP never uses it (PCL 1.8.1)
+
+    def setInputSource(self, cloud):
+        self._input = cloud
+        ptr, n, stride = self._cloud_arg(cloud)
+        self._check(self._lib.mgicp_set_source(self._h, ptr, n, stride), "setInputSource")
+
+    def setInputTarget(self, cloud):
+        ptr, n, stride = self._cloud_arg(cloud)
+        self._check(self._lib.mgicp_set_target(self._h, ptr, n, stride), "setInputTarget")
+
+    @staticmethod
+    def _cloud_arg(cloud):
+        if isinstance(cloud, PointCloudRGB):
+            return cloud.ctypes_xyz()
+        a = np.ascontiguousarray(cloud, dtype=np.float32).reshape(-1, 3)
+        return a.ctypes.data, len(a), 12
+
+    def set_source_xyz(self, xyz):
+        self._src_keep = np.ascontiguousarray(xyz, dtype=np.float32).reshape(-1, 3)
+        self._input = None
+        self._check(self._lib.mgicp_set_source(self._h, self._src_keep.ctypes.data, len(self._src_keep), 12),
+                    "set_source")
+
+    def set_target_xyz(self, xyz):
+        self._tgt_keep = np.ascontiguousarray(xyz, dtype=np.float32).reshape(-1, 3)
+        self._check(self._lib.mgicp_set_target(self._h, self._tgt_keep.ctypes.data, len(self._tgt_keep), 12),
+                    "set_target")
+
+    def set_source_device(self, ptr: int, n: int, stride: int):
+        self._input = None
+        self._check(self._lib.mgicp_set_source_device(self._h, ctypes.c_void_p(ptr), n, stride), "set_source_device")
+
+    def set_target_device(self, ptr: int, n: int, stride: int):
+        self._check(self._lib.mgicp_set_target_device(self._h, ctypes.c_void_p(ptr), n, stride), "set_target_device")
+
+    # -- the hot path ----------------------------------------------------------------------
+    def align(self, output: PointCloudRGB | None = None, guess=None) -> np.ndarray:
+        """Registration::align(output, guess).  Returns getFinalTransformation()."""
+        g = _cm(guess) if guess is not None else None
+        out = np.zeros(16, np.float32)
+        res = _lib.MgicpResult()
+        rc = self._lib.mgicp_align(self._h, _fp(g) if g is not None else None, _fp(out), ctypes.byref(res))
+        self.last_result = {k: getattr(res, k) for k, _ in _lib.MgicpResult._fields_}
+        if rc == _lib.MGICP_E_SOLVER:
+            self._converged = False  # PCL catches the solver exception; converged_ stays false
+        else:
+            self._check(rc, "align")
+            self._converged = bool(res.converged)
+        self._final = _from_cm(out)
+        if output is not None and self._input is not None:
+            # output = transformPointCloud(*input_, output, final_transformation_)
+            output.copy_from(self._input)
+            self.transform_source_into(self._final, output)
+        return self._final
+
+    def hasConverged(self) -> bool:
+        return self._converged
+
+    def getFinalTransformation(self) -> np.ndarray:
+        return self._final.copy()
+
+    def getFitnessScore(self, max_range: float = DBL_MAX) -> float:
+        out = ctypes.c_double()
+        self._check(self._lib.mgicp_fitness(self._h, _fp(_cm(self._final)), max_range, ctypes.byref(out)),
+                    "getFitnessScore")
+        return out.value
+
+    def fitness(self, T, max_range: float = DBL_MAX) -> float:
+        out = ctypes.c_double()
+        self._check(self._lib.mgicp_fitness(self._h, _fp(_cm(T)), max_range, ctypes.byref(out)), "fitness")
+        return out.value
+
+    def transform_source_into(self, T, cloud: PointCloudRGB):
+        """xyz of `cloud` := T * source (device kernel; `cloud` must have the source's size)."""
+        ptr, n, stride = cloud.ctypes_xyz()
+        self._check(self._lib.mgicp_transform_source(self._h, _fp(_cm(T)), ctypes.c_void_p(ptr), stride),
+                    "transform_source")
+
+    # -- multi-GPU ------------------------------------------------------------------------
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = ctypes.create_string_buffer(128)
+        rc = _lib.load().mgicp_get_unique_id(buf)
+        if rc != 0:
+            raise _lib.MgicpError(rc, "mgicp_get_unique_id")
+        return buf.raw
+
+    def comm_init(self, nranks: int, rank: int, uid: bytes | None):
+        buf = ctypes.create_string_buffer(uid, 128) if uid is not None else None
+        self._check(self._lib.mgicp_comm_init(self._h, nranks, rank, buf), "comm_init")
+
+    # -- introspection (parity tests, profiling) ----------------------------------------------
+    def debug_covariances(self, which: str, n: int) -> np.ndarray:
+        out = np.zeros((n, 6), np.float64)
+        self._check(self._lib.mgicp_debug_covariances(self._h, 0 if which == "source" else 1, _dp(out)),
+                    "debug_covariances")
+        return out
+
+    def debug_correspondences(self, T, n: int):
+        tgt = np.full(n, -1, np.int32)
+        M = np.zeros((n, 6), np.float64)
+        m = self._check(self._lib.mgicp_debug_correspondences(
+            self._h, _fp(_cm(T)), tgt.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), _dp(M)), "debug_correspondences")
+        return m, tgt, M
+
+    def debug_fdf(self, x):
+        x = np.asarray(x, np.float64)
+        f = ctypes.c_double()
+        g = np.zeros(6, np.float64)
+        self._check(self._lib.mgicp_debug_fdf(self._h, _dp(x), ctypes.byref(f), _dp(g)), "debug_fdf")
+        return f.value, g
+
+    def debug_trace(self, max_iters: int = 1000):
+        buf = np.zeros(16 * max_iters, np.float32)
+        n = self._check(self._lib.mgicp_debug_trace(self._h, _fp(buf), max_iters), "debug_trace")
+        return [_from_cm(buf[16 * i:16 * i + 16]) for i in range(min(n, max_iters))]
+
+    def set_profiling(self, on: bool):
+        self._check(self._lib.mgicp_set_profiling(self._h, int(on)), "set_profiling")
+
+    def kernel_times(self):
+        ms = np.zeros(4, np.float64)
+        cnt = np.zeros(4, np.int32)
+        self._check(self._lib.mgicp_debug_kernel_times(self._h, _dp(ms), cnt.ctypes.data_as(ctypes.POINTER(ctypes.c_int))),
+                    "kernel_times")
+        names = ["knn_cov", "correspond", "fdf", "reduce_finish"]
+        return {names[i]: {"avg_ms": float(ms[i]), "count": int(cnt[i])} for i in range(4)}

@@ -1,0 +1,91 @@
+/*
+ * gicp_ref.h -- TEST INFRASTRUCTURE ONLY (the parity oracle / CPU baseline).
+ *
+ * A plain-C CPU restatement of PCL 1.8.1 pcl::GeneralizedIterativeClosestPoint
+ * as instantiated by the reference at include/GICPAlignment.h:153 and driven by
+ * GICPAlignment::fineAlignment (src/GICPAlignment.cpp:86-109).  PCL is not
+ * vendored under /root/reference and is not installed here, so this file
+ * restates the published PCL 1.8.1 algorithm (registration/impl/gicp.hpp,
+ * registration/bfgs.h, registration/impl/registration.hpp) -- see SURVEY.md
+ * Appendix A and DESIGN.md "Oracle".
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
+ * this library, and only as the checker / the timed CPU path.  The product
+ * (leica_point_cloud_processing_amd/) never links or calls it.
+ *
+ * Conventions: 4x4 matrices crossing this header are COLUMN-MAJOR (Eigen's
+ * default storage), like include/mi355x_gicp.h.
+ */
+#ifndef GICP_REF_H
+#define GICP_REF_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+    int    max_iterations;         /* max_iterations_       (src/GICPAlignment.cpp:30 -> 100) */
+    double transformation_epsilon; /* transformation_epsilon_ (src/GICPAlignment.cpp:29 -> 4e-3) */
+    double rotation_epsilon;       /* rotation_epsilon_     (PCL GICP default 2e-3) */
+    double max_corr_dist;          /* corr_dist_threshold_  (src/GICPAlignment.cpp:31 -> 0.04), squared before use */
+    double gicp_epsilon;           /* gicp_epsilon_         (PCL GICP default 1e-3) */
+    int    k_correspondences;      /* k_correspondences_    (PCL GICP default 20) */
+    int    max_inner_iterations;   /* max_inner_iterations_ (PCL GICP default 20) */
+    int    fixed_iterations;       /* test hook: 1 => ignore the delta test, run exactly max_iterations */
+    int    threads;                /* <=1: single thread (PCL 1.8.1 GICP is single-threaded); >1: OpenMP */
+} ref_params;
+
+typedef struct {
+    int    converged;      /* PCL hasConverged() */
+    int    iterations;     /* nr_iterations_ */
+    int    n_corr_last;    /* correspondences in the last outer iteration */
+    int    n_evals;        /* BFGS functor passes over the correspondences (f, df or fdf) */
+    double t_cov_s;        /* trees + covariances (one-time phase) */
+    double t_loop_s;       /* outer GICP loop (correspondences + BFGS) */
+    double t_total_s;
+} ref_result;
+
+/* status codes (mirror include/mi355x_gicp.h) */
+#define REF_OK               0
+#define REF_E_INVALID       -1
+#define REF_E_TOO_FEW_POINTS -2
+#define REF_E_NONFINITE     -4
+
+typedef struct ref_gicp ref_gicp;
+
+void      ref_default_params(ref_params* p);
+ref_gicp* ref_create(const ref_params* p);
+void      ref_destroy(ref_gicp* g);
+int       ref_set_params(ref_gicp* g, const ref_params* p);
+/* Copies the clouds (xyz at byte offset 0, 4, 8 of each record) and marks them dirty. */
+int       ref_set_source(ref_gicp* g, const float* xyz, size_t n, size_t stride_bytes);
+int       ref_set_target(ref_gicp* g, const float* xyz, size_t n, size_t stride_bytes);
+/* Registration::align(output, guess).  trace (optional, max_iterations*16 floats) receives
+ * transformation_ after every outer iteration (column-major). */
+int       ref_align(ref_gicp* g, const float guess_cm[16], float out_T_cm[16], ref_result* res,
+                    float* trace);
+/* Registration::getFitnessScore(max_range) for the final transform T. */
+int       ref_fitness(ref_gicp* g, const float T_cm[16], double max_range, double* out);
+
+/* ---- component hooks used by the parity tests ---- */
+/* GICP::computeCovariances: out_c6 = n x {c00,c01,c02,c11,c12,c22} (fp64). */
+int ref_covariances(const float* xyz, size_t n, size_t stride_bytes, int k, double eps,
+                    int threads, double* out_c6);
+/* Exact kNN (k nearest by (float d^2, index) order, self included). */
+int ref_knn(const float* xyz, size_t n, size_t stride_bytes, const float* queries, size_t nq,
+            int k, int* out_idx, float* out_d2);
+/* One outer-iteration correspondence sweep at transformation T (col-major) with R = (T*guess)3x3.
+ * out_tgt[i] = target index or -1 if rejected; out_M9 (optional) = row-major Mahalanobis. */
+int ref_correspondences(ref_gicp* g, const float T_cm[16], const float guess_cm[16],
+                        int* out_tgt, float* out_d2, double* out_M9);
+/* OptimizationFunctorWithIndices::fdf at state x for the last correspondence set. */
+int ref_fdf(ref_gicp* g, const double x[6], double* f, double g6[6]);
+/* applyState(I, x): column-major float 4x4. */
+void ref_apply_state(const double x[6], float out_cm[16]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,38 @@
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libmgicp.so)")
+    config.addinivalue_line("markers", "slow: long-running CPU test")
+
+
+@pytest.fixture(scope="session")
+def cube_clouds():
+    """The reference unit-test fixture (test_gicp_alignment.cpp:32-47): 5000 glibc-rand()
+    samples of cube.ply and their Rz(0.175) rotation."""
+    from leica_point_cloud_processing_amd import synth
+
+    src, tgt, T = synth.cube_fixture(os.path.join(GOLDEN, "cube.ply"))
+    return src, tgt, T
+
+
+@pytest.fixture(scope="session")
+def part_small():
+    """A 20k/20k scan-vs-CAD case of the synthetic aero part (seeded)."""
+    from leica_point_cloud_processing_amd import synth
+
+    scan, cad, T = synth.scan_vs_cad(20000, 20000)
+    return scan, cad, T
+
+
+def frob(a, b) -> float:
+    return float(np.linalg.norm(np.asarray(a, np.float64) - np.asarray(b, np.float64)))
