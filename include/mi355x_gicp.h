@@ -99,6 +99,18 @@ int mgicp_fitness(mgicp_ctx* ctx, const float T_cm[16], double max_range, double
  * other bytes of each record untouched. */
 int mgicp_transform_source(mgicp_ctx* ctx, const float T_cm[16], float* out, size_t out_stride_bytes);
 
+/* ---- helpers of GICPAlignment(use_covariances = true) ----
+ * Utils::computeCloudResolution (src/Utils.cpp:145-174): mean distance from each point to its
+ * nearest other point (the 2nd of a 2-NN query), fp64 sum of float sqrt. */
+int mgicp_cloud_resolution(mgicp_ctx* ctx, const float* xyz, size_t n, size_t stride_bytes,
+                           double* out);
+/* The NaN-normal removal of GICPAlignment::getCovariances (src/GICPAlignment.cpp:56-71):
+ * pcl::NormalEstimation yields a NaN normal when fewer than 3 points (self included) lie
+ * within the search radius (KdTreeFLANN::radiusSearch: float d^2 < float(radius^2)).
+ * keep[i] = 1 iff at least min_neighbors such points exist. */
+int mgicp_radius_filter(mgicp_ctx* ctx, const float* xyz, size_t n, size_t stride_bytes,
+                        double radius, int min_neighbors, unsigned char* keep);
+
 /* ---- multi-GPU: one process per GPU, point-range shards of the source cloud ----
  * Rank 0 calls mgicp_get_unique_id and broadcasts the 128 bytes out of band (bench.py uses
  * torch.distributed); every rank then calls mgicp_comm_init before set_* / align. */

@@ -16,6 +16,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -28,7 +29,7 @@ using namespace mgicp;
 
 namespace {
 
-constexpr double kOccupancyTarget = 12.0;           // mean points per non-empty cell
+constexpr double kDefaultOccupancy = 12.0;          // mean points per non-empty cell
 constexpr size_t kMaxCells = size_t(1) << 29;       // dense cell table cap (2 GiB of uint32)
 
 double now_ms() {
@@ -200,6 +201,12 @@ struct mgicp_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   Cloud src, tgt;
+  Cloud aux;  // scratch cloud of the resolution / radius helpers
+  double occupancy = kDefaultOccupancy;  // grid cell sizing target (env MGICP_GRID_OCC)
+  // objective-pass launch shape, A/B-measured on MI355X at 5M points (profiles/README.md):
+  // in-launch finish + 512 blocks beat a separate finish kernel and 2048 blocks
+  bool fused_finish = true;              // in-launch reduction finish (env MGICP_FUSED_FINISH)
+  int fdf_max_blocks = 512;              // objective-pass grid cap (env MGICP_FDF_BLOCKS)
   double ms_upload_pending = 0;
   // per source point (sorted), rank shard only
   DevBuf<float4> src_out;  // guess-applied source (only when guess != I)
@@ -209,7 +216,9 @@ struct mgicp_ctx {
   DevBuf<int> dbg_nn;
   DevBuf<double> partial;
   DevBuf<double> red;      // kRedVals
-  double* h_red = nullptr; // pinned
+  double* h_red = nullptr;   // pinned, mapped, coherent host memory
+  double* d_h_red = nullptr; // its device address
+  DevBuf<unsigned int> ticket;  // arrival counter of the in-launch reduction finish
   // build scratch
   DevBuf<uint32_t> counts, keys, keys_sorted, vals;
   DevBuf<unsigned char> scratch;
@@ -326,8 +335,10 @@ int upload_cloud(mgicp_ctx* ctx, Cloud& cl, const float* xyz, size_t n, size_t s
   cl.n = n;
   cl.dirty = true;
   cl.have_cov = false;
-  ctx->have_corr = false;
-  ctx->ms_upload_pending += now_ms() - t0;
+  if (&cl != &ctx->aux) {
+    ctx->have_corr = false;
+    ctx->ms_upload_pending += now_ms() - t0;
+  }
   return MGICP_OK;
 }
 
@@ -361,7 +372,7 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
     maxext = std::max(maxext, ext[d]);
     maxabs = std::max(maxabs, std::max(std::fabs(mn[d]), std::fabs(mx[d])));
   }
-  // 2. cell size: aim at kOccupancyTarget points per non-empty cell
+  // 2. cell size: aim at ctx->occupancy points per non-empty cell
   auto dims = [&](double h, int* nd) {
     size_t nc = 1;
     for (int d = 0; d < 3; ++d) {
@@ -394,9 +405,9 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
     rc = sync(ctx);
     if (rc) return rc;
     const double occ = static_cast<double>(n) / std::max<unsigned long long>(nonempty, 1);
-    if ((occ > 0.6 * kOccupancyTarget && occ < 1.6 * kOccupancyTarget) || nc >= kMaxCells / 2)
+    if ((occ > 0.6 * ctx->occupancy && occ < 1.6 * ctx->occupancy) || nc >= kMaxCells / 2)
       break;
-    if (nonempty <= 1 && occ < kOccupancyTarget) break;  // everything in one cell already
+    if (nonempty <= 1 && occ < ctx->occupancy) break;  // everything in one cell already
     double dim = 2.0;
     if (h_prev > 0 && occ_prev > 0 && std::fabs(std::log(h / h_prev)) > 1e-3) {
       dim = std::log(occ / occ_prev) / std::log(h / h_prev);
@@ -404,7 +415,7 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
     }
     h_prev = h;
     occ_prev = occ;
-    h = h * std::pow(kOccupancyTarget / occ, 1.0 / dim);
+    h = h * std::pow(ctx->occupancy / occ, 1.0 / dim);
     h = std::max(h, 1e-6);
   }
   size_t nc = dims(h, nd);
@@ -490,6 +501,14 @@ int prepare(mgicp_ctx* ctx, bool need_cov) {
   return MGICP_OK;
 }
 
+int ensure_host_red(mgicp_ctx* ctx) {
+  if (ctx->h_red) return MGICP_OK;
+  HIPCK(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_red), kRedVals * sizeof(double),
+                      hipHostMallocMapped | hipHostMallocCoherent));
+  HIPCK(hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->d_h_red), ctx->h_red, 0));
+  return MGICP_OK;
+}
+
 int ensure_iter_buffers(mgicp_ctx* ctx) {
   const size_t n = ctx->src.n;
   HIPCK(ctx->qbuf.reserve(n));
@@ -497,7 +516,12 @@ int ensure_iter_buffers(mgicp_ctx* ctx) {
   const int nb = std::max(fdf_grid_blocks(n), static_cast<int>((n + 255) / 256));
   HIPCK(ctx->partial.reserve(static_cast<size_t>(nb) * kRedVals));
   HIPCK(ctx->red.reserve(kRedVals));
-  if (!ctx->h_red) HIPCK(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_red), kRedVals * sizeof(double)));
+  int rc = ensure_host_red(ctx);
+  if (rc) return rc;
+  if (!ctx->ticket.p) {
+    HIPCK(ctx->ticket.reserve(1));
+    HIPCK(hipMemsetAsync(ctx->ticket.p, 0, sizeof(unsigned int), ctx->stream));
+  }
   return MGICP_OK;
 }
 
@@ -567,13 +591,32 @@ struct DeviceFunctor {
   int pass(const Vec6& x, double sums[kRedVals]) {
     const Mat4 A = apply_state(x);
     const size_t p0 = ctx->shard_p0(), p1 = ctx->shard_p1();
-    const int nb = fdf_grid_blocks(p1 - p0);
-    {
-      ProfScope ps(ctx, kFamFdf);
-      HIPCK(launch_fdf(ctx->d_out, ctx->qbuf.p, mahal3(ctx), p0, p1, A.xf(), ctx->partial.p, nb,
-                       ctx->stream));
+    const int nb = fdf_grid_blocks(p1 - p0, ctx->fdf_max_blocks);
+    int rc;
+    if (ctx->fused_finish) {
+      // the last block writes the sums straight into mapped pinned host memory (single GPU)
+      // or device memory (multi-GPU: then one 16-double RCCL all-reduce and a D2H copy)
+      double* out = ctx->nranks > 1 ? ctx->red.p : ctx->d_h_red;
+      {
+        ProfScope ps(ctx, kFamFdf);
+        HIPCK(launch_fdf(ctx->d_out, ctx->qbuf.p, mahal3(ctx), p0, p1, A.xf(), ctx->partial.p,
+                         nb, ctx->ticket.p, out, ctx->stream));
+      }
+      if (ctx->nranks > 1) {
+        NCCLCK(ncclAllReduce(ctx->red.p, ctx->red.p, kRedVals, ncclDouble, ncclSum, ctx->comm,
+                             ctx->stream));
+        HIPCK(hipMemcpyAsync(ctx->h_red, ctx->red.p, kRedVals * sizeof(double),
+                             hipMemcpyDeviceToHost, ctx->stream));
+      }
+      rc = sync(ctx);
+    } else {
+      {
+        ProfScope ps(ctx, kFamFdf);
+        HIPCK(launch_fdf(ctx->d_out, ctx->qbuf.p, mahal3(ctx), p0, p1, A.xf(), ctx->partial.p,
+                         nb, nullptr, nullptr, ctx->stream));
+      }
+      rc = reduce_to_host(ctx, nb);
     }
-    int rc = reduce_to_host(ctx, nb);
     if (rc) return rc;
     std::memcpy(sums, ctx->h_red, kRedVals * sizeof(double));
     ctx->n_evals++;
@@ -698,6 +741,15 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
   if (!out) return MGICP_E_INVALID;
   *out = nullptr;
   mgicp_ctx* ctx = new mgicp_ctx();
+  if (const char* occ = std::getenv("MGICP_GRID_OCC")) {
+    const double v = std::atof(occ);
+    if (v >= 1.0 && v <= 256.0) ctx->occupancy = v;
+  }
+  if (const char* ff = std::getenv("MGICP_FUSED_FINISH")) ctx->fused_finish = std::atoi(ff) != 0;
+  if (const char* fb = std::getenv("MGICP_FDF_BLOCKS")) {
+    const int v = std::atoi(fb);
+    if (v >= 1 && v <= 65536) ctx->fdf_max_blocks = v;
+  }
   if (p) ctx->prm = *p;
   else mgicp_default_params(&ctx->prm);
   int rc = check_params(ctx, ctx->prm);
@@ -749,7 +801,7 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
-  for (Cloud* c : {&ctx->src, &ctx->tgt}) {
+  for (Cloud* c : {&ctx->src, &ctx->tgt, &ctx->aux}) {
     c->raw.release(); c->orig.release(); c->pts.release(); c->perm.release();
     c->cell_start.release(); c->cov.release();
   }
@@ -757,6 +809,7 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   ctx->partial.release(); ctx->red.release(); ctx->counts.release(); ctx->keys.release();
   ctx->keys_sorted.release(); ctx->vals.release(); ctx->scratch.release(); ctx->u64.release();
   ctx->fpartial.release();
+  ctx->ticket.release();
   if (ctx->h_red) (void)hipHostFree(ctx->h_red);
   prof_resolve(ctx);
   for (hipEvent_t e : ctx->pool) (void)hipEventDestroy(e);
@@ -901,6 +954,43 @@ int mgicp_transform_source(mgicp_ctx* ctx, const float T_cm[16], float* out, siz
     o[2] = h[i].z;
   }
   return MGICP_OK;
+}
+
+int mgicp_cloud_resolution(mgicp_ctx* ctx, const float* xyz, size_t n, size_t stride, double* out) {
+  if (!ctx || !out) return MGICP_E_INVALID;
+  HIPCK(hipSetDevice(ctx->device));
+  *out = 0.0;
+  if (n < 2) return MGICP_OK;  // no point has a 2nd neighbour: res stays 0
+  int rc = upload_cloud(ctx, ctx->aux, xyz, n, stride, false);
+  if (rc || (rc = build_grid(ctx, ctx->aux))) return rc;
+  const int nb = static_cast<int>((n + 255) / 256);
+  HIPCK(ctx->partial.reserve(static_cast<size_t>(nb) * kRedVals));
+  HIPCK(ctx->red.reserve(kRedVals));
+  if ((rc = ensure_host_red(ctx))) return rc;
+  HIPCK(launch_resolution(ctx->aux.view, n, ctx->partial.p, nb, ctx->stream));
+  HIPCK(launch_reduce_finish(ctx->partial.p, nb, ctx->red.p, ctx->stream));
+  HIPCK(hipMemcpyAsync(ctx->h_red, ctx->red.p, kRedVals * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+  if ((rc = sync(ctx))) return rc;
+  const double cnt = ctx->h_red[13];
+  *out = cnt > 0 ? ctx->h_red[0] / cnt : 0.0;
+  return MGICP_OK;
+}
+
+int mgicp_radius_filter(mgicp_ctx* ctx, const float* xyz, size_t n, size_t stride, double radius,
+                        int min_neighbors, unsigned char* keep) {
+  if (!ctx || !keep || min_neighbors < 1 || !(radius >= 0)) return MGICP_E_INVALID;
+  HIPCK(hipSetDevice(ctx->device));
+  if (n == 0) return MGICP_OK;
+  int rc = upload_cloud(ctx, ctx->aux, xyz, n, stride, false);
+  if (rc || (rc = build_grid(ctx, ctx->aux))) return rc;
+  DevBuf<unsigned char> d_keep;
+  HIPCK(d_keep.reserve(n));
+  const float r2 = static_cast<float>(radius * radius);
+  HIPCK(launch_radius_keep(ctx->aux.view, n, r2, min_neighbors, d_keep.p, ctx->stream));
+  HIPCK(hipMemcpyAsync(keep, d_keep.p, n, hipMemcpyDeviceToHost, ctx->stream));
+  rc = sync(ctx);
+  d_keep.release();
+  return rc;
 }
 
 int mgicp_get_unique_id(unsigned char id[128]) {

@@ -60,12 +60,17 @@ hipError_t launch_correspond(const GridView& tgt, const Cov3& cov_t, const float
                              const Cov3& cov_s, size_t p0, size_t p1, Xf34 T, Rot33d R,
                              double thr, float4* qbuf, Cov3 mahal, int* dbg_nn,
                              hipStream_t s);
-int        fdf_grid_blocks(size_t n);
+int        fdf_grid_blocks(size_t n, int max_blocks = 2048);
+// objective pass + in-launch finish: writes the kRedVals sums to `out` (device or mapped host)
 hipError_t launch_fdf(const float4* src, const float4* qbuf, const Cov3& mahal, size_t p0,
-                      size_t p1, Xf34 A, double* partial, int nb, hipStream_t s);
+                      size_t p1, Xf34 A, double* partial, int nb, unsigned int* ticket,
+                      double* out, hipStream_t s);
 hipError_t launch_fitness(const GridView& tgt, const float4* src, size_t p0, size_t p1,
                           Xf34 T, double max_range, double* partial, int nb, hipStream_t s);
 hipError_t launch_reduce_finish(const double* partial, int nb, double* out, hipStream_t s);
+hipError_t launch_resolution(const GridView& g, size_t n, double* partial, int nb, hipStream_t s);
+hipError_t launch_radius_keep(const GridView& g, size_t n, float r2, int need, unsigned char* keep,
+                              hipStream_t s);
 
 // radix sort / scan scratch (hipcub)
 size_t sort_scratch_bytes(size_t n, int bits);

@@ -75,6 +75,14 @@ __device__ __forceinline__ float axis_bound(float q, float o, float h, int c, in
   return fminf(dlo, dhi);
 }
 
+// lower bound of the distance from q to cell c's slab [o + c h, o + (c+1) h) along one axis
+__device__ __forceinline__ float cell_gap(float q, float o, float h, int c, float slop) {
+  const float lo = o + static_cast<float>(c) * h;
+  const float hi = o + static_cast<float>(c + 1) * h;
+  const float d = fmaxf(lo - q, q - hi);
+  return fmaxf(d - slop, 0.f);
+}
+
 __device__ __forceinline__ int dist_out(int c, int n) {
   return c < 0 ? -c : (c > n - 1 ? c - (n - 1) : 0);
 }
@@ -103,13 +111,29 @@ __device__ __forceinline__ void ring_search(const GridView& g, float qx, float q
     const int zlo = max(z0, 0), zhi = min(z1, g.nz - 1);
     for (int z = zlo; z <= zhi; ++z) {
       const bool zf = (z == z0) || (z == z1);
+      const float gz = cell_gap(qz, g.oz, g.h, z, g.slop);
       for (int y = ylo; y <= yhi; ++y) {
+        // ball-cell pruning: skip rows / cells whose box lies beyond the visitor's current
+        // worst distance (margin 1e-5 relative + slop keeps the search exact, ties included)
+        const float w = vis.prune2() * 1.00001f;
+        const float gy = cell_gap(qy, g.oy, g.h, y, g.slop);
+        const float gyz = gy * gy + gz * gz;
+        if (gyz > w) continue;
         const uint32_t* row = g.cell_start + (static_cast<size_t>(z) * g.ny + y) * g.nx;
         if (zf || y == y0 || y == y1) {
-          if (xlo <= xhi) vis.range(g, row[xlo], row[xhi + 1]);
+          const float rx = sqrtf(w - gyz) + g.slop;
+          const int xa = max(xlo, qcell(qx - rx, g.ox, g.inv_h));
+          const int xb = min(xhi, qcell(qx + rx, g.ox, g.inv_h));
+          if (xa <= xb) vis.range(g, row[xa], row[xb + 1]);
         } else {
-          if (x0 >= 0) vis.range(g, row[x0], row[x0 + 1]);
-          if (x1 < g.nx) vis.range(g, row[x1], row[x1 + 1]);
+          if (x0 >= 0) {
+            const float gx = cell_gap(qx, g.ox, g.h, x0, g.slop);
+            if (gx * gx + gyz <= w) vis.range(g, row[x0], row[x0 + 1]);
+          }
+          if (x1 < g.nx) {
+            const float gx = cell_gap(qx, g.ox, g.h, x1, g.slop);
+            if (gx * gx + gyz <= vis.prune2() * 1.00001f) vis.range(g, row[x1], row[x1 + 1]);
+          }
         }
       }
     }
@@ -131,6 +155,10 @@ struct KnnVisitor {
   __device__ __forceinline__ bool done(float Ls) const {
     if (key[K - 1] == ~0ull || !(Ls > 0.f)) return false;
     return __uint_as_float(static_cast<uint32_t>(key[K - 1] >> 32)) < Ls * Ls;
+  }
+  // squared radius beyond which no point can enter the result
+  __device__ __forceinline__ float prune2() const {
+    return key[K - 1] == ~0ull ? INFINITY : __uint_as_float(static_cast<uint32_t>(key[K - 1] >> 32));
   }
   __device__ __forceinline__ void insert(unsigned long long c, uint32_t cp) {
 #pragma unroll
@@ -157,11 +185,17 @@ struct KnnVisitor {
 struct NnVisitor {
   float qx, qy, qz;
   double thr;
+  float thr_f;  // float upper bound of thr (pruning radius cap)
   unsigned long long best;
   uint32_t pos;
 
   __device__ __forceinline__ void init(float x, float y, float z, double t) {
     qx = x; qy = y; qz = z; thr = t; best = ~0ull; pos = 0u;
+    thr_f = (t >= 3.0e38) ? INFINITY : __double2float_ru(t);
+  }
+  __device__ __forceinline__ float prune2() const {
+    const float b = best == ~0ull ? INFINITY : __uint_as_float(static_cast<uint32_t>(best >> 32));
+    return fminf(b, thr_f);
   }
   __device__ __forceinline__ bool done(float Ls) const {
     if (!(Ls > 0.f)) return false;
@@ -174,6 +208,25 @@ struct NnVisitor {
       const float4 p = g.pts[j];
       const unsigned long long c = mkkey(dist2(qx, qy, qz, p), p.w);
       if (c < best) { best = c; pos = j; }
+    }
+  }
+};
+
+// radius-count visitor: counts points with float d2 < r2 (FLANN RadiusResultSet: dist < radius),
+// stopping as soon as `need` are found
+struct RadiusCountVisitor {
+  float qx, qy, qz;
+  float r2;
+  int need, count;
+
+  __device__ __forceinline__ bool done(float Ls) const {
+    if (count >= need) return true;
+    return Ls > 0.f && Ls * Ls >= r2;
+  }
+  __device__ __forceinline__ float prune2() const { return count >= need ? 0.f : r2; }
+  __device__ __forceinline__ void range(const GridView& g, uint32_t a, uint32_t b) {
+    for (uint32_t j = a; j < b && count < need; ++j) {
+      if (dist2(qx, qy, qz, g.pts[j]) < r2) ++count;
     }
   }
 };
@@ -467,6 +520,7 @@ __device__ __forceinline__ double wave_sum(double v) {
 __device__ __forceinline__ void block_reduce_store(double (&acc)[kRedVals], double* dst) {
   __shared__ double sm[4][kRedVals];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __syncthreads();  // sm may still be read by a previous call in this block
 #pragma unroll
   for (int v = 0; v < kRedVals; ++v) {
     const double w = wave_sum(acc[v]);
@@ -483,10 +537,46 @@ __device__ __forceinline__ void block_reduce_store(double (&acc)[kRedVals], doub
   }
 }
 
+// In-launch deterministic finish (cdna_hip_programming.md Guideline 16, split-K counter form):
+// every block publishes its partial with an agent-scope release and takes a ticket; the block
+// that draws the last ticket acquires, sums all partials in block order and writes `out`
+// (device memory or mapped pinned host memory), then re-arms the ticket for the next launch.
+__device__ __forceinline__ void finish_in_last_block(const double* partial, unsigned int* ticket,
+                                                     double* out) {
+  __shared__ int last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = (prev == gridDim.x - 1) ? 1 : 0;
+  }
+  __syncthreads();
+  if (!last) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  double acc[kRedVals];
+#pragma unroll
+  for (int v = 0; v < kRedVals; ++v) acc[v] = 0.0;
+  const int nb = gridDim.x;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+#pragma unroll
+    for (int v = 0; v < kRedVals; ++v) acc[v] += partial[static_cast<size_t>(b) * kRedVals + v];
+  }
+  block_reduce_store(acc, out);
+  if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __global__ __launch_bounds__(256) void fdf_kernel(const float4* __restrict__ src,
                                                   const float4* __restrict__ qbuf, Cov3 mahal,
                                                   size_t p0, size_t p1, Xf34 A,
-                                                  double* __restrict__ partial) {
+                                                  double* __restrict__ partial,
+                                                  unsigned int* __restrict__ ticket,
+                                                  double* __restrict__ out) {
   double acc[kRedVals];
 #pragma unroll
   for (int v = 0; v < kRedVals; ++v) acc[v] = 0.0;
@@ -516,6 +606,7 @@ __global__ __launch_bounds__(256) void fdf_kernel(const float4* __restrict__ src
     acc[13] += 1.0;
   }
   block_reduce_store(acc, partial + static_cast<size_t>(blockIdx.x) * kRedVals);
+  if (ticket) finish_in_last_block(partial, ticket, out);
 }
 
 __global__ __launch_bounds__(256) void fitness_kernel(GridView tg, const float4* __restrict__ src,
@@ -542,6 +633,36 @@ __global__ __launch_bounds__(256) void fitness_kernel(GridView tg, const float4*
     }
   }
   block_reduce_store(acc, partial + static_cast<size_t>(blockIdx.x) * kRedVals);
+}
+
+// Utils::computeCloudResolution: sqrt of the 2nd-nearest (self is 1st) float d2, summed in fp64
+__global__ __launch_bounds__(256) void resolution_kernel(GridView g, size_t n,
+                                                         double* __restrict__ partial) {
+  double acc[kRedVals];
+#pragma unroll
+  for (int v = 0; v < kRedVals; ++v) acc[v] = 0.0;
+  const size_t p = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (p < n && n >= 2) {
+    const float4 q = g.pts[p];
+    KnnVisitor<2> vis;
+    vis.init(q.x, q.y, q.z);
+    ring_search(g, q.x, q.y, q.z, vis);
+    const float d2 = __uint_as_float(static_cast<uint32_t>(vis.key[1] >> 32));
+    acc[0] = static_cast<double>(sqrtf(d2));
+    acc[13] = 1.0;
+  }
+  block_reduce_store(acc, partial + static_cast<size_t>(blockIdx.x) * kRedVals);
+}
+
+// NormalEstimation's NaN-normal test: fewer than `need` radius neighbours (self included)
+__global__ void radius_keep_kernel(GridView g, size_t n, float r2, int need,
+                                   unsigned char* __restrict__ keep_orig) {
+  const size_t p = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const float4 q = g.pts[p];
+  RadiusCountVisitor vis{q.x, q.y, q.z, r2, need, 0};
+  ring_search(g, q.x, q.y, q.z, vis);
+  keep_orig[__float_as_uint(q.w)] = vis.count >= need ? 1 : 0;
 }
 
 __global__ __launch_bounds__(256) void reduce_finish_kernel(const double* __restrict__ partial,
@@ -640,21 +761,34 @@ hipError_t launch_correspond(const GridView& tgt, const Cov3& cov_t, const float
   return hipGetLastError();
 }
 
-int fdf_grid_blocks(size_t n) {
+int fdf_grid_blocks(size_t n, int max_blocks) {
   // ~8 points per thread keeps >= 8 waves per CU resident on 256 CUs at 5M points
   const size_t want = (n + 256 * 8 - 1) / (256 * 8);
-  return static_cast<int>(std::max<size_t>(1, std::min<size_t>(want, 2048)));
+  return static_cast<int>(std::max<size_t>(1, std::min<size_t>(want, max_blocks)));
 }
 
 hipError_t launch_fdf(const float4* src, const float4* qbuf, const Cov3& mahal, size_t p0,
-                      size_t p1, Xf34 A, double* partial, int nb, hipStream_t s) {
-  fdf_kernel<<<nb, 256, 0, s>>>(src, qbuf, mahal, p0, p1, A, partial);
+                      size_t p1, Xf34 A, double* partial, int nb, unsigned int* ticket,
+                      double* out, hipStream_t s) {
+  fdf_kernel<<<nb, 256, 0, s>>>(src, qbuf, mahal, p0, p1, A, partial, ticket, out);
   return hipGetLastError();
 }
 
 hipError_t launch_fitness(const GridView& tgt, const float4* src, size_t p0, size_t p1, Xf34 T,
                           double max_range, double* partial, int nb, hipStream_t s) {
   fitness_kernel<<<nb, 256, 0, s>>>(tgt, src, p0, p1, T, max_range, partial);
+  return hipGetLastError();
+}
+
+hipError_t launch_resolution(const GridView& g, size_t n, double* partial, int nb, hipStream_t s) {
+  resolution_kernel<<<nb, 256, 0, s>>>(g, n, partial);
+  return hipGetLastError();
+}
+
+hipError_t launch_radius_keep(const GridView& g, size_t n, float r2, int need, unsigned char* keep,
+                              hipStream_t s) {
+  if (!n) return hipSuccess;
+  radius_keep_kernel<<<nblk(n), 256, 0, s>>>(g, n, r2, need, keep);
   return hipGetLastError();
 }
 

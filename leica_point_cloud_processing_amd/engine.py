@@ -9,6 +9,7 @@ All compute goes through libmgicp.so (include/mi355x_gicp.h); nothing runs on th
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 
 import numpy as np
@@ -17,6 +18,13 @@ from . import _lib
 from .cloud import PointCloudRGB
 
 DBL_MAX = float(np.finfo(np.float64).max)
+_LIVE: set = set()
+_SHUTTING_DOWN = [False]
+
+
+@atexit.register
+def _mark_shutdown():
+    _SHUTTING_DOWN[0] = True
 
 
 def _cm(T) -> np.ndarray:
@@ -47,6 +55,7 @@ class GICPEngine:
         if rc != 0:
             raise _lib.MgicpError(rc, "mgicp_create failed (no HIP device or invalid parameters)")
         self._h = h
+        _LIVE.add(id(self))
         self.ransac_outlier_threshold = 0.05
         self._input = None
         self._converged = False
@@ -54,11 +63,24 @@ class GICPEngine:
         self.last_result = None
 
     def close(self):
-        if getattr(self, "_h", None):
-            self._lib.mgicp_destroy(self._h)
+        """Release the device context (deterministically, before interpreter shutdown)."""
+        h = getattr(self, "_h", None)
+        if h:
             self._h = None
+            _LIVE.discard(id(self))
+            self._lib.mgicp_destroy(h)
 
-    __del__ = close
+    def __del__(self):
+        # at interpreter shutdown the HIP runtime may already be torn down: leave the context
+        # to the process exit instead of racing the runtime's own destructors
+        if not _SHUTTING_DOWN[0]:
+            self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
     # -- helpers -------------------------------------------------------------------------
     def _check(self, rc: int, what: str):
