@@ -99,6 +99,12 @@ int mgicp_fitness(mgicp_ctx* ctx, const float T_cm[16], double max_range, double
  * other bytes of each record untouched. */
 int mgicp_transform_source(mgicp_ctx* ctx, const float T_cm[16], float* out, size_t out_stride_bytes);
 
+/* pcl::transformPointCloud(in, out, T) for any cloud (GICPAlignment::applyTFtoCloud,
+ * src/GICPAlignment.cpp:144-147): xyz of n records of `in` are transformed on the GPU and
+ * written into `out` (other bytes of the out records untouched; in == out allowed). */
+int mgicp_transform_cloud(mgicp_ctx* ctx, const float T_cm[16], const float* in, size_t n,
+                          size_t in_stride_bytes, float* out, size_t out_stride_bytes);
+
 /* ---- helpers of GICPAlignment(use_covariances = true) ----
  * Utils::computeCloudResolution (src/Utils.cpp:145-174): mean distance from each point to its
  * nearest other point (the 2nd of a 2-NN query), fp64 sum of float sqrt. */
@@ -113,7 +119,8 @@ int mgicp_radius_filter(mgicp_ctx* ctx, const float* xyz, size_t n, size_t strid
 
 /* ---- multi-GPU: one process per GPU, point-range shards of the source cloud ----
  * Rank 0 calls mgicp_get_unique_id and broadcasts the 128 bytes out of band (bench.py uses
- * torch.distributed); every rank then calls mgicp_comm_init before set_* / align. */
+ * the TCP rendezvous of leica_point_cloud_processing_amd/parallel.py); every rank then calls
+ * mgicp_comm_init before set_* / align.  Every objective pass then all-reduces 16 doubles. */
 int mgicp_get_unique_id(unsigned char id[128]);
 int mgicp_comm_init(mgicp_ctx* ctx, int nranks, int rank, const unsigned char id[128]);
 
@@ -125,6 +132,11 @@ int mgicp_debug_covariances(mgicp_ctx* ctx, int which, double* out_c6);
 int mgicp_debug_correspondences(mgicp_ctx* ctx, const float T_cm[16], int* out_tgt, double* out_M6);
 /* OptimizationFunctorWithIndices::fdf at x over the last correspondence sweep */
 int mgicp_debug_fdf(mgicp_ctx* ctx, const double x[6], double* f, double g6[6]);
+/* the raw reduced sums of one objective pass at x: [0] sum r'Mr, [1..3] sum Mr,
+ * [4..12] sum s (Mr)' row-major, [13] correspondence count.  With mgicp_comm_init(ctx, n, r,
+ * NULL) (a "detached" shard, no RCCL) they cover rank r's source range only, so sharding can
+ * be verified on one device; align/fitness refuse to run in that mode. */
+int mgicp_debug_fdf_sums(mgicp_ctx* ctx, const double x[6], double out16[16]);
 /* per-iteration transformation_ of the last align (col-major, iterations x 16) */
 int mgicp_debug_trace(mgicp_ctx* ctx, float* out, int max_iters);
 /* average device time (ms) of each kernel family during the last align, for roofline

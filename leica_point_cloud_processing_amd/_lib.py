@@ -77,11 +77,15 @@ _SIGNATURES = {
     "mgicp_align": (ctypes.c_int, [_P, _FP, _FP, ctypes.POINTER(MgicpResult)]),
     "mgicp_fitness": (ctypes.c_int, [_P, _FP, ctypes.c_double, _DP]),
     "mgicp_transform_source": (ctypes.c_int, [_P, _FP, _P, _SZ]),
+    "mgicp_transform_cloud": (ctypes.c_int, [_P, _FP, _P, _SZ, _SZ, _P, _SZ]),
+    "mgicp_cloud_resolution": (ctypes.c_int, [_P, _P, _SZ, _SZ, _DP]),
+    "mgicp_radius_filter": (ctypes.c_int, [_P, _P, _SZ, _SZ, ctypes.c_double, ctypes.c_int, _P]),
     "mgicp_get_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
     "mgicp_comm_init": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]),
     "mgicp_debug_covariances": (ctypes.c_int, [_P, ctypes.c_int, _DP]),
     "mgicp_debug_correspondences": (ctypes.c_int, [_P, _FP, _IP, _DP]),
     "mgicp_debug_fdf": (ctypes.c_int, [_P, _DP, _DP, _DP]),
+    "mgicp_debug_fdf_sums": (ctypes.c_int, [_P, _DP, _DP]),
     "mgicp_debug_trace": (ctypes.c_int, [_P, _FP, ctypes.c_int]),
     "mgicp_debug_kernel_times": (ctypes.c_int, [_P, _DP, _IP]),
     "mgicp_set_profiling": (ctypes.c_int, [_P, ctypes.c_int]),

@@ -571,7 +571,7 @@ int reduce_to_host(mgicp_ctx* ctx, int nb) {
     ProfScope ps(ctx, kFamRed);
     HIPCK(launch_reduce_finish(ctx->partial.p, nb, ctx->red.p, ctx->stream));
   }
-  if (ctx->nranks > 1)
+  if (ctx->comm)
     NCCLCK(ncclAllReduce(ctx->red.p, ctx->red.p, kRedVals, ncclDouble, ncclSum, ctx->comm,
                          ctx->stream));
   HIPCK(hipMemcpyAsync(ctx->h_red, ctx->red.p, kRedVals * sizeof(double), hipMemcpyDeviceToHost,
@@ -596,13 +596,13 @@ struct DeviceFunctor {
     if (ctx->fused_finish) {
       // the last block writes the sums straight into mapped pinned host memory (single GPU)
       // or device memory (multi-GPU: then one 16-double RCCL all-reduce and a D2H copy)
-      double* out = ctx->nranks > 1 ? ctx->red.p : ctx->d_h_red;
+      double* out = ctx->comm ? ctx->red.p : ctx->d_h_red;
       {
         ProfScope ps(ctx, kFamFdf);
         HIPCK(launch_fdf(ctx->d_out, ctx->qbuf.p, mahal3(ctx), p0, p1, A.xf(), ctx->partial.p,
                          nb, ctx->ticket.p, out, ctx->stream));
       }
-      if (ctx->nranks > 1) {
+      if (ctx->comm) {
         NCCLCK(ncclAllReduce(ctx->red.p, ctx->red.p, kRedVals, ncclDouble, ncclSum, ctx->comm,
                              ctx->stream));
         HIPCK(hipMemcpyAsync(ctx->h_red, ctx->red.p, kRedVals * sizeof(double),
@@ -841,6 +841,8 @@ int mgicp_set_source_device(mgicp_ctx* ctx, const float* d_xyz, size_t n, size_t
 
 int mgicp_align(mgicp_ctx* ctx, const float guess_cm[16], float out_T_cm[16], mgicp_result* res) {
   if (!ctx || !out_T_cm) return MGICP_E_INVALID;
+  if (ctx->nranks > 1 && !ctx->comm)
+    return fail(ctx, MGICP_E_INVALID, "detached shard context: only the debug entry points are available");
   HIPCK(hipSetDevice(ctx->device));
   mgicp_result r;
   std::memset(&r, 0, sizeof(r));
@@ -917,6 +919,8 @@ int mgicp_align(mgicp_ctx* ctx, const float guess_cm[16], float out_T_cm[16], mg
 
 int mgicp_fitness(mgicp_ctx* ctx, const float T_cm[16], double max_range, double* out) {
   if (!ctx || !T_cm || !out) return MGICP_E_INVALID;
+  if (ctx->nranks > 1 && !ctx->comm)
+    return fail(ctx, MGICP_E_INVALID, "detached shard context: only the debug entry points are available");
   HIPCK(hipSetDevice(ctx->device));
   int rc = prepare(ctx, false);
   if (rc) return rc;
@@ -945,6 +949,38 @@ int mgicp_transform_source(mgicp_ctx* ctx, const float T_cm[16], float* out, siz
   HIPCK(hipMemcpyAsync(h.data(), tmp.p, n * sizeof(float4), hipMemcpyDeviceToHost, ctx->stream));
   int rc = sync(ctx);
   tmp.release();
+  if (rc) return rc;
+  unsigned char* base = reinterpret_cast<unsigned char*>(out);
+  for (size_t i = 0; i < n; ++i) {
+    float* o = reinterpret_cast<float*>(base + i * out_stride);
+    o[0] = h[i].x;
+    o[1] = h[i].y;
+    o[2] = h[i].z;
+  }
+  return MGICP_OK;
+}
+
+int mgicp_transform_cloud(mgicp_ctx* ctx, const float T_cm[16], const float* in, size_t n,
+                          size_t in_stride, float* out, size_t out_stride) {
+  if (!ctx || !T_cm || (n && (!in || !out)) || in_stride < 12 || out_stride < 12 ||
+      (in_stride % 4) || (out_stride % 4))
+    return MGICP_E_INVALID;
+  HIPCK(hipSetDevice(ctx->device));
+  if (n == 0) return MGICP_OK;
+  DevBuf<unsigned char> raw;
+  DevBuf<float4> a, b;
+  HIPCK(raw.reserve(n * in_stride));
+  HIPCK(a.reserve(n));
+  HIPCK(b.reserve(n));
+  HIPCK(hipMemcpyAsync(raw.p, in, n * in_stride, hipMemcpyHostToDevice, ctx->stream));
+  HIPCK(launch_pack_points(raw.p, n, in_stride, a.p, ctx->stream));
+  HIPCK(launch_xform_points(a.p, n, Mat4::from_cm(T_cm).xf(), b.p, ctx->stream));
+  std::vector<float4> h(n);
+  HIPCK(hipMemcpyAsync(h.data(), b.p, n * sizeof(float4), hipMemcpyDeviceToHost, ctx->stream));
+  int rc = sync(ctx);
+  raw.release();
+  a.release();
+  b.release();
   if (rc) return rc;
   unsigned char* base = reinterpret_cast<unsigned char*>(out);
   for (size_t i = 0; i < n; ++i) {
@@ -1003,7 +1039,7 @@ int mgicp_get_unique_id(unsigned char id[128]) {
 }
 
 int mgicp_comm_init(mgicp_ctx* ctx, int nranks, int rank, const unsigned char id[128]) {
-  if (!ctx || nranks < 1 || rank < 0 || rank >= nranks || (nranks > 1 && !id)) return MGICP_E_INVALID;
+  if (!ctx || nranks < 1 || rank < 0 || rank >= nranks) return MGICP_E_INVALID;
   HIPCK(hipSetDevice(ctx->device));
   if (ctx->comm) {
     (void)ncclCommDestroy(ctx->comm);
@@ -1013,7 +1049,7 @@ int mgicp_comm_init(mgicp_ctx* ctx, int nranks, int rank, const unsigned char id
   ctx->rank = rank;
   ctx->src.have_cov = false;
   ctx->have_corr = false;
-  if (nranks == 1) return MGICP_OK;
+  if (nranks == 1 || !id) return MGICP_OK;  // id == NULL: detached shard (debug entry points only)
   ncclUniqueId uid;
   std::memcpy(&uid, id, 128);
   NCCLCK(ncclCommInitRank(&ctx->comm, nranks, uid, rank));
@@ -1089,6 +1125,15 @@ int mgicp_debug_fdf(mgicp_ctx* ctx, const double x[6], double* f, double g6[6]) 
   if (g6)
     for (int i = 0; i < 6; ++i) g6[i] = gv[i];
   return MGICP_OK;
+}
+
+int mgicp_debug_fdf_sums(mgicp_ctx* ctx, const double x[6], double out16[16]) {
+  if (!ctx || !x || !out16 || !ctx->have_corr) return MGICP_E_INVALID;
+  HIPCK(hipSetDevice(ctx->device));
+  DeviceFunctor fn{ctx};
+  Vec6 xv;
+  for (int i = 0; i < 6; ++i) xv[i] = x[i];
+  return fn.pass(xv, out16);
 }
 
 int mgicp_debug_trace(mgicp_ctx* ctx, float* out, int max_iters) {

@@ -116,19 +116,20 @@ class GICPEngine:
 
     def setInputSource(self, cloud):
         self._input = cloud
-        ptr, n, stride = self._cloud_arg(cloud)
+        keep, ptr, n, stride = self._cloud_arg(cloud)
         self._check(self._lib.mgicp_set_source(self._h, ptr, n, stride), "setInputSource")
 
     def setInputTarget(self, cloud):
-        ptr, n, stride = self._cloud_arg(cloud)
+        keep, ptr, n, stride = self._cloud_arg(cloud)
         self._check(self._lib.mgicp_set_target(self._h, ptr, n, stride), "setInputTarget")
 
     @staticmethod
     def _cloud_arg(cloud):
+        """(owner, pointer, n, stride); `owner` keeps a converted copy alive across the call."""
         if isinstance(cloud, PointCloudRGB):
-            return cloud.ctypes_xyz()
+            return (cloud,) + cloud.ctypes_xyz()
         a = np.ascontiguousarray(cloud, dtype=np.float32).reshape(-1, 3)
-        return a.ctypes.data, len(a), 12
+        return a, a.ctypes.data, len(a), 12
 
     def set_source_xyz(self, xyz):
         self._src_keep = np.ascontiguousarray(xyz, dtype=np.float32).reshape(-1, 3)
@@ -162,7 +163,7 @@ class GICPEngine:
             self._check(rc, "align")
             self._converged = bool(res.converged)
         self._final = _from_cm(out)
-        if output is not None and self._input is not None:
+        if output is not None and isinstance(self._input, PointCloudRGB):
             # output = transformPointCloud(*input_, output, final_transformation_)
             output.copy_from(self._input)
             self.transform_source_into(self._final, output)
@@ -190,6 +191,32 @@ class GICPEngine:
         ptr, n, stride = cloud.ctypes_xyz()
         self._check(self._lib.mgicp_transform_source(self._h, _fp(_cm(T)), ctypes.c_void_p(ptr), stride),
                     "transform_source")
+
+    def transform_cloud(self, T, cloud_in: PointCloudRGB, cloud_out: PointCloudRGB) -> None:
+        """pcl::transformPointCloud(cloud_in, cloud_out, T) with the xyz transform on the GPU."""
+        if cloud_out is not cloud_in:
+            cloud_out.copy_from(cloud_in)
+        _, ptr, n, stride = self._cloud_arg(cloud_out)
+        self._check(self._lib.mgicp_transform_cloud(self._h, _fp(_cm(T)), ctypes.c_void_p(ptr), n, stride,
+                                                    ctypes.c_void_p(ptr), stride), "transform_cloud")
+
+    # -- helpers of GICPAlignment(use_covariances=true) --------------------------------------
+    def cloud_resolution(self, cloud) -> float:
+        """Utils::computeCloudResolution on the GPU (mean distance to the nearest other point)."""
+        keep, ptr, n, stride = self._cloud_arg(cloud)
+        out = ctypes.c_double()
+        self._check(self._lib.mgicp_cloud_resolution(self._h, ctypes.c_void_p(ptr), n, stride, ctypes.byref(out)),
+                    "cloud_resolution")
+        return out.value
+
+    def radius_filter(self, cloud, radius: float, min_neighbors: int = 3) -> np.ndarray:
+        """bool mask: >= min_neighbors points (self included) within `radius` (NormalEstimation's
+        non-NaN condition)."""
+        keep, ptr, n, stride = self._cloud_arg(cloud)
+        keep = np.zeros(n, np.uint8)
+        self._check(self._lib.mgicp_radius_filter(self._h, ctypes.c_void_p(ptr), n, stride, float(radius),
+                                                  int(min_neighbors), keep.ctypes.data), "radius_filter")
+        return keep.astype(bool)
 
     # -- multi-GPU ------------------------------------------------------------------------
     @staticmethod
@@ -224,6 +251,12 @@ class GICPEngine:
         g = np.zeros(6, np.float64)
         self._check(self._lib.mgicp_debug_fdf(self._h, _dp(x), ctypes.byref(f), _dp(g)), "debug_fdf")
         return f.value, g
+
+    def debug_fdf_sums(self, x) -> np.ndarray:
+        x = np.asarray(x, np.float64)
+        out = np.zeros(16, np.float64)
+        self._check(self._lib.mgicp_debug_fdf_sums(self._h, _dp(x), _dp(out)), "debug_fdf_sums")
+        return out
 
     def debug_trace(self, max_iters: int = 1000):
         buf = np.zeros(16 * max_iters, np.float32)

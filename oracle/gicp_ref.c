@@ -622,6 +622,21 @@ static void functor_eval(ref_gicp* g, const double x[6], double* f, double grad[
     }
 }
 
+int ref_fdf_sums(ref_gicp* g, const double x[6], int c0, int c1, double out14[14]) {
+    if (!g || !out14 || c0 < 0 || c1 > g->m || c0 > c1) return REF_E_INVALID;
+    float A[4][4];
+    apply_state(x, A);
+    fdf_acc acc;
+    fdf_range(g, A, c0, c1, &acc);
+    out14[0] = acc.f;
+    for (int a = 0; a < 3; ++a) {
+        out14[1 + a] = acc.gt[a];
+        for (int b = 0; b < 3; ++b) out14[4 + 3 * a + b] = acc.R[a][b];
+    }
+    out14[13] = (double)(c1 - c0);
+    return REF_OK;
+}
+
 int ref_fdf(ref_gicp* g, const double x[6], double* f, double g6[6]) {
     if (!g || g->m <= 0) return REF_E_INVALID;
     functor_eval(g, x, f, g6);

@@ -82,6 +82,9 @@ int ref_correspondences(ref_gicp* g, const float T_cm[16], const float guess_cm[
                         int* out_tgt, float* out_d2, double* out_M9);
 /* OptimizationFunctorWithIndices::fdf at state x for the last correspondence set. */
 int ref_fdf(ref_gicp* g, const double x[6], double* f, double g6[6]);
+/* raw sums of the functor over correspondences [c0, c1): f, g_t[3], Rsum[9] row-major, count
+ * (the per-shard partials of the multi-GPU decomposition) */
+int ref_fdf_sums(ref_gicp* g, const double x[6], int c0, int c1, double out14[14]);
 /* applyState(I, x): column-major float 4x4. */
 void ref_apply_state(const double x[6], float out_cm[16]);
 

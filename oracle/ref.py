@@ -71,6 +71,7 @@ def load():
         "ref_knn": (ctypes.c_int, [P, sz, sz, P, sz, ctypes.c_int, IP, FP]),
         "ref_correspondences": (ctypes.c_int, [P, FP, FP, IP, FP, DP]),
         "ref_fdf": (ctypes.c_int, [P, DP, DP, DP]),
+        "ref_fdf_sums": (ctypes.c_int, [P, DP, ctypes.c_int, ctypes.c_int, DP]),
         "ref_apply_state": (None, [DP, FP]),
     }
     for name, (res, args) in sig.items():
@@ -169,6 +170,13 @@ class RefGICP:
         g = cm(np.eye(4) if guess is None else guess)
         m = self.lib.ref_correspondences(self.h, _fp(cm(T)), _fp(g), _ip(tgt), _fp(d2), _dp(M))
         return m, tgt, d2, M
+
+    def fdf_sums(self, x, c0, c1):
+        x = np.asarray(x, np.float64)
+        out = np.zeros(14, np.float64)
+        rc = self.lib.ref_fdf_sums(self.h, _dp(x), int(c0), int(c1), _dp(out))
+        assert rc == 0
+        return out
 
     def fdf(self, x):
         x = np.asarray(x, np.float64)
