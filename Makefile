@@ -8,10 +8,16 @@ HDRS  := $(wildcard $(PKG)/csrc/*.hpp) include/mi355x_gicp.h
 # -ffp-contract=off: no FMA contraction, so fp32/fp64 expressions round like PCL's SSE2 Eigen
 HIPFLAGS := -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -ffp-contract=off -Wall -Wno-unused-result
 
-all: $(LIB) oracle
+all: $(LIB) oracle adapter-example
 
 $(LIB): $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS) -lrccl
+
+# plain C++ host program over the C-ABI (g++, no HIP headers): what an integrator links
+adapter/cabi_example: adapter/cabi_example.cpp include/mi355x_gicp.h $(LIB)
+	g++ -O2 -std=c++14 -Wall -Iinclude -o $@ adapter/cabi_example.cpp -L$(PKG) -lmgicp -Wl,-rpath,'$$ORIGIN/../$(PKG)'
+
+adapter-example: adapter/cabi_example
 
 oracle:
 	$(MAKE) -C oracle
@@ -20,4 +26,4 @@ clean:
 	rm -f $(LIB)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean
+.PHONY: all oracle clean adapter-example
