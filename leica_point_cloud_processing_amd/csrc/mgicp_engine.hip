@@ -185,6 +185,8 @@ struct Cloud {
   DevBuf<float4> pts;         // grid-sorted
   DevBuf<uint32_t> perm;      // sorted pos -> original index
   DevBuf<uint32_t> cell_start;
+  DevBuf<uint8_t> empty_dist; // empty-space map (target only: 1-NN queries leave the surface)
+  bool want_empty_map = false;
   DevBuf<double2> cov;        // 3 * n
   GridView view{};
   size_t ncells = 0;
@@ -203,16 +205,27 @@ struct mgicp_ctx {
   Cloud src, tgt;
   Cloud aux;  // scratch cloud of the resolution / radius helpers
   double occupancy = kDefaultOccupancy;  // grid cell sizing target (env MGICP_GRID_OCC)
-  // objective-pass launch shape, A/B-measured on MI355X at 5M points (profiles/README.md):
-  // in-launch finish + 512 blocks beat a separate finish kernel and 2048 blocks
+  // objective-pass launch shape, A/B-measured on MI355X at 5M points (profiles/r01/ab3_*.json):
+  // fence-free in-launch finish at 256 blocks (one per CU) beats 128..2048 blocks and a
+  // separate finish kernel
   bool fused_finish = true;              // in-launch reduction finish (env MGICP_FUSED_FINISH)
-  int fdf_max_blocks = 512;              // objective-pass grid cap (env MGICP_FDF_BLOCKS)
+  int fdf_max_blocks = 256;              // objective-pass grid cap (env MGICP_FDF_BLOCKS)
+  bool compact = true;                   // compacted SoA objective streams (env MGICP_FDF_COMPACT)
   double ms_upload_pending = 0;
   // per source point (sorted), rank shard only
   DevBuf<float4> src_out;  // guess-applied source (only when guess != I)
   const float4* d_out = nullptr;
   DevBuf<float4> qbuf;
   DevBuf<double2> mahal;   // 3 * n
+  // compacted accepted correspondences of the current outer iteration (shard-relative)
+  DevBuf<uint32_t> prev_pos;  // last iteration's matched target position (1-NN seed)
+  DevBuf<uint32_t> flags, cpos;
+  DevBuf<float> corr_f;    // 6 streams
+  DevBuf<double> corr_d;   // 6 streams
+  DevBuf<unsigned char> cscratch;
+  size_t corr_cap = 0;     // elements per stream (multiple of 4)
+  size_t m_local = 0;      // accepted correspondences of this rank
+  bool seed_valid = false;
   DevBuf<int> dbg_nn;
   DevBuf<double> partial;
   DevBuf<double> red;      // kRedVals
@@ -463,6 +476,14 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
   g.nz = nd[2];
   g.cell_start = cl.cell_start.p;
   g.pts = cl.pts.p;
+  g.empty_dist = nullptr;
+  if (cl.want_empty_map) {
+    HIPCK(cl.empty_dist.reserve(nc));
+    HIPCK(ctx->scratch.reserve(nc));
+    HIPCK(launch_empty_map(cl.cell_start.p, nd[0], nd[1], nd[2], cl.empty_dist.p, ctx->scratch.p, s));
+    if ((rc = sync(ctx))) return rc;
+    g.empty_dist = cl.empty_dist.p;
+  }
   cl.ncells = nc;
   cl.dirty = false;
   cl.have_cov = false;
@@ -518,6 +539,17 @@ int ensure_iter_buffers(mgicp_ctx* ctx) {
   HIPCK(ctx->red.reserve(kRedVals));
   int rc = ensure_host_red(ctx);
   if (rc) return rc;
+  const size_t ns = ctx->shard_p1() - ctx->shard_p0();
+  const size_t cap = (ns + 3) / 4 * 4 + 4;
+  HIPCK(ctx->prev_pos.reserve(ns + 1));
+  HIPCK(ctx->flags.reserve(ns + 1));
+  HIPCK(ctx->cpos.reserve(ns + 1));
+  if (ctx->corr_cap < cap) {
+    HIPCK(ctx->corr_f.reserve(6 * cap));
+    HIPCK(ctx->corr_d.reserve(6 * cap));
+    ctx->corr_cap = cap;
+  }
+  HIPCK(ctx->cscratch.reserve(scan_scratch_bytes(ns + 1)));
   if (!ctx->ticket.p) {
     HIPCK(ctx->ticket.reserve(1));
     HIPCK(hipMemsetAsync(ctx->ticket.p, 0, sizeof(unsigned int), ctx->stream));
@@ -555,12 +587,40 @@ Rot33d rot_of(const Mat4& T, const Mat4& G) {
   return R;
 }
 
-int correspond(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, int* dbg) {
+CorrSoA corr_soa(mgicp_ctx* ctx) {
+  const size_t c = ctx->corr_cap;
+  float* f = ctx->corr_f.p;
+  double* d = ctx->corr_d.p;
+  return CorrSoA{f, f + c, f + 2 * c, f + 3 * c, f + 4 * c, f + 5 * c,
+                 d, d + c, d + 2 * c, d + 3 * c, d + 4 * c, d + 5 * c};
+}
+
+// One correspondence sweep (the loop body of computeTransformation before the BFGS call):
+// exact 1-NN + Mahalanobis per source point, then a deterministic compaction of the accepted
+// ones (exclusive scan of the flags, scatter in grid-sorted order) into the SoA streams.
+// `seed` uses the previous sweep's matches as 1-NN starting candidates (exact either way).
+int correspond(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, int* dbg, bool seed) {
   const double thr = ctx->prm.max_corr_dist * ctx->prm.max_corr_dist;
-  ProfScope ps(ctx, kFamCorr);
-  HIPCK(launch_correspond(ctx->tgt.view, ctx->tgt.cov3(), ctx->d_out, ctx->src.cov3(),
-                          ctx->shard_p0(), ctx->shard_p1(), T.xf(), rot_of(T, G), thr,
-                          ctx->qbuf.p, mahal3(ctx), dbg, ctx->stream));
+  const size_t p0 = ctx->shard_p0(), p1 = ctx->shard_p1(), ns = p1 - p0;
+  hipStream_t s = ctx->stream;
+  if (!seed || !ctx->seed_valid) HIPCK(hipMemsetAsync(ctx->prev_pos.p, 0xff, (ns + 1) * sizeof(uint32_t), s));
+  HIPCK(hipMemsetAsync(ctx->flags.p + ns, 0, sizeof(uint32_t), s));
+  {
+    ProfScope ps(ctx, kFamCorr);
+    HIPCK(launch_correspond(ctx->tgt.view, ctx->tgt.cov3(), ctx->d_out, ctx->src.cov3(), p0, p1,
+                            T.xf(), rot_of(T, G), thr, ctx->qbuf.p, mahal3(ctx), dbg,
+                            ctx->prev_pos.p, ctx->flags.p, s));
+  }
+  ctx->seed_valid = true;
+  const size_t sb = scan_scratch_bytes(ns + 1);
+  HIPCK(launch_exclusive_scan(ctx->cscratch.p, sb, ctx->flags.p, ctx->cpos.p, ns + 1, s));
+  HIPCK(launch_compact(ctx->d_out, ctx->qbuf.p, mahal3(ctx), ctx->flags.p, ctx->cpos.p, p0, p1,
+                       corr_soa(ctx), s));
+  uint32_t m = 0;
+  HIPCK(hipMemcpyAsync(&m, ctx->cpos.p + ns, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  int rc = sync(ctx);
+  if (rc) return rc;
+  ctx->m_local = m;
   ctx->have_corr = true;
   return MGICP_OK;
 }
@@ -591,7 +651,7 @@ struct DeviceFunctor {
   int pass(const Vec6& x, double sums[kRedVals]) {
     const Mat4 A = apply_state(x);
     const size_t p0 = ctx->shard_p0(), p1 = ctx->shard_p1();
-    const int nb = fdf_grid_blocks(p1 - p0, ctx->fdf_max_blocks);
+    const int nb = fdf_grid_blocks(ctx->compact ? ctx->m_local : p1 - p0, ctx->fdf_max_blocks);
     int rc;
     if (ctx->fused_finish) {
       // the last block writes the sums straight into mapped pinned host memory (single GPU)
@@ -599,8 +659,12 @@ struct DeviceFunctor {
       double* out = ctx->comm ? ctx->red.p : ctx->d_h_red;
       {
         ProfScope ps(ctx, kFamFdf);
-        HIPCK(launch_fdf(ctx->d_out, ctx->qbuf.p, mahal3(ctx), p0, p1, A.xf(), ctx->partial.p,
-                         nb, ctx->ticket.p, out, ctx->stream));
+        if (ctx->compact)
+          HIPCK(launch_fdf_soa(corr_soa(ctx), ctx->m_local, A.xf(), ctx->partial.p, nb,
+                               ctx->ticket.p, out, ctx->stream));
+        else
+          HIPCK(launch_fdf(ctx->d_out, ctx->qbuf.p, mahal3(ctx), p0, p1, A.xf(), ctx->partial.p,
+                           nb, ctx->ticket.p, out, ctx->stream));
       }
       if (ctx->comm) {
         NCCLCK(ncclAllReduce(ctx->red.p, ctx->red.p, kRedVals, ncclDouble, ncclSum, ctx->comm,
@@ -612,8 +676,12 @@ struct DeviceFunctor {
     } else {
       {
         ProfScope ps(ctx, kFamFdf);
-        HIPCK(launch_fdf(ctx->d_out, ctx->qbuf.p, mahal3(ctx), p0, p1, A.xf(), ctx->partial.p,
-                         nb, nullptr, nullptr, ctx->stream));
+        if (ctx->compact)
+          HIPCK(launch_fdf_soa(corr_soa(ctx), ctx->m_local, A.xf(), ctx->partial.p, nb, nullptr,
+                               nullptr, ctx->stream));
+        else
+          HIPCK(launch_fdf(ctx->d_out, ctx->qbuf.p, mahal3(ctx), p0, p1, A.xf(), ctx->partial.p,
+                           nb, nullptr, nullptr, ctx->stream));
       }
       rc = reduce_to_host(ctx, nb);
     }
@@ -746,6 +814,7 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
     if (v >= 1.0 && v <= 256.0) ctx->occupancy = v;
   }
   if (const char* ff = std::getenv("MGICP_FUSED_FINISH")) ctx->fused_finish = std::atoi(ff) != 0;
+  if (const char* fc = std::getenv("MGICP_FDF_COMPACT")) ctx->compact = std::atoi(fc) != 0;
   if (const char* fb = std::getenv("MGICP_FDF_BLOCKS")) {
     const int v = std::atoi(fb);
     if (v >= 1 && v <= 65536) ctx->fdf_max_blocks = v;
@@ -772,6 +841,8 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
     delete ctx;
     return MGICP_E_HIP;
   }
+  ctx->tgt.want_empty_map = true;  // correspondence / fitness queries start off the surface
+  if (const char* em = std::getenv("MGICP_EMPTY_MAP")) ctx->tgt.want_empty_map = std::atoi(em) != 0;
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
     return MGICP_E_HIP;
@@ -803,13 +874,15 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->stream);
   for (Cloud* c : {&ctx->src, &ctx->tgt, &ctx->aux}) {
     c->raw.release(); c->orig.release(); c->pts.release(); c->perm.release();
-    c->cell_start.release(); c->cov.release();
+    c->cell_start.release(); c->cov.release(); c->empty_dist.release();
   }
   ctx->src_out.release(); ctx->qbuf.release(); ctx->mahal.release(); ctx->dbg_nn.release();
   ctx->partial.release(); ctx->red.release(); ctx->counts.release(); ctx->keys.release();
   ctx->keys_sorted.release(); ctx->vals.release(); ctx->scratch.release(); ctx->u64.release();
   ctx->fpartial.release();
   ctx->ticket.release();
+  ctx->prev_pos.release(); ctx->flags.release(); ctx->cpos.release();
+  ctx->corr_f.release(); ctx->corr_d.release(); ctx->cscratch.release();
   if (ctx->h_red) (void)hipHostFree(ctx->h_red);
   prof_resolve(ctx);
   for (hipEvent_t e : ctx->pool) (void)hipEventDestroy(e);
@@ -862,7 +935,7 @@ int mgicp_align(mgicp_ctx* ctx, const float guess_cm[16], float out_T_cm[16], mg
   bool converged = false;
   int solver_rc = MGICP_OK;
   while (!converged) {
-    if ((rc = correspond(ctx, T, G, nullptr))) return rc;
+    if ((rc = correspond(ctx, T, G, nullptr, nr_iterations > 0))) return rc;
     prev = T;
     int ncorr = 0;
     rc = estimate_bfgs(ctx, T, &ncorr);
@@ -1088,7 +1161,7 @@ int mgicp_debug_correspondences(mgicp_ctx* ctx, const float T_cm[16], int* out_t
   HIPCK(hipMemsetAsync(ctx->dbg_nn.p, 0xff, n * sizeof(int), ctx->stream));
   const Mat4 G = Mat4::identity();
   if ((rc = set_output(ctx, G))) return rc;
-  if ((rc = correspond(ctx, Mat4::from_cm(T_cm), G, ctx->dbg_nn.p))) return rc;
+  if ((rc = correspond(ctx, Mat4::from_cm(T_cm), G, ctx->dbg_nn.p, false))) return rc;
   std::vector<int> nn(n);
   std::vector<double2> M(3 * n);
   std::vector<uint32_t> perm(n);

@@ -23,12 +23,25 @@ struct GridView {
   int nx, ny, nz;
   const uint32_t* cell_start;  // nx*ny*nz + 1
   const float4* pts;           // sorted points
+  // optional empty-space map: per cell, the Chebyshev distance (in cells) to the nearest
+  // non-empty cell, capped at kEmptyCap + 1; rings closer than it hold no point
+  const uint8_t* empty_dist;
 };
+
+constexpr int kEmptyCap = 15;
 
 struct Cov3 {  // SoA triple of double2 arrays
   double2* a;  // {m00, m01}
   double2* b;  // {m02, m11}
   double2* c;  // {m12, m22}
+};
+
+// Accepted correspondences of one outer iteration, compacted in grid-sorted source order and
+// stored as 12 streams (each padded to a multiple of 4 elements) so that an objective pass reads
+// 72 bytes per correspondence with 16-byte loads and no branch.
+struct CorrSoA {
+  float *sx, *sy, *sz, *qx, *qy, *qz;
+  double *m00, *m01, *m02, *m11, *m12, *m22;
 };
 
 // Number of values reduced per objective pass:
@@ -56,10 +69,20 @@ hipError_t launch_xform_points(const float4* in, size_t n, Xf34 T, float4* out,
                                hipStream_t s);
 hipError_t launch_knn_cov(const GridView& g, int k, double eps, size_t p0, size_t p1,
                           Cov3 cov, hipStream_t s);
+// prev_pos (nullable): per source point (shard-relative) the target sorted position matched in
+// the previous outer iteration (UINT32_MAX = none); seeds the exact 1-NN search and is updated.
+// flags (nullable): per source point (shard-relative) 1 if accepted.
 hipError_t launch_correspond(const GridView& tgt, const Cov3& cov_t, const float4* src,
                              const Cov3& cov_s, size_t p0, size_t p1, Xf34 T, Rot33d R,
                              double thr, float4* qbuf, Cov3 mahal, int* dbg_nn,
-                             hipStream_t s);
+                             uint32_t* prev_pos, uint32_t* flags, hipStream_t s);
+// scatter accepted correspondences to their compacted slots (pos = exclusive scan of flags)
+hipError_t launch_compact(const float4* src, const float4* qbuf, const Cov3& mahal,
+                          const uint32_t* flags, const uint32_t* pos, size_t p0, size_t p1,
+                          CorrSoA out, hipStream_t s);
+// objective pass over m compacted correspondences (+ in-launch finish)
+hipError_t launch_fdf_soa(const CorrSoA& c, size_t m, Xf34 A, double* partial, int nb,
+                          unsigned int* ticket, double* out, hipStream_t s);
 int        fdf_grid_blocks(size_t n, int max_blocks = 2048);
 // objective pass + in-launch finish: writes the kRedVals sums to `out` (device or mapped host)
 hipError_t launch_fdf(const float4* src, const float4* qbuf, const Cov3& mahal, size_t p0,
@@ -81,5 +104,8 @@ size_t scan_scratch_bytes(size_t n);
 hipError_t launch_exclusive_scan(void* scratch, size_t scratch_bytes, const uint32_t* in,
                                  uint32_t* out, size_t n, hipStream_t s);
 hipError_t launch_iota(uint32_t* v, size_t n, hipStream_t s);
+// empty-space distance map of a grid (3 separable capped min-max passes); scratch: nc bytes
+hipError_t launch_empty_map(const uint32_t* cell_start, int nx, int ny, int nz, uint8_t* out,
+                            uint8_t* scratch, hipStream_t s);
 
 }  // namespace mgicp

@@ -95,7 +95,12 @@ __device__ __forceinline__ void ring_search(const GridView& g, float qx, float q
                                             V& vis) {
   const int cx = qcell(qx, g.ox, g.inv_h), cy = qcell(qy, g.oy, g.inv_h),
             cz = qcell(qz, g.oz, g.inv_h);
-  const int rmin = max(max(dist_out(cx, g.nx), dist_out(cy, g.ny)), dist_out(cz, g.nz));
+  int rmin = max(max(dist_out(cx, g.nx), dist_out(cy, g.ny)), dist_out(cz, g.nz));
+  if (rmin == 0 && g.empty_dist) {
+    // rings nearer than the closest non-empty cell hold no point: start there (exact)
+    rmin = g.empty_dist[static_cast<size_t>(cx) +
+                        static_cast<size_t>(g.nx) * (static_cast<size_t>(cy) + static_cast<size_t>(g.ny) * cz)];
+  }
   for (int r = rmin; r < (1 << 22); ++r) {
     if (r > 0) {
       const float L = fminf(fminf(axis_bound(qx, g.ox, g.h, cx, r - 1, g.nx),
@@ -172,12 +177,20 @@ struct KnnVisitor {
     }
     if (c < key[0]) { key[0] = c; pos[0] = cp; }
   }
+  __device__ __forceinline__ void test(const float4& p, uint32_t j) {
+    const unsigned long long c = mkkey(dist2(qx, qy, qz, p), p.w);
+    if (c < key[K - 1]) insert(c, j);
+  }
   __device__ __forceinline__ void range(const GridView& g, uint32_t a, uint32_t b) {
-    for (uint32_t j = a; j < b; ++j) {
-      const float4 p = g.pts[j];
-      const unsigned long long c = mkkey(dist2(qx, qy, qz, p), p.w);
-      if (c < key[K - 1]) insert(c, j);
+    uint32_t j = a;
+    for (; j + 4 <= b; j += 4) {  // four gathers in flight per lane (latency-bound loop)
+      const float4 p0 = g.pts[j], p1 = g.pts[j + 1], p2 = g.pts[j + 2], p3 = g.pts[j + 3];
+      test(p0, j);
+      test(p1, j + 1);
+      test(p2, j + 2);
+      test(p3, j + 3);
     }
+    for (; j < b; ++j) test(g.pts[j], j);
   }
 };
 
@@ -203,12 +216,20 @@ struct NnVisitor {
     if (best == ~0ull) return false;
     return __uint_as_float(static_cast<uint32_t>(best >> 32)) < Ls * Ls;
   }
+  __device__ __forceinline__ void test(const float4& p, uint32_t j) {
+    const unsigned long long c = mkkey(dist2(qx, qy, qz, p), p.w);
+    if (c < best) { best = c; pos = j; }
+  }
   __device__ __forceinline__ void range(const GridView& g, uint32_t a, uint32_t b) {
-    for (uint32_t j = a; j < b; ++j) {
-      const float4 p = g.pts[j];
-      const unsigned long long c = mkkey(dist2(qx, qy, qz, p), p.w);
-      if (c < best) { best = c; pos = j; }
+    uint32_t j = a;
+    for (; j + 4 <= b; j += 4) {  // four gathers in flight per lane (latency-bound loop)
+      const float4 p0 = g.pts[j], p1 = g.pts[j + 1], p2 = g.pts[j + 2], p3 = g.pts[j + 3];
+      test(p0, j);
+      test(p1, j + 1);
+      test(p2, j + 2);
+      test(p3, j + 3);
     }
+    for (; j < b; ++j) test(g.pts[j], j);
   }
 };
 
@@ -309,6 +330,27 @@ __global__ void xform_points_kernel(const float4* in, size_t n, Xf34 T, float4* 
   float x, y, z;
   xform(T, p.x, p.y, p.z, x, y, z);
   out[i] = make_float4(x, y, z, p.w);
+}
+
+// empty-space map, pass 0: 0 for non-empty cells, 255 for empty ones
+__global__ void empty_init_kernel(const uint32_t* __restrict__ cs, size_t nc, uint8_t* __restrict__ e) {
+  const size_t c = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (c < nc) e[c] = cs[c + 1] > cs[c] ? 0 : 255;
+}
+
+// one separable pass of the Chebyshev (L-inf) distance transform along an axis of extent n and
+// element stride `stride`: out(c) = min_{|d| <= cap} max(|d|, in(c + d*stride)), capped at cap+1
+__global__ void empty_pass_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                  size_t nc, int n, size_t stride, int cap) {
+  const size_t c = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (c >= nc) return;
+  const int x = static_cast<int>((c / stride) % static_cast<size_t>(n));
+  int best = min(static_cast<int>(in[c]), cap + 1);
+  for (int d = 1; d <= cap && d < best; ++d) {
+    if (x - d >= 0) best = min(best, max(d, static_cast<int>(in[c - d * stride])));
+    if (x + d < n) best = min(best, max(d, static_cast<int>(in[c + d * stride])));
+  }
+  out[c] = static_cast<uint8_t>(min(best, cap + 1));
 }
 
 __global__ void iota_kernel(uint32_t* v, size_t n) {
@@ -446,7 +488,8 @@ __global__ __launch_bounds__(256) void correspond_kernel(GridView tg, Cov3 cov_t
                                                          Cov3 cov_s, size_t p0, size_t p1,
                                                          Xf34 T, Rot33d R, double thr,
                                                          float4* __restrict__ qbuf, Cov3 mahal,
-                                                         int* dbg_nn) {
+                                                         int* dbg_nn, uint32_t* __restrict__ prev_pos,
+                                                         uint32_t* __restrict__ flags) {
   const size_t p = p0 + static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (p >= p1) return;
   const float4 s = src[p];
@@ -454,9 +497,17 @@ __global__ __launch_bounds__(256) void correspond_kernel(GridView tg, Cov3 cov_t
   xform(T, s.x, s.y, s.z, qx, qy, qz);
   NnVisitor vis;
   vis.init(qx, qy, qz, thr);
+  if (prev_pos) {
+    // seed with last iteration's match: a real candidate, so the exact search only tightens it,
+    // and the ball-cell pruning starts from a near-final radius
+    const uint32_t pp = prev_pos[p - p0];
+    if (pp != 0xffffffffu) vis.range(tg, pp, pp + 1);
+  }
   ring_search(tg, qx, qy, qz, vis);
   const bool ok = vis.best != ~0ull &&
                   static_cast<double>(__uint_as_float(static_cast<uint32_t>(vis.best >> 32))) < thr;
+  if (prev_pos) prev_pos[p - p0] = ok ? vis.pos : 0xffffffffu;
+  if (flags) flags[p - p0] = ok ? 1u : 0u;
   if (!ok) {
     qbuf[p] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (dbg_nn) {
@@ -537,35 +588,58 @@ __device__ __forceinline__ void block_reduce_store(double (&acc)[kRedVals], doub
   }
 }
 
-// In-launch deterministic finish (cdna_hip_programming.md Guideline 16, split-K counter form):
-// every block publishes its partial with an agent-scope release and takes a ticket; the block
-// that draws the last ticket acquires, sums all partials in block order and writes `out`
-// (device memory or mapped pinned host memory), then re-arms the ticket for the next launch.
+// In-launch deterministic finish, fence-free form of cdna_hip_programming.md Guideline 16
+// (MI355X_MICROARCH.md "Valid forms", first table row): the 16 partial sums of each block are
+// stored write-through (sc1, relaxed agent-scope atomic stores) by wave 0, which drains them
+// (s_waitcnt vmcnt(0)) before one lane takes an agent-scope ticket; the block drawing the last
+// ticket reads every partial with sc1 loads (relaxed agent-scope atomic loads), sums them in block
+// order and writes `out` (device memory or mapped pinned host memory), then re-arms the ticket.
+// No buffer_wbl2 / buffer_inv: a release fence per block cost ~25 us per launch at 1024 blocks.
+__device__ __forceinline__ void store_partial_sc1(double (&acc)[kRedVals], double* dst) {
+  __shared__ double sm[4][kRedVals];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __syncthreads();
+#pragma unroll
+  for (int v = 0; v < kRedVals; ++v) {
+    const double w = wave_sum(acc[v]);
+    if (lane == 0) sm[wid][v] = w;
+  }
+  __syncthreads();
+  if (threadIdx.x < kRedVals) {
+    const int v = threadIdx.x;
+    double s = sm[0][v];
+    s = s + sm[1][v];
+    s = s + sm[2][v];
+    s = s + sm[3][v];
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(dst + v),
+                       static_cast<unsigned long long>(__double_as_longlong(s)), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 __device__ __forceinline__ void finish_in_last_block(const double* partial, unsigned int* ticket,
                                                      double* out) {
   __shared__ int last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  if (threadIdx.x < 64) {  // wave 0 issued every partial store of this block
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = (prev == gridDim.x - 1) ? 1 : 0;
+    if (threadIdx.x == 0) {
+      const unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = (prev == gridDim.x - 1) ? 1 : 0;
+    }
   }
   __syncthreads();
   if (!last) return;
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
   double acc[kRedVals];
 #pragma unroll
   for (int v = 0; v < kRedVals; ++v) acc[v] = 0.0;
   const int nb = gridDim.x;
+  const unsigned long long* pp = reinterpret_cast<const unsigned long long*>(partial);
   for (int b = threadIdx.x; b < nb; b += blockDim.x) {
 #pragma unroll
-    for (int v = 0; v < kRedVals; ++v) acc[v] += partial[static_cast<size_t>(b) * kRedVals + v];
+    for (int v = 0; v < kRedVals; ++v)
+      acc[v] += __longlong_as_double(static_cast<long long>(__hip_atomic_load(
+          const_cast<unsigned long long*>(pp + static_cast<size_t>(b) * kRedVals + v),
+          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
   }
   block_reduce_store(acc, out);
   if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -605,8 +679,95 @@ __global__ __launch_bounds__(256) void fdf_kernel(const float4* __restrict__ src
     acc[10] += sz * t0; acc[11] += sz * t1; acc[12] += sz * t2;
     acc[13] += 1.0;
   }
-  block_reduce_store(acc, partial + static_cast<size_t>(blockIdx.x) * kRedVals);
-  if (ticket) finish_in_last_block(partial, ticket, out);
+  if (ticket) {
+    store_partial_sc1(acc, partial + static_cast<size_t>(blockIdx.x) * kRedVals);
+    finish_in_last_block(partial, ticket, out);
+  } else {
+    block_reduce_store(acc, partial + static_cast<size_t>(blockIdx.x) * kRedVals);
+  }
+}
+
+__global__ void compact_kernel(const float4* __restrict__ src, const float4* __restrict__ qbuf,
+                               Cov3 mahal, const uint32_t* __restrict__ flags,
+                               const uint32_t* __restrict__ pos, size_t p0, size_t p1, CorrSoA o) {
+  const size_t p = p0 + static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (p >= p1 || !flags[p - p0]) return;
+  const size_t i = pos[p - p0];
+  const float4 s = src[p], q = qbuf[p];
+  const double2 a = mahal.a[p], b = mahal.b[p], c = mahal.c[p];
+  o.sx[i] = s.x; o.sy[i] = s.y; o.sz[i] = s.z;
+  o.qx[i] = q.x; o.qy[i] = q.y; o.qz[i] = q.z;
+  o.m00[i] = a.x; o.m01[i] = a.y; o.m02[i] = b.x;
+  o.m11[i] = b.y; o.m12[i] = c.x; o.m22[i] = c.y;
+}
+
+// one correspondence of the objective (identical arithmetic to fdf_kernel)
+__device__ __forceinline__ void fdf_point(const Xf34& A, float sx, float sy, float sz, float qx,
+                                          float qy, float qz, double m00, double m01, double m02,
+                                          double m11, double m12, double m22,
+                                          double (&acc)[kRedVals]) {
+  float px, py, pz;
+  xform(A, sx, sy, sz, px, py, pz);
+  const double r0 = static_cast<double>(px - qx);
+  const double r1 = static_cast<double>(py - qy);
+  const double r2 = static_cast<double>(pz - qz);
+  double t0 = m00 * r0; t0 = t0 + m01 * r1; t0 = t0 + m02 * r2;
+  double t1 = m01 * r0; t1 = t1 + m11 * r1; t1 = t1 + m12 * r2;
+  double t2 = m02 * r0; t2 = t2 + m12 * r1; t2 = t2 + m22 * r2;
+  double d = r0 * t0; d = d + r1 * t1; d = d + r2 * t2;
+  const double dx = sx, dy = sy, dz = sz;
+  acc[0] += d;
+  acc[1] += t0; acc[2] += t1; acc[3] += t2;
+  acc[4] += dx * t0; acc[5] += dx * t1; acc[6] += dx * t2;
+  acc[7] += dy * t0; acc[8] += dy * t1; acc[9] += dy * t2;
+  acc[10] += dz * t0; acc[11] += dz * t1; acc[12] += dz * t2;
+  acc[13] += 1.0;
+}
+
+// Objective pass over the compacted streams: 4 correspondences per thread-iteration, every load
+// 16 bytes per lane (float4 of 4 coordinates, double2 of 2 matrix entries).
+__global__ __launch_bounds__(256) void fdf_soa_kernel(CorrSoA c, size_t m, Xf34 A,
+                                                      double* __restrict__ partial,
+                                                      unsigned int* __restrict__ ticket,
+                                                      double* __restrict__ out) {
+  double acc[kRedVals];
+#pragma unroll
+  for (int v = 0; v < kRedVals; ++v) acc[v] = 0.0;
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  const size_t m4 = m / 4;
+  for (size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < m4; i += stride) {
+    const float4 sx = reinterpret_cast<const float4*>(c.sx)[i];
+    const float4 sy = reinterpret_cast<const float4*>(c.sy)[i];
+    const float4 sz = reinterpret_cast<const float4*>(c.sz)[i];
+    const float4 qx = reinterpret_cast<const float4*>(c.qx)[i];
+    const float4 qy = reinterpret_cast<const float4*>(c.qy)[i];
+    const float4 qz = reinterpret_cast<const float4*>(c.qz)[i];
+    const double2* M00 = reinterpret_cast<const double2*>(c.m00) + 2 * i;
+    const double2* M01 = reinterpret_cast<const double2*>(c.m01) + 2 * i;
+    const double2* M02 = reinterpret_cast<const double2*>(c.m02) + 2 * i;
+    const double2* M11 = reinterpret_cast<const double2*>(c.m11) + 2 * i;
+    const double2* M12 = reinterpret_cast<const double2*>(c.m12) + 2 * i;
+    const double2* M22 = reinterpret_cast<const double2*>(c.m22) + 2 * i;
+    const double2 a0 = M00[0], a1 = M00[1], b0 = M01[0], b1 = M01[1], e0 = M02[0], e1 = M02[1];
+    const double2 f0 = M11[0], f1 = M11[1], g0 = M12[0], g1 = M12[1], h0 = M22[0], h1 = M22[1];
+    fdf_point(A, sx.x, sy.x, sz.x, qx.x, qy.x, qz.x, a0.x, b0.x, e0.x, f0.x, g0.x, h0.x, acc);
+    fdf_point(A, sx.y, sy.y, sz.y, qx.y, qy.y, qz.y, a0.y, b0.y, e0.y, f0.y, g0.y, h0.y, acc);
+    fdf_point(A, sx.z, sy.z, sz.z, qx.z, qy.z, qz.z, a1.x, b1.x, e1.x, f1.x, g1.x, h1.x, acc);
+    fdf_point(A, sx.w, sy.w, sz.w, qx.w, qy.w, qz.w, a1.y, b1.y, e1.y, f1.y, g1.y, h1.y, acc);
+  }
+  // tail (m % 4 correspondences) on the first threads of the grid
+  const size_t t = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t < m - 4 * m4) {
+    const size_t j = 4 * m4 + t;
+    fdf_point(A, c.sx[j], c.sy[j], c.sz[j], c.qx[j], c.qy[j], c.qz[j], c.m00[j], c.m01[j], c.m02[j],
+              c.m11[j], c.m12[j], c.m22[j], acc);
+  }
+  if (ticket) {
+    store_partial_sc1(acc, partial + static_cast<size_t>(blockIdx.x) * kRedVals);
+    finish_in_last_block(partial, ticket, out);
+  } else {
+    block_reduce_store(acc, partial + static_cast<size_t>(blockIdx.x) * kRedVals);
+  }
 }
 
 __global__ __launch_bounds__(256) void fitness_kernel(GridView tg, const float4* __restrict__ src,
@@ -725,6 +886,19 @@ hipError_t launch_xform_points(const float4* in, size_t n, Xf34 T, float4* out, 
   return hipGetLastError();
 }
 
+hipError_t launch_empty_map(const uint32_t* cell_start, int nx, int ny, int nz, uint8_t* out,
+                            uint8_t* scratch, hipStream_t s) {
+  const size_t nc = static_cast<size_t>(nx) * ny * nz;
+  if (!nc) return hipSuccess;
+  empty_init_kernel<<<nblk(nc), 256, 0, s>>>(cell_start, nc, out);
+  empty_pass_kernel<<<nblk(nc), 256, 0, s>>>(out, scratch, nc, nx, 1, kEmptyCap);
+  empty_pass_kernel<<<nblk(nc), 256, 0, s>>>(scratch, out, nc, ny, static_cast<size_t>(nx), kEmptyCap);
+  empty_pass_kernel<<<nblk(nc), 256, 0, s>>>(out, scratch, nc, nz, static_cast<size_t>(nx) * ny, kEmptyCap);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return hipMemcpyAsync(out, scratch, nc, hipMemcpyDeviceToDevice, s);
+}
+
 hipError_t launch_iota(uint32_t* v, size_t n, hipStream_t s) {
   if (!n) return hipSuccess;
   iota_kernel<<<nblk(n), 256, 0, s>>>(v, n);
@@ -754,10 +928,25 @@ hipError_t launch_knn_cov(const GridView& g, int k, double eps, size_t p0, size_
 
 hipError_t launch_correspond(const GridView& tgt, const Cov3& cov_t, const float4* src,
                              const Cov3& cov_s, size_t p0, size_t p1, Xf34 T, Rot33d R,
-                             double thr, float4* qbuf, Cov3 mahal, int* dbg_nn, hipStream_t s) {
+                             double thr, float4* qbuf, Cov3 mahal, int* dbg_nn,
+                             uint32_t* prev_pos, uint32_t* flags, hipStream_t s) {
   if (p1 <= p0) return hipSuccess;
   correspond_kernel<<<nblk(p1 - p0), 256, 0, s>>>(tgt, cov_t, src, cov_s, p0, p1, T, R, thr,
-                                                  qbuf, mahal, dbg_nn);
+                                                  qbuf, mahal, dbg_nn, prev_pos, flags);
+  return hipGetLastError();
+}
+
+hipError_t launch_compact(const float4* src, const float4* qbuf, const Cov3& mahal,
+                          const uint32_t* flags, const uint32_t* pos, size_t p0, size_t p1,
+                          CorrSoA out, hipStream_t s) {
+  if (p1 <= p0) return hipSuccess;
+  compact_kernel<<<nblk(p1 - p0), 256, 0, s>>>(src, qbuf, mahal, flags, pos, p0, p1, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_fdf_soa(const CorrSoA& c, size_t m, Xf34 A, double* partial, int nb,
+                          unsigned int* ticket, double* out, hipStream_t s) {
+  fdf_soa_kernel<<<nb, 256, 0, s>>>(c, m, A, partial, ticket, out);
   return hipGetLastError();
 }
 

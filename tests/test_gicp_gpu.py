@@ -74,15 +74,32 @@ def test_covariances_bitexact(engine_mod, cube_clouds, part_small):
 def test_correspondences_exact(engine_mod, part_small):
     src, tgt, Ttrue = part_small
     o, e = _pair(engine_mod, src, tgt)
-    for T in [np.eye(4, dtype=np.float32), np.linalg.inv(Ttrue).astype(np.float32)]:
+    off = np.eye(4, dtype=np.float32)
+    off[:3, 3] = [0.0, 0.0, 0.035]  # most points near the 4 cm gate: empty-space map + rejection
+    far = np.eye(4, dtype=np.float32)
+    far[:3, 3] = [0.3, -0.2, 0.5]  # nothing within the gate
+    for T in [np.eye(4, dtype=np.float32), np.linalg.inv(Ttrue).astype(np.float32), off, far]:
         m_ref, tj_ref, _, M_ref = o.correspondences(T)
         m_gpu, tj_gpu, M_gpu = e.debug_correspondences(T, len(src))
         assert m_gpu == m_ref
         np.testing.assert_array_equal(tj_gpu, tj_ref)
         ok = tj_ref >= 0
-        Mu = _upper(M_ref)[ok]
-        rel = np.abs(M_gpu[ok] - Mu).max() / np.abs(Mu).max()
-        assert rel <= 1e-12, rel
+        if ok.any():
+            Mu = _upper(M_ref)[ok]
+            rel = np.abs(M_gpu[ok] - Mu).max() / np.abs(Mu).max()
+            assert rel <= 1e-12, rel
+
+
+def test_fitness_far_source(engine_mod, part_small):
+    """Unbounded 1-NN (getFitnessScore) for a source 1-3 m away from the target: the capped
+    empty-space map only lower-bounds the search, results stay exact."""
+    src, tgt, _ = part_small
+    o, e = _pair(engine_mod, src, tgt)
+    for t in ([1.0, 0.0, 0.0], [0.0, -2.0, 1.0], [0.05, 0.0, 0.0]):
+        T = np.eye(4, dtype=np.float32)
+        T[:3, 3] = t
+        f_ref, f_gpu = o.fitness(T), e.fitness(T)
+        assert abs(f_gpu - f_ref) <= 1e-9 * f_ref, (t, f_gpu, f_ref)
 
 
 def test_objective_pass(engine_mod, part_small):
@@ -98,6 +115,22 @@ def test_objective_pass(engine_mod, part_small):
         f_gpu, g_gpu = e.debug_fdf(x)
         assert abs(f_gpu - f_ref) <= 1e-10 * abs(f_ref)
         assert np.abs(g_gpu - g_ref).max() <= 1e-9 * max(1.0, np.abs(g_ref).max())
+
+
+def test_inlaunch_finish_no_stale_partials(engine_mod, part_small):
+    """The in-launch reduction finish (sc1 partials + agent ticket) must never read a partial of
+    a previous launch: alternate two states many times, every repeat bit-identical."""
+    src, tgt, _ = part_small
+    e = engine_mod()
+    e.set_source_xyz(src)
+    e.set_target_xyz(tgt)
+    e.debug_correspondences(np.eye(4, dtype=np.float32), len(src))
+    xs = [np.array([0.001, -0.002, 0.0005, 0.0003, -0.0002, 0.0004]), np.zeros(6)]
+    first = [e.debug_fdf_sums(x) for x in xs]
+    assert not np.array_equal(first[0], first[1])
+    for k in range(200):
+        s = e.debug_fdf_sums(xs[k % 2])
+        assert np.array_equal(s, first[k % 2]), k
 
 
 @pytest.mark.parametrize("case", ["K1_test_config", "K2_defaults"])
