@@ -28,11 +28,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
-# algorithmic bytes of one fdf objective pass (DESIGN.md "Kernels"): per accepted source point
-# s float4 (16) + matched target float4 (16) + Mahalanobis upper triangle fp64 (48); a rejected
-# point only has its float4 match flag read (16)
-FDF_BYTES_ACCEPTED = 80
-FDF_BYTES_REJECTED = 16
+# algorithmic bytes of one objective pass (DESIGN.md "Kernels"): per accepted correspondence
+# source xyz fp32 (12) + matched target xyz fp32 (12) + Mahalanobis upper triangle fp64 (48);
+# rejected source points are compacted away once per outer iteration and cost nothing per pass
+FDF_BYTES_ACCEPTED = 72
+FDF_BYTES_REJECTED = 0
 
 
 def parse():
@@ -46,6 +46,8 @@ def parse():
                     help="points per cloud of the bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=1)
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01_pmc_fdf.json"))
+    ap.add_argument("--no-events", action="store_true",
+                    help="time the steps without per-launch HIP events (A/B of the event overhead)")
     return ap.parse_args()
 
 
@@ -109,7 +111,7 @@ def main():
     # timed region: K full align loops, HIP events on the engine's stream around every kernel.
     # align() is host-synchronous (it returns with T on the host after its stream drained), so
     # the barrier on each side is the whole device synchronisation.
-    eng.set_profiling(True)
+    eng.set_profiling(not args.no_events)
     pg.barrier()
     t0 = time.perf_counter()
     total_iters = 0

@@ -210,7 +210,9 @@ struct mgicp_ctx {
   // separate finish kernel
   bool fused_finish = true;              // in-launch reduction finish (env MGICP_FUSED_FINISH)
   int fdf_max_blocks = 256;              // objective-pass grid cap (env MGICP_FDF_BLOCKS)
-  bool compact = true;                   // compacted SoA objective streams (env MGICP_FDF_COMPACT)
+  // alternate the objective-pass direction: 360 MB of streams at 5M points exceed the 256 MiB
+  // Infinity Cache, so each pass re-reads the previous pass's tail from it (73 -> 68 us)
+  bool alt_sweep = true;                 // (env MGICP_FDF_ALT)
   double ms_upload_pending = 0;
   // per source point (sorted), rank shard only
   DevBuf<float4> src_out;  // guess-applied source (only when guess != I)
@@ -231,6 +233,10 @@ struct mgicp_ctx {
   DevBuf<double> red;      // kRedVals
   double* h_red = nullptr;   // pinned, mapped, coherent host memory
   double* d_h_red = nullptr; // its device address
+  unsigned long long* h_flag = nullptr;  // pass-completion word (host / device views)
+  unsigned long long* d_flag = nullptr;
+  unsigned long long pass_seq = 0;
+  bool poll = true;          // poll the completion word instead of hipStreamSynchronize (env MGICP_POLL)
   DevBuf<unsigned int> ticket;  // arrival counter of the in-launch reduction finish
   // build scratch
   DevBuf<uint32_t> counts, keys, keys_sorted, vals;
@@ -524,9 +530,30 @@ int prepare(mgicp_ctx* ctx, bool need_cov) {
 
 int ensure_host_red(mgicp_ctx* ctx) {
   if (ctx->h_red) return MGICP_OK;
-  HIPCK(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_red), kRedVals * sizeof(double),
+  // kRedVals sums followed by the pass-completion word (see launch_fdf_soa's done_flag)
+  HIPCK(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_red), 2 * kRedVals * sizeof(double),
                       hipHostMallocMapped | hipHostMallocCoherent));
   HIPCK(hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->d_h_red), ctx->h_red, 0));
+  std::memset(ctx->h_red, 0, 2 * kRedVals * sizeof(double));
+  ctx->h_flag = reinterpret_cast<unsigned long long*>(ctx->h_red + kRedVals);
+  ctx->d_flag = reinterpret_cast<unsigned long long*>(ctx->d_h_red + kRedVals);
+  return MGICP_OK;
+}
+
+// Wait for pass `seq` to publish its sums: spin on the mapped completion word; after ~0.5 s fall
+// back to a stream synchronisation so a failed launch surfaces as an error instead of a hang.
+int wait_pass(mgicp_ctx* ctx, unsigned long long seq) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned spins = 0;; ++spins) {
+    if (__atomic_load_n(ctx->h_flag, __ATOMIC_ACQUIRE) == seq) return MGICP_OK;
+    if ((spins & 1023u) == 1023u &&
+        std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(500))
+      break;
+  }
+  int rc = sync(ctx);
+  if (rc) return rc;
+  if (__atomic_load_n(ctx->h_flag, __ATOMIC_ACQUIRE) != seq)
+    return fail(ctx, MGICP_E_HIP, "objective pass finished without publishing its sums");
   return MGICP_OK;
 }
 
@@ -650,21 +677,22 @@ struct DeviceFunctor {
 
   int pass(const Vec6& x, double sums[kRedVals]) {
     const Mat4 A = apply_state(x);
-    const size_t p0 = ctx->shard_p0(), p1 = ctx->shard_p1();
-    const int nb = fdf_grid_blocks(ctx->compact ? ctx->m_local : p1 - p0, ctx->fdf_max_blocks);
+    const int nb = fdf_grid_blocks(ctx->m_local, ctx->fdf_max_blocks);
     int rc;
+    // alternate the sweep direction so each pass starts on the Infinity-Cache-resident tail
+    // of the previous one (deterministic: the direction follows the pass index)
+    const int reverse = ctx->alt_sweep ? (ctx->n_evals & 1) : 0;
     if (ctx->fused_finish) {
       // the last block writes the sums straight into mapped pinned host memory (single GPU)
       // or device memory (multi-GPU: then one 16-double RCCL all-reduce and a D2H copy)
       double* out = ctx->comm ? ctx->red.p : ctx->d_h_red;
+      const bool poll = ctx->poll && !ctx->comm;
+      const unsigned long long seq = ++ctx->pass_seq;
       {
         ProfScope ps(ctx, kFamFdf);
-        if (ctx->compact)
-          HIPCK(launch_fdf_soa(corr_soa(ctx), ctx->m_local, A.xf(), ctx->partial.p, nb,
-                               ctx->ticket.p, out, ctx->stream));
-        else
-          HIPCK(launch_fdf(ctx->d_out, ctx->qbuf.p, mahal3(ctx), p0, p1, A.xf(), ctx->partial.p,
-                           nb, ctx->ticket.p, out, ctx->stream));
+        HIPCK(launch_fdf_soa(corr_soa(ctx), ctx->m_local, A.xf(), ctx->partial.p, nb,
+                             ctx->ticket.p, out, reverse, poll ? ctx->d_flag : nullptr, seq,
+                             ctx->stream));
       }
       if (ctx->comm) {
         NCCLCK(ncclAllReduce(ctx->red.p, ctx->red.p, kRedVals, ncclDouble, ncclSum, ctx->comm,
@@ -672,16 +700,12 @@ struct DeviceFunctor {
         HIPCK(hipMemcpyAsync(ctx->h_red, ctx->red.p, kRedVals * sizeof(double),
                              hipMemcpyDeviceToHost, ctx->stream));
       }
-      rc = sync(ctx);
+      rc = poll ? wait_pass(ctx, seq) : sync(ctx);
     } else {
       {
         ProfScope ps(ctx, kFamFdf);
-        if (ctx->compact)
-          HIPCK(launch_fdf_soa(corr_soa(ctx), ctx->m_local, A.xf(), ctx->partial.p, nb, nullptr,
-                               nullptr, ctx->stream));
-        else
-          HIPCK(launch_fdf(ctx->d_out, ctx->qbuf.p, mahal3(ctx), p0, p1, A.xf(), ctx->partial.p,
-                           nb, nullptr, nullptr, ctx->stream));
+        HIPCK(launch_fdf_soa(corr_soa(ctx), ctx->m_local, A.xf(), ctx->partial.p, nb, nullptr,
+                             nullptr, reverse, nullptr, 0, ctx->stream));
       }
       rc = reduce_to_host(ctx, nb);
     }
@@ -814,7 +838,8 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
     if (v >= 1.0 && v <= 256.0) ctx->occupancy = v;
   }
   if (const char* ff = std::getenv("MGICP_FUSED_FINISH")) ctx->fused_finish = std::atoi(ff) != 0;
-  if (const char* fc = std::getenv("MGICP_FDF_COMPACT")) ctx->compact = std::atoi(fc) != 0;
+  if (const char* fa = std::getenv("MGICP_FDF_ALT")) ctx->alt_sweep = std::atoi(fa) != 0;
+  if (const char* po = std::getenv("MGICP_POLL")) ctx->poll = std::atoi(po) != 0;
   if (const char* fb = std::getenv("MGICP_FDF_BLOCKS")) {
     const int v = std::atoi(fb);
     if (v >= 1 && v <= 65536) ctx->fdf_max_blocks = v;
@@ -965,6 +990,8 @@ int mgicp_align(mgicp_ctx* ctx, const float guess_cm[16], float out_T_cm[16], mg
       prev = T;
     }
   }
+  // polled passes leave their kernels' completion unobserved: drain the stream once
+  if ((rc = sync(ctx))) return rc;
   // final_transformation_ = previous_transformation_ (3x3) * guess (3x3); t = prev t + guess t
   Mat4 F = Mat4::identity();
   for (int i = 0; i < 3; ++i)

@@ -81,13 +81,12 @@ hipError_t launch_compact(const float4* src, const float4* qbuf, const Cov3& mah
                           const uint32_t* flags, const uint32_t* pos, size_t p0, size_t p1,
                           CorrSoA out, hipStream_t s);
 // objective pass over m compacted correspondences (+ in-launch finish)
+// done_flag (nullable, mapped host memory): the last block stores `seq` there with a
+// system-scope release after `out`, so the host can poll instead of synchronising the stream
 hipError_t launch_fdf_soa(const CorrSoA& c, size_t m, Xf34 A, double* partial, int nb,
-                          unsigned int* ticket, double* out, hipStream_t s);
+                          unsigned int* ticket, double* out, int reverse,
+                          unsigned long long* done_flag, unsigned long long seq, hipStream_t s);
 int        fdf_grid_blocks(size_t n, int max_blocks = 2048);
-// objective pass + in-launch finish: writes the kRedVals sums to `out` (device or mapped host)
-hipError_t launch_fdf(const float4* src, const float4* qbuf, const Cov3& mahal, size_t p0,
-                      size_t p1, Xf34 A, double* partial, int nb, unsigned int* ticket,
-                      double* out, hipStream_t s);
 hipError_t launch_fitness(const GridView& tgt, const float4* src, size_t p0, size_t p1,
                           Xf34 T, double max_range, double* partial, int nb, hipStream_t s);
 hipError_t launch_reduce_finish(const double* partial, int nb, double* out, hipStream_t s);

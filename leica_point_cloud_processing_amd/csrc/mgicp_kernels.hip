@@ -618,7 +618,9 @@ __device__ __forceinline__ void store_partial_sc1(double (&acc)[kRedVals], doubl
 }
 
 __device__ __forceinline__ void finish_in_last_block(const double* partial, unsigned int* ticket,
-                                                     double* out) {
+                                                     double* out,
+                                                     unsigned long long* done_flag = nullptr,
+                                                     unsigned long long seq = 0) {
   __shared__ int last;
   if (threadIdx.x < 64) {  // wave 0 issued every partial store of this block
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -643,47 +645,10 @@ __device__ __forceinline__ void finish_in_last_block(const double* partial, unsi
   }
   block_reduce_store(acc, out);
   if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__global__ __launch_bounds__(256) void fdf_kernel(const float4* __restrict__ src,
-                                                  const float4* __restrict__ qbuf, Cov3 mahal,
-                                                  size_t p0, size_t p1, Xf34 A,
-                                                  double* __restrict__ partial,
-                                                  unsigned int* __restrict__ ticket,
-                                                  double* __restrict__ out) {
-  double acc[kRedVals];
-#pragma unroll
-  for (int v = 0; v < kRedVals; ++v) acc[v] = 0.0;
-  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
-  for (size_t p = p0 + static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; p < p1;
-       p += stride) {
-    const float4 q = qbuf[p];
-    if (q.w == 0.f) continue;
-    const float4 s = src[p];
-    const double2 ma = mahal.a[p], mb = mahal.b[p], mc = mahal.c[p];
-    float px, py, pz;
-    xform(A, s.x, s.y, s.z, px, py, pz);
-    const double r0 = static_cast<double>(px - q.x);
-    const double r1 = static_cast<double>(py - q.y);
-    const double r2 = static_cast<double>(pz - q.z);
-    const double m00 = ma.x, m01 = ma.y, m02 = mb.x, m11 = mb.y, m12 = mc.x, m22 = mc.y;
-    double t0 = m00 * r0; t0 = t0 + m01 * r1; t0 = t0 + m02 * r2;
-    double t1 = m01 * r0; t1 = t1 + m11 * r1; t1 = t1 + m12 * r2;
-    double t2 = m02 * r0; t2 = t2 + m12 * r1; t2 = t2 + m22 * r2;
-    double d = r0 * t0; d = d + r1 * t1; d = d + r2 * t2;
-    const double sx = s.x, sy = s.y, sz = s.z;
-    acc[0] += d;
-    acc[1] += t0; acc[2] += t1; acc[3] += t2;
-    acc[4] += sx * t0; acc[5] += sx * t1; acc[6] += sx * t2;
-    acc[7] += sy * t0; acc[8] += sy * t1; acc[9] += sy * t2;
-    acc[10] += sz * t0; acc[11] += sz * t1; acc[12] += sz * t2;
-    acc[13] += 1.0;
-  }
-  if (ticket) {
-    store_partial_sc1(acc, partial + static_cast<size_t>(blockIdx.x) * kRedVals);
-    finish_in_last_block(partial, ticket, out);
-  } else {
-    block_reduce_store(acc, partial + static_cast<size_t>(blockIdx.x) * kRedVals);
+  if (done_flag && threadIdx.x < 64) {
+    // wave 0 wrote every out[v]; once they are drained, publish the pass number to the host
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (threadIdx.x == 0) __hip_atomic_store(done_flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -701,7 +666,8 @@ __global__ void compact_kernel(const float4* __restrict__ src, const float4* __r
   o.m11[i] = b.y; o.m12[i] = c.x; o.m22[i] = c.y;
 }
 
-// one correspondence of the objective (identical arithmetic to fdf_kernel)
+// one correspondence of OptimizationFunctorWithIndices::fdf: pp = A s (fp32, Eigen order),
+// r = fp32(pp - q) widened to fp64, t = M r, accumulate r't, t and s t'
 __device__ __forceinline__ void fdf_point(const Xf34& A, float sx, float sy, float sz, float qx,
                                           float qy, float qz, double m00, double m01, double m02,
                                           double m11, double m12, double m22,
@@ -729,13 +695,18 @@ __device__ __forceinline__ void fdf_point(const Xf34& A, float sx, float sy, flo
 __global__ __launch_bounds__(256) void fdf_soa_kernel(CorrSoA c, size_t m, Xf34 A,
                                                       double* __restrict__ partial,
                                                       unsigned int* __restrict__ ticket,
-                                                      double* __restrict__ out) {
+                                                      double* __restrict__ out, int reverse,
+                                                      unsigned long long* done_flag,
+                                                      unsigned long long seq) {
   double acc[kRedVals];
 #pragma unroll
   for (int v = 0; v < kRedVals; ++v) acc[v] = 0.0;
   const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
   const size_t m4 = m / 4;
-  for (size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < m4; i += stride) {
+  for (size_t k = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; k < m4; k += stride) {
+    // reverse: the chip walks the streams back to front, so the tail of the previous pass
+    // (still in the 256 MiB Infinity Cache) is consumed first
+    const size_t i = reverse ? m4 - 1 - k : k;
     const float4 sx = reinterpret_cast<const float4*>(c.sx)[i];
     const float4 sy = reinterpret_cast<const float4*>(c.sy)[i];
     const float4 sz = reinterpret_cast<const float4*>(c.sz)[i];
@@ -764,7 +735,7 @@ __global__ __launch_bounds__(256) void fdf_soa_kernel(CorrSoA c, size_t m, Xf34 
   }
   if (ticket) {
     store_partial_sc1(acc, partial + static_cast<size_t>(blockIdx.x) * kRedVals);
-    finish_in_last_block(partial, ticket, out);
+    finish_in_last_block(partial, ticket, out, done_flag, seq);
   } else {
     block_reduce_store(acc, partial + static_cast<size_t>(blockIdx.x) * kRedVals);
   }
@@ -945,8 +916,9 @@ hipError_t launch_compact(const float4* src, const float4* qbuf, const Cov3& mah
 }
 
 hipError_t launch_fdf_soa(const CorrSoA& c, size_t m, Xf34 A, double* partial, int nb,
-                          unsigned int* ticket, double* out, hipStream_t s) {
-  fdf_soa_kernel<<<nb, 256, 0, s>>>(c, m, A, partial, ticket, out);
+                          unsigned int* ticket, double* out, int reverse,
+                          unsigned long long* done_flag, unsigned long long seq, hipStream_t s) {
+  fdf_soa_kernel<<<nb, 256, 0, s>>>(c, m, A, partial, ticket, out, reverse, done_flag, seq);
   return hipGetLastError();
 }
 
@@ -954,13 +926,6 @@ int fdf_grid_blocks(size_t n, int max_blocks) {
   // ~8 points per thread keeps >= 8 waves per CU resident on 256 CUs at 5M points
   const size_t want = (n + 256 * 8 - 1) / (256 * 8);
   return static_cast<int>(std::max<size_t>(1, std::min<size_t>(want, max_blocks)));
-}
-
-hipError_t launch_fdf(const float4* src, const float4* qbuf, const Cov3& mahal, size_t p0,
-                      size_t p1, Xf34 A, double* partial, int nb, unsigned int* ticket,
-                      double* out, hipStream_t s) {
-  fdf_kernel<<<nb, 256, 0, s>>>(src, qbuf, mahal, p0, p1, A, partial, ticket, out);
-  return hipGetLastError();
 }
 
 hipError_t launch_fitness(const GridView& tgt, const float4* src, size_t p0, size_t p1, Xf34 T,
