@@ -35,20 +35,40 @@ FDF_BYTES_ACCEPTED = 72
 FDF_BYTES_REJECTED = 0
 
 
+# BASELINE.json configs (C1, the cube plumbing case, is the unit-test fixture, not a bench line)
+CONFIGS = {
+    "C2": dict(n_source=100_000, n_target=100_000, max_iter=100, fixed=False, occlusion=0.0,
+               text="C2: 100k-pt synthetic scan vs 100k-pt CAD-sampled cloud, k=20"),
+    "C3": dict(n_source=1_000_000, n_target=1_000_000, max_iter=50, fixed=True, occlusion=0.0,
+               text="C3: 1M-pt scan vs 1M-pt CAD, exactly 50 GICP iterations (delta test off)"),
+    "C4": dict(n_source=5_000_000, n_target=5_000_000, max_iter=100, fixed=False, occlusion=0.0,
+               text="C4: 5M-pt scan vs 5M-pt CAD-sampled synthetic aero part"),
+    "C5": dict(n_source=20_000_000, n_target=5_000_000, max_iter=100, fixed=False, occlusion=0.25,
+               text="C5: 20M-pt scan (25% of the surface occluded) vs 5M-pt CAD, guess=I, full converge"),
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n-source", type=int, default=5_000_000)
-    ap.add_argument("--n-target", type=int, default=5_000_000)
+    ap.add_argument("--config", default="C4", choices=sorted(CONFIGS),
+                    help="BASELINE.json workload (default C4: the metric's 5M<->5M)")
+    ap.add_argument("--n-source", type=int, default=None, help="override the config's scan size")
+    ap.add_argument("--n-target", type=int, default=None, help="override the config's CAD size")
     ap.add_argument("--cpu-sample", type=int, default=500_000,
                     help="points per cloud of the bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=1)
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01_pmc_fdf.json"))
     ap.add_argument("--no-events", action="store_true",
                     help="time the steps without per-launch HIP events (A/B of the event overhead)")
-    return ap.parse_args()
+    args = ap.parse_args()
+    cfg = CONFIGS[args.config]
+    args.n_source = args.n_source or cfg["n_source"]
+    args.n_target = args.n_target or cfg["n_target"]
+    args.max_iter, args.fixed, args.occlusion, args.cfg_text = cfg["max_iter"], cfg["fixed"], cfg["occlusion"], cfg["text"]
+    return args
 
 
 def dist_setup(args):
@@ -66,14 +86,14 @@ def dist_setup(args):
     return world, rank, local, Rendezvous(rank, world)
 
 
-def cpu_baseline(n, threads):
+def cpu_baseline(n, threads, occlusion=0.0):
     """Oracle (PCL 1.8.1 restatement, single thread like PCL GICP) on a bounded sample of the
     same synthetic workload; per-iteration cost grows at least linearly with N, so the
     5M-equivalent rate is reported as sample_rate * n / 5M (an upper bound for the CPU)."""
     from leica_point_cloud_processing_amd import synth
     from oracle import ref
 
-    scan, cad, _ = synth.scan_vs_cad(n, n)
+    scan, cad, _ = synth.scan_vs_cad(n, n, occlusion=occlusion)
     g = ref.RefGICP(threads=threads)
     g.set_source(scan)
     g.set_target(cad)
@@ -89,10 +109,10 @@ def main():
     from leica_point_cloud_processing_amd.engine import GICPEngine
 
     t_gen = time.time()
-    scan, cad, T_true = synth.scan_vs_cad(args.n_source, args.n_target)
+    scan, cad, T_true = synth.scan_vs_cad(args.n_source, args.n_target, occlusion=args.occlusion)
     t_gen = time.time() - t_gen
 
-    eng = GICPEngine(device=local)
+    eng = GICPEngine(device=local, max_iter=args.max_iter, fixed_iterations=int(args.fixed))
     if world > 1:
         uid = pg.broadcast(GICPEngine.unique_id() if rank == 0 else None)
         eng.comm_init(world, rank, uid)
@@ -179,19 +199,21 @@ def main():
     cpu = None
     frob_sample = None
     if args.cpu_sample > 0:
-        rate, info, T_cpu, (s_scan, s_cad) = cpu_baseline(args.cpu_sample, args.cpu_threads)
-        scale = args.cpu_sample / args.n_source
+        n_cpu = min(args.cpu_sample, args.n_source)
+        rate, info, T_cpu, (s_scan, s_cad) = cpu_baseline(n_cpu, args.cpu_threads, args.occlusion)
+        scale = n_cpu / args.n_source
         cpu = {
             "value": rate * scale,
             "unit": "iterations/s",
             "cores": args.cpu_threads,
             "kind": "port",
             "sample": (f"oracle/gicp_ref.c (PCL 1.8.1 GICP restatement, kd-tree, BFGS) single align on a "
-                       f"{args.cpu_sample}<->{args.cpu_sample} sample of the same synthetic workload: "
+                       f"{n_cpu}<->{n_cpu} sample of the same synthetic workload: "
                        f"{info['iterations']} iterations in {info['t_loop_s']:.2f} s loop "
                        f"({rate:.3f} it/s at sample size; covariances {info['t_cov_s']:.2f} s), "
                        f"scaled x{scale:g} to {args.n_source} points (linear, favours the CPU)"),
             "sample_rate": rate,
+            "sample_frac_scale": scale,
         }
         # final-transform parity on the sample (the 5M oracle run is not bounded)
         e3 = GICPEngine(device=local)
@@ -202,7 +224,8 @@ def main():
         e3.close()
 
     line = {
-        "metric": "GICP iterations/sec, 5M<->5M scan-vs-CAD (PCL-1.8.1-faithful BFGS GICP)",
+        "metric": ("GICP iterations/sec, 5M<->5M scan-vs-CAD (PCL-1.8.1-faithful BFGS GICP)" if args.config == "C4"
+                   else f"GICP iterations/sec, {args.config} (PCL-1.8.1-faithful BFGS GICP)"),
         "value": round(value, 3),
         "unit": "iterations/s",
         "n_gpus": world,
@@ -215,8 +238,9 @@ def main():
         "dtype": "f32 transform / f64 accumulate",
         "data": "synthetic",
         "config": {
-            "workload": f"C4: {args.n_source}-pt scan vs {args.n_target}-pt CAD-sampled synthetic aero part, "
-                        "k=20, maxCorrDist=0.04, tf_eps=4e-3, rot_eps=2e-3, max_iter=100, guess=I",
+            "workload": f"{args.cfg_text} ({args.n_source} vs {args.n_target} points), synthetic aero part, "
+                        f"k=20, maxCorrDist=0.04, tf_eps=4e-3, rot_eps=2e-3, max_iter={args.max_iter}, guess=I",
+            "name": args.config,
             "n_source": args.n_source,
             "n_target": args.n_target,
             "parallelism": f"source point-range shards x{world}, target replicated, RCCL all-reduce per pass",

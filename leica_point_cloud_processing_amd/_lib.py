@@ -10,7 +10,7 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmgicp.so")
+LIB_PATH = os.path.join(_HERE, os.environ.get("MGICP_LIB_NAME", "libmgicp.so"))  # variant builds for A/B
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "mi355x_gicp.h")
 
 MGICP_OK = 0

@@ -15,6 +15,10 @@
 // expression rounds exactly like PCL's non-FMA SSE2 Eigen code and like oracle/gicp_ref.c.
 #pragma clang fp contract(off)
 
+#ifndef MGICP_NN_UNROLL
+#define MGICP_NN_UNROLL 4  // candidate gathers in flight per lane in the 1-NN scans
+#endif
+
 #include "mgicp_internal.hpp"
 
 #include <hipcub/hipcub.hpp>
@@ -222,6 +226,15 @@ struct NnVisitor {
   }
   __device__ __forceinline__ void range(const GridView& g, uint32_t a, uint32_t b) {
     uint32_t j = a;
+#if MGICP_NN_UNROLL >= 8
+    for (; j + 8 <= b; j += 8) {  // eight gathers in flight per lane (latency-bound loop)
+      float4 p[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) p[u] = g.pts[j + u];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) test(p[u], j + u);
+    }
+#endif
     for (; j + 4 <= b; j += 4) {  // four gathers in flight per lane (latency-bound loop)
       const float4 p0 = g.pts[j], p1 = g.pts[j + 1], p2 = g.pts[j + 2], p3 = g.pts[j + 3];
       test(p0, j);
