@@ -339,6 +339,10 @@ static void compute_covariances(const kdtree* t, int k, double eps, int threads,
 /* ------------------------------------------------------------------------------------ */
 /* GICP state                                                                            */
 /* ------------------------------------------------------------------------------------ */
+/* moment layout: [0] S0 = sum r0'M r0; [1..12] B[a][i] = sum (M r0)_a w_i; [13..72]
+ * Q[ab][ij] = sum M_ab w_i w_j (ab over 00,01,02,11,12,22; ij over the upper pairs of 4);
+ * [73] count; w = (s - ctr, 1), r0 = fl(fl(T0 s) - q) */
+#define MOM_VALS 74
 struct ref_gicp {
     ref_params prm;
     float* src; int ns; int src_dirty;
@@ -350,6 +354,10 @@ struct ref_gicp {
     double* mahal;    /* ns x 9 row-major */
     int* corr_src; int* corr_tgt; int m;
     int n_evals;
+    /* moment-form objective (prm.objective == 1): taken at the correspondence transform T0 */
+    double mom[MOM_VALS];
+    float T0[4][4];
+    double ctr[3];
 };
 
 void ref_default_params(ref_params* p) {
@@ -362,6 +370,7 @@ void ref_default_params(ref_params* p) {
     p->max_inner_iterations = 20;
     p->fixed_iterations = 0;
     p->threads = 1;
+    p->objective = 0;
 }
 
 ref_gicp* ref_create(const ref_params* p) {
@@ -586,7 +595,95 @@ static void fdf_range(const ref_gicp* g, const float A[4][4], int c0, int c1, fd
     }
 }
 
+static const int kSymA[6][2] = {{0, 0}, {0, 1}, {0, 2}, {1, 1}, {1, 2}, {2, 2}};
+static const int kSymW[10][2] = {{0, 0}, {0, 1}, {0, 2}, {0, 3}, {1, 1}, {1, 2}, {1, 3}, {2, 2}, {2, 3}, {3, 3}};
+static int sym_a(int a, int b) { static const int t[3][3] = {{0, 1, 2}, {1, 3, 4}, {2, 4, 5}}; return t[a][b]; }
+static int sym_w(int i, int j) {
+    static const int t[4][4] = {{0, 1, 2, 3}, {1, 4, 5, 6}, {2, 5, 7, 8}, {3, 6, 8, 9}};
+    return t[i][j];
+}
+
+/* One pass over the correspondences at T0: the 74 moments of the quadratic objective. */
+static void moments_build(ref_gicp* g, const float T0[4][4]) {
+    memcpy(g->T0, T0, sizeof(g->T0));
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int i = 0; i < g->ns; ++i)
+        for (int a = 0; a < 3; ++a) {
+            float v = g->out[3 * (size_t)i + a];
+            if (v < lo[a]) lo[a] = v;
+            if (v > hi[a]) hi[a] = v;
+        }
+    for (int a = 0; a < 3; ++a) g->ctr[a] = (double)(0.5f * (lo[a] + hi[a]));
+    double* mo = g->mom;
+    memset(mo, 0, sizeof(g->mom));
+    for (int c = 0; c < g->m; ++c) {
+        int i = g->corr_src[c], j = g->corr_tgt[c];
+        const float* ps = g->out + 3 * (size_t)i;
+        const float* pt = g->tgt + 3 * (size_t)j;
+        float pp[3];
+        xform(T0, ps, pp);
+        double r0[3] = {(double)(pp[0] - pt[0]), (double)(pp[1] - pt[1]), (double)(pp[2] - pt[2])};
+        const double* M = g->mahal + 9 * (size_t)i;
+        double w[4] = {(double)ps[0] - g->ctr[0], (double)ps[1] - g->ctr[1], (double)ps[2] - g->ctr[2], 1.0};
+        double Mr[3];
+        for (int a = 0; a < 3; ++a) Mr[a] = M[3 * a] * r0[0] + M[3 * a + 1] * r0[1] + M[3 * a + 2] * r0[2];
+        mo[0] += r0[0] * Mr[0] + r0[1] * Mr[1] + r0[2] * Mr[2];
+        for (int a = 0; a < 3; ++a)
+            for (int k = 0; k < 4; ++k) mo[1 + 4 * a + k] += Mr[a] * w[k];
+        for (int p = 0; p < 6; ++p) {
+            double mab = M[3 * kSymA[p][0] + kSymA[p][1]];
+            for (int q = 0; q < 10; ++q) mo[13 + 10 * p + q] += mab * (w[kSymW[q][0]] * w[kSymW[q][1]]);
+        }
+        mo[73] += 1.0;
+    }
+}
+
+/* f / grad at x from the moments: r(x) = r0 + Y w, Y = [dR | dR ctr + dt], dA = A(x) - T0 */
+static void moments_eval(ref_gicp* g, const double x[6], double* f, double grad[6]) {
+    float A[4][4];
+    apply_state(x, A);
+    const double* mo = g->mom;
+    double Y[3][4];
+    for (int a = 0; a < 3; ++a) {
+        double u = (double)A[a][3] - (double)g->T0[a][3];
+        for (int k = 0; k < 3; ++k) {
+            Y[a][k] = (double)A[a][k] - (double)g->T0[a][k];
+            u += Y[a][k] * g->ctr[k];
+        }
+        Y[a][3] = u;
+    }
+    /* G[b][i] = sum w_i (M r)_b = B[b][i] + sum_{c,j} Y[c][j] Q[bc][ij] */
+    double G[3][4];
+    for (int b = 0; b < 3; ++b)
+        for (int i = 0; i < 4; ++i) {
+            double acc = 0.0;
+            for (int c = 0; c < 3; ++c)
+                for (int j = 0; j < 4; ++j) acc += Y[c][j] * mo[13 + 10 * sym_a(b, c) + sym_w(i, j)];
+            G[b][i] = mo[1 + 4 * b + i] + acc;
+        }
+    double m = mo[73];
+    g->n_evals++;
+    if (f) {
+        double corr = 0.0;
+        for (int a = 0; a < 3; ++a)
+            for (int i = 0; i < 4; ++i) corr += Y[a][i] * (mo[1 + 4 * a + i] + G[a][i]);
+        *f = (mo[0] + corr) / m;
+    }
+    if (grad) {
+        double s = 2.0 / m;
+        double R[3][3];
+        for (int b = 0; b < 3; ++b) grad[b] = G[b][3] * s;
+        for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 3; ++b) R[a][b] = (G[b][a] + g->ctr[a] * G[b][3]) * s;
+        r_derivative(x, R, grad);
+    }
+}
+
 static void functor_eval(ref_gicp* g, const double x[6], double* f, double grad[6]) {
+    if (g->prm.objective == 1) {
+        moments_eval(g, x, f, grad);
+        return;
+    }
     float A[4][4];
     apply_state(x, A);
     int m = g->m;
@@ -634,6 +731,15 @@ int ref_fdf_sums(ref_gicp* g, const double x[6], int c0, int c1, double out14[14
         for (int b = 0; b < 3; ++b) out14[4 + 3 * a + b] = acc.R[a][b];
     }
     out14[13] = (double)(c1 - c0);
+    return REF_OK;
+}
+
+int ref_moments(ref_gicp* g, const float T0_cm[16], double out74[74]) {
+    if (!g || !g->out || g->m <= 0) return REF_E_INVALID;
+    float T0[4][4];
+    cm_to_rm(T0_cm, T0);
+    moments_build(g, T0);
+    if (out74) memcpy(out74, g->mom, sizeof(g->mom));
     return REF_OK;
 }
 
@@ -1110,6 +1216,7 @@ int ref_align(ref_gicp* g, const float guess_cm[16], float out_T_cm[16], ref_res
     while (!converged) {
         correspondence_sweep(g, T, G, NULL, NULL);
         r.n_corr_last = g->m;
+        if (g->prm.objective == 1) moments_build(g, T);
         memcpy(prev, T, sizeof(T));
         if (estimate_bfgs(g, T) != 0) break; /* PCLException: converged_ stays false */
         double delta = 0.;

@@ -35,6 +35,10 @@ typedef struct {
     int    max_inner_iterations;   /* max_inner_iterations_ (PCL GICP default 20) */
     int    fixed_iterations;       /* test hook: 1 => ignore the delta test, run exactly max_iterations */
     int    threads;                /* <=1: single thread (PCL 1.8.1 GICP is single-threaded); >1: OpenMP */
+    int    objective;              /* 0: PCL per-point functor passes (default, PCL 1.8.1 itself);
+                                      1: moment form -- the same quadratic objective evaluated from
+                                      74 fp64 moments taken once per outer iteration (checker for the
+                                      engine's MGICP_OBJ_MOMENTS mode) */
 } ref_params;
 
 typedef struct {
@@ -80,6 +84,9 @@ int ref_knn(const float* xyz, size_t n, size_t stride_bytes, const float* querie
  * out_tgt[i] = target index or -1 if rejected; out_M9 (optional) = row-major Mahalanobis. */
 int ref_correspondences(ref_gicp* g, const float T_cm[16], const float guess_cm[16],
                         int* out_tgt, float* out_d2, double* out_M9);
+/* Moment-form objective (ref_params.objective = 1): build the 74 moments of the last
+ * correspondence set at transform T0 (col-major); out74 optional. */
+int ref_moments(ref_gicp* g, const float T0_cm[16], double out74[74]);
 /* OptimizationFunctorWithIndices::fdf at state x for the last correspondence set. */
 int ref_fdf(ref_gicp* g, const double x[6], double* f, double g6[6]);
 /* raw sums of the functor over correspondences [c0, c1): f, g_t[3], Rsum[9] row-major, count

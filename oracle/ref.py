@@ -26,6 +26,7 @@ class RefParams(ctypes.Structure):
         ("max_inner_iterations", ctypes.c_int),
         ("fixed_iterations", ctypes.c_int),
         ("threads", ctypes.c_int),
+        ("objective", ctypes.c_int),
     ]
 
 
@@ -71,6 +72,7 @@ def load():
         "ref_knn": (ctypes.c_int, [P, sz, sz, P, sz, ctypes.c_int, IP, FP]),
         "ref_correspondences": (ctypes.c_int, [P, FP, FP, IP, FP, DP]),
         "ref_fdf": (ctypes.c_int, [P, DP, DP, DP]),
+        "ref_moments": (ctypes.c_int, [P, FP, DP]),
         "ref_fdf_sums": (ctypes.c_int, [P, DP, ctypes.c_int, ctypes.c_int, DP]),
         "ref_apply_state": (None, [DP, FP]),
     }
@@ -108,7 +110,7 @@ class RefGICP:
 
     def __init__(self, max_iterations=100, transformation_epsilon=4e-3, rotation_epsilon=2e-3,
                  max_corr_dist=0.04, gicp_epsilon=1e-3, k=20, max_inner_iterations=20,
-                 fixed_iterations=False, threads=1):
+                 fixed_iterations=False, threads=1, objective=0):
         self.lib = load()
         self.p = RefParams()
         self.lib.ref_default_params(ctypes.byref(self.p))
@@ -121,6 +123,7 @@ class RefGICP:
         self.p.max_inner_iterations = max_inner_iterations
         self.p.fixed_iterations = int(bool(fixed_iterations))
         self.p.threads = threads
+        self.p.objective = objective
         self.h = self.lib.ref_create(ctypes.byref(self.p))
         self.ns = 0
 
@@ -175,6 +178,12 @@ class RefGICP:
         x = np.asarray(x, np.float64)
         out = np.zeros(14, np.float64)
         rc = self.lib.ref_fdf_sums(self.h, _dp(x), int(c0), int(c1), _dp(out))
+        assert rc == 0
+        return out
+
+    def moments(self, T0):
+        out = np.zeros(74, np.float64)
+        rc = self.lib.ref_moments(self.h, _fp(cm(T0)), _dp(out))
         assert rc == 0
         return out
 

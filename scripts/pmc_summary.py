@@ -46,6 +46,14 @@ def main():
         "fdf_hbm_bytes_per_launch": hbm,
         "correction": "bytes = 2*FETCH_SIZE*1024 (gfx950 wide-read halving) + WRITE_SIZE*1024",
     }
+    # the other kernels of the path, for DESIGN.md (same correction; gathers use 16 B/lane loads)
+    others = {}
+    for k in ("correspond_kernel", "compact_kernel", "knn_cov_kernel", "xform_points", "fitness_kernel"):
+        fk, wk = per_dispatch(fdir, "FETCH_SIZE", k), per_dispatch(wdir, "WRITE_SIZE", k)
+        if fk and wk:
+            others[k] = {"dispatches": len(fk),
+                         "hbm_bytes_per_launch": 2.0 * sum(fk) / len(fk) * 1024 + sum(wk) / len(wk) * 1024}
+    res["other_kernels"] = others
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res))
