@@ -137,6 +137,30 @@ def test_gradient_matches_finite_differences(part_small):
         assert abs(fd - g[i]) <= 2e-3 * max(1.0, abs(g[i])), (i, fd, g[i])
 
 
+def test_moment_form_matches_functor(part_small):
+    """The moment form of the objective (oracle objective=1) is PCL's functor up to
+    the fp32 rounding of A*s: identical at the expansion point, ~1e-6 relative elsewhere."""
+    from oracle import ref
+
+    scan, cad, _ = part_small
+    o = ref.RefGICP()
+    o.set_source(scan)
+    o.set_target(cad)
+    T0 = np.eye(4, dtype=np.float32)
+    o.correspondences(T0)
+    o.moments(T0)
+    rng = np.random.default_rng(3)
+    for scale in (0.0, 1e-5, 1e-3, 1e-2):
+        x = rng.normal(size=6) * scale
+        o.set_params(objective=0)
+        f0, g0 = o.fdf(x)
+        o.set_params(objective=1)
+        f1, g1 = o.fdf(x)
+        tol = 1e-12 if scale == 0.0 else 1e-4
+        assert abs(f1 - f0) <= tol * abs(f0), (scale, f0, f1)
+        assert np.abs(g1 - g0).max() <= max(tol, 1e-4) * max(1.0, np.abs(g0).max()), (scale, g0, g1)
+
+
 def test_apply_state_matches_numpy_restatement():
     from oracle import golden_numpy, ref
 
