@@ -13,6 +13,10 @@ all: $(LIB) oracle adapter-example
 $(LIB): $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS) -lrccl
 
+# A/B builds: make variant NAME=w8 DEFS=-DMGICP_CORR_WAVES=8 -> libmgicp_w8.so (MGICP_LIB_NAME selects it)
+variant: $(SRCS) $(HDRS)
+	$(HIPCC) $(HIPFLAGS) $(DEFS) -shared -o $(PKG)/libmgicp_$(NAME).so $(SRCS) -lrccl
+
 # plain C++ host program over the C-ABI (g++, no HIP headers): what an integrator links
 adapter/cabi_example: adapter/cabi_example.cpp include/mi355x_gicp.h $(LIB)
 	g++ -O2 -std=c++14 -Wall -Iinclude -o $@ adapter/cabi_example.cpp -L$(PKG) -lmgicp -Wl,-rpath,'$$ORIGIN/../$(PKG)'
@@ -23,7 +27,7 @@ oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -f $(LIB)
+	rm -f $(LIB) $(PKG)/libmgicp_*.so
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean adapter-example
+.PHONY: all oracle clean adapter-example variant

@@ -192,6 +192,7 @@ def main():
         "knn_cov": {"avg_ms": cov_ms, "points": args.n_target,
                     "algorithmic_GBps": (args.n_target * (21 * 16 + 48)) / (cov_ms * 1e-3) / 1e9 if cov_ms else None},
         "correspond": kt["correspond"],
+        "compact_mahalanobis": kt["compact"],
         "fdf": kt["fdf"],
         "reduce_finish": kt["reduce_finish"],
     }

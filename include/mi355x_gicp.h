@@ -139,10 +139,12 @@ int mgicp_debug_fdf(mgicp_ctx* ctx, const double x[6], double* f, double g6[6]);
 int mgicp_debug_fdf_sums(mgicp_ctx* ctx, const double x[6], double out16[16]);
 /* per-iteration transformation_ of the last align (col-major, iterations x 16) */
 int mgicp_debug_trace(mgicp_ctx* ctx, float* out, int max_iters);
-/* average device time (ms) of each kernel family during the last align, for roofline
- * reporting: [0] covariance kNN, [1] correspondence, [2] BFGS objective pass,
- * [3] reduction finish; counts in out_counts (optional) */
-int mgicp_debug_kernel_times(mgicp_ctx* ctx, double out_ms[4], int out_counts[4]);
+/* average device time (ms) of each kernel family while profiling is on, for roofline
+ * reporting: [0] covariance kNN, [1] correspondence 1-NN, [2] BFGS objective pass,
+ * [3] separate reduction finish, [4] compaction + Mahalanobis; counts in out_counts (optional) */
+#define MGICP_KERNEL_FAMILIES 5
+int mgicp_debug_kernel_times(mgicp_ctx* ctx, double out_ms[MGICP_KERNEL_FAMILIES],
+                             int out_counts[MGICP_KERNEL_FAMILIES]);
 /* enable (1) / disable (0) per-launch HIP event timing (off by default) */
 int mgicp_set_profiling(mgicp_ctx* ctx, int on);
 

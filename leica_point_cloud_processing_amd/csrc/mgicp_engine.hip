@@ -193,7 +193,7 @@ struct Cloud {
   Cov3 cov3() const { return Cov3{cov.p, cov.p + n, cov.p + 2 * n}; }
 };
 
-enum { kFamCov = 0, kFamCorr = 1, kFamFdf = 2, kFamRed = 3 };
+enum { kFamCov = 0, kFamCorr = 1, kFamFdf = 2, kFamRed = 3, kFamCompact = 4, kFams = 5 };
 
 }  // namespace
 
@@ -217,10 +217,8 @@ struct mgicp_ctx {
   // per source point (sorted), rank shard only
   DevBuf<float4> src_out;  // guess-applied source (only when guess != I)
   const float4* d_out = nullptr;
-  DevBuf<float4> qbuf;
-  DevBuf<double2> mahal;   // 3 * n
   // compacted accepted correspondences of the current outer iteration (shard-relative)
-  DevBuf<uint32_t> prev_pos;  // last iteration's matched target position (1-NN seed)
+  DevBuf<uint32_t> prev_pos;  // matched target sorted position per shard point (also the next 1-NN seed)
   DevBuf<uint32_t> flags, cpos;
   DevBuf<float> corr_f;    // 6 streams
   DevBuf<double> corr_d;   // 6 streams
@@ -228,7 +226,6 @@ struct mgicp_ctx {
   size_t corr_cap = 0;     // elements per stream (multiple of 4)
   size_t m_local = 0;      // accepted correspondences of this rank
   bool seed_valid = false;
-  DevBuf<int> dbg_nn;
   DevBuf<double> partial;
   DevBuf<double> red;      // kRedVals
   double* h_red = nullptr;   // pinned, mapped, coherent host memory
@@ -256,8 +253,8 @@ struct mgicp_ctx {
   struct EvPair { hipEvent_t a, b; int fam; };
   std::vector<EvPair> pending;
   std::vector<hipEvent_t> pool;
-  double fam_ms[4] = {0, 0, 0, 0};
-  int fam_cnt[4] = {0, 0, 0, 0};
+  double fam_ms[kFams] = {};
+  int fam_cnt[kFams] = {};
 
   size_t shard_p0() const { return src.n * static_cast<size_t>(rank) / nranks; }
   size_t shard_p1() const { return src.n * static_cast<size_t>(rank + 1) / nranks; }
@@ -559,8 +556,6 @@ int wait_pass(mgicp_ctx* ctx, unsigned long long seq) {
 
 int ensure_iter_buffers(mgicp_ctx* ctx) {
   const size_t n = ctx->src.n;
-  HIPCK(ctx->qbuf.reserve(n));
-  HIPCK(ctx->mahal.reserve(3 * n));
   const int nb = std::max(fdf_grid_blocks(n), static_cast<int>((n + 255) / 256));
   HIPCK(ctx->partial.reserve(static_cast<size_t>(nb) * kRedVals));
   HIPCK(ctx->red.reserve(kRedVals));
@@ -582,11 +577,6 @@ int ensure_iter_buffers(mgicp_ctx* ctx) {
     HIPCK(hipMemsetAsync(ctx->ticket.p, 0, sizeof(unsigned int), ctx->stream));
   }
   return MGICP_OK;
-}
-
-Cov3 mahal3(mgicp_ctx* ctx) {
-  const size_t n = ctx->src.n;
-  return Cov3{ctx->mahal.p, ctx->mahal.p + n, ctx->mahal.p + 2 * n};
 }
 
 // guess-applied source cloud ("output" after transformPointCloud(output, output, guess))
@@ -623,26 +613,30 @@ CorrSoA corr_soa(mgicp_ctx* ctx) {
 }
 
 // One correspondence sweep (the loop body of computeTransformation before the BFGS call):
-// exact 1-NN + Mahalanobis per source point, then a deterministic compaction of the accepted
-// ones (exclusive scan of the flags, scatter in grid-sorted order) into the SoA streams.
-// `seed` uses the previous sweep's matches as 1-NN starting candidates (exact either way).
-int correspond(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, int* dbg, bool seed) {
+// exact 1-NN per source point, then a deterministic compaction of the accepted ones (exclusive
+// scan of the flags, scatter in grid-sorted order) that computes their Mahalanobis matrices
+// straight into the SoA streams.  `seed` uses the previous sweep's matches as 1-NN starting
+// candidates (exact either way).
+int correspond(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
   const double thr = ctx->prm.max_corr_dist * ctx->prm.max_corr_dist;
   const size_t p0 = ctx->shard_p0(), p1 = ctx->shard_p1(), ns = p1 - p0;
   hipStream_t s = ctx->stream;
-  if (!seed || !ctx->seed_valid) HIPCK(hipMemsetAsync(ctx->prev_pos.p, 0xff, (ns + 1) * sizeof(uint32_t), s));
+  const bool seeded = seed && ctx->seed_valid;
   HIPCK(hipMemsetAsync(ctx->flags.p + ns, 0, sizeof(uint32_t), s));
   {
     ProfScope ps(ctx, kFamCorr);
-    HIPCK(launch_correspond(ctx->tgt.view, ctx->tgt.cov3(), ctx->d_out, ctx->src.cov3(), p0, p1,
-                            T.xf(), rot_of(T, G), thr, ctx->qbuf.p, mahal3(ctx), dbg,
+    HIPCK(launch_correspond(ctx->tgt.view, ctx->d_out, p0, p1, T.xf(), thr, seeded ? 1 : 0,
                             ctx->prev_pos.p, ctx->flags.p, s));
   }
   ctx->seed_valid = true;
   const size_t sb = scan_scratch_bytes(ns + 1);
   HIPCK(launch_exclusive_scan(ctx->cscratch.p, sb, ctx->flags.p, ctx->cpos.p, ns + 1, s));
-  HIPCK(launch_compact(ctx->d_out, ctx->qbuf.p, mahal3(ctx), ctx->flags.p, ctx->cpos.p, p0, p1,
-                       corr_soa(ctx), s));
+  {
+    ProfScope ps(ctx, kFamCompact);
+    HIPCK(launch_compact(ctx->d_out, ctx->tgt.view.pts, ctx->src.cov3(), ctx->tgt.cov3(),
+                         rot_of(T, G), ctx->prev_pos.p, ctx->flags.p, ctx->cpos.p, p0, p1,
+                         corr_soa(ctx), s));
+  }
   uint32_t m = 0;
   HIPCK(hipMemcpyAsync(&m, ctx->cpos.p + ns, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   int rc = sync(ctx);
@@ -901,7 +895,7 @@ void mgicp_destroy(mgicp_ctx* ctx) {
     c->raw.release(); c->orig.release(); c->pts.release(); c->perm.release();
     c->cell_start.release(); c->cov.release(); c->empty_dist.release();
   }
-  ctx->src_out.release(); ctx->qbuf.release(); ctx->mahal.release(); ctx->dbg_nn.release();
+  ctx->src_out.release();
   ctx->partial.release(); ctx->red.release(); ctx->counts.release(); ctx->keys.release();
   ctx->keys_sorted.release(); ctx->vals.release(); ctx->scratch.release(); ctx->u64.release();
   ctx->fpartial.release();
@@ -960,7 +954,7 @@ int mgicp_align(mgicp_ctx* ctx, const float guess_cm[16], float out_T_cm[16], mg
   bool converged = false;
   int solver_rc = MGICP_OK;
   while (!converged) {
-    if ((rc = correspond(ctx, T, G, nullptr, nr_iterations > 0))) return rc;
+    if ((rc = correspond(ctx, T, G, nr_iterations > 0))) return rc;
     prev = T;
     int ncorr = 0;
     rc = estimate_bfgs(ctx, T, &ncorr);
@@ -1184,29 +1178,29 @@ int mgicp_debug_correspondences(mgicp_ctx* ctx, const float T_cm[16], int* out_t
   if (rc) return rc;
   if ((rc = ensure_iter_buffers(ctx))) return rc;
   const size_t n = ctx->src.n;
-  HIPCK(ctx->dbg_nn.reserve(n));
-  HIPCK(hipMemsetAsync(ctx->dbg_nn.p, 0xff, n * sizeof(int), ctx->stream));
   const Mat4 G = Mat4::identity();
   if ((rc = set_output(ctx, G))) return rc;
-  if ((rc = correspond(ctx, Mat4::from_cm(T_cm), G, ctx->dbg_nn.p, false))) return rc;
-  std::vector<int> nn(n);
-  std::vector<double2> M(3 * n);
-  std::vector<uint32_t> perm(n);
-  HIPCK(hipMemcpyAsync(nn.data(), ctx->dbg_nn.p, n * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-  HIPCK(hipMemcpyAsync(M.data(), ctx->mahal.p, 3 * n * sizeof(double2), hipMemcpyDeviceToHost, ctx->stream));
+  if ((rc = correspond(ctx, Mat4::from_cm(T_cm), G, false))) return rc;
+  const size_t p0 = ctx->shard_p0(), p1 = ctx->shard_p1(), ns = p1 - p0;
+  std::vector<uint32_t> nn(ns), flag(ns), slot(ns), perm(n), tperm(ctx->tgt.n);
+  HIPCK(hipMemcpyAsync(nn.data(), ctx->prev_pos.p, ns * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCK(hipMemcpyAsync(flag.data(), ctx->flags.p, ns * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCK(hipMemcpyAsync(slot.data(), ctx->cpos.p, ns * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
   HIPCK(hipMemcpyAsync(perm.data(), ctx->src.perm.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCK(hipMemcpyAsync(tperm.data(), ctx->tgt.perm.p, ctx->tgt.n * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+  const size_t cap = ctx->corr_cap;
+  std::vector<double> M(6 * cap);
+  HIPCK(hipMemcpyAsync(M.data(), ctx->corr_d.p, 6 * cap * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
   if ((rc = sync(ctx))) return rc;
   int cnt = 0;
-  const size_t p0 = ctx->shard_p0(), p1 = ctx->shard_p1();
   for (size_t p = p0; p < p1; ++p) {
-    const size_t i = perm[p];
-    if (out_tgt) out_tgt[i] = nn[p];
-    if (nn[p] >= 0) cnt++;
+    const size_t i = perm[p], k = p - p0;
+    const bool ok = flag[k] != 0;
+    if (out_tgt) out_tgt[i] = ok ? static_cast<int>(tperm[nn[k]]) : -1;
+    if (ok) cnt++;
     if (out_M6) {
       double* o = out_M6 + 6 * i;
-      o[0] = M[p].x; o[1] = M[p].y;
-      o[2] = M[n + p].x; o[3] = M[n + p].y;
-      o[4] = M[2 * n + p].x; o[5] = M[2 * n + p].y;
+      for (int v = 0; v < 6; ++v) o[v] = ok ? M[v * cap + slot[k]] : 0.0;
     }
   }
   return cnt;
@@ -1244,10 +1238,11 @@ int mgicp_debug_trace(mgicp_ctx* ctx, float* out, int max_iters) {
   return n;
 }
 
-int mgicp_debug_kernel_times(mgicp_ctx* ctx, double out_ms[4], int out_counts[4]) {
+int mgicp_debug_kernel_times(mgicp_ctx* ctx, double out_ms[MGICP_KERNEL_FAMILIES],
+                             int out_counts[MGICP_KERNEL_FAMILIES]) {
   if (!ctx || !out_ms) return MGICP_E_INVALID;
   prof_resolve(ctx);
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < kFams; ++i) {
     out_ms[i] = ctx->fam_cnt[i] ? ctx->fam_ms[i] / ctx->fam_cnt[i] : 0.0;
     if (out_counts) out_counts[i] = ctx->fam_cnt[i];
   }
@@ -1260,7 +1255,7 @@ int mgicp_set_profiling(mgicp_ctx* ctx, int on) {
   (void)hipStreamSynchronize(ctx->stream);
   prof_resolve(ctx);
   ctx->profiling = on != 0;
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < kFams; ++i) {
     ctx->fam_ms[i] = 0;
     ctx->fam_cnt[i] = 0;
   }

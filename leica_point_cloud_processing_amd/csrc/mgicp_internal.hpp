@@ -6,9 +6,10 @@
 //   pts        float4[n]      (x, y, z, bit_cast<float>(original index))
 //   cell_start uint32[nc + 1] exclusive prefix of per-cell counts (dense over the bbox)
 //   cov        3 x double2[n] symmetric covariance {c00,c01},{c02,c11},{c12,c22}
-// Per source point (sorted order), rewritten every outer iteration:
-//   qbuf       float4[n]      matched target xyz, w = 1 if the correspondence is accepted
-//   mahal      3 x double2[n] Mahalanobis matrix (R Cs R' + Ct)^-1, upper triangle
+// Per source point of the shard (sorted order), rewritten every outer iteration:
+//   nn_pos     uint32[n]      matched target sorted position (UINT32_MAX = rejected)
+//   flags/pos  uint32[n+1]    acceptance and its exclusive scan (compacted slot)
+// Accepted correspondences: CorrSoA (below), 72 bytes each.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstddef>
@@ -69,15 +70,15 @@ hipError_t launch_xform_points(const float4* in, size_t n, Xf34 T, float4* out,
                                hipStream_t s);
 hipError_t launch_knn_cov(const GridView& g, int k, double eps, size_t p0, size_t p1,
                           Cov3 cov, hipStream_t s);
-// prev_pos (nullable): per source point (shard-relative) the target sorted position matched in
-// the previous outer iteration (UINT32_MAX = none); seeds the exact 1-NN search and is updated.
-// flags (nullable): per source point (shard-relative) 1 if accepted.
-hipError_t launch_correspond(const GridView& tgt, const Cov3& cov_t, const float4* src,
-                             const Cov3& cov_s, size_t p0, size_t p1, Xf34 T, Rot33d R,
-                             double thr, float4* qbuf, Cov3 mahal, int* dbg_nn,
-                             uint32_t* prev_pos, uint32_t* flags, hipStream_t s);
-// scatter accepted correspondences to their compacted slots (pos = exclusive scan of flags)
-hipError_t launch_compact(const float4* src, const float4* qbuf, const Cov3& mahal,
+// nn_pos: per source point (shard-relative) the matched target sorted position, UINT32_MAX when
+// rejected; with `seeded` its previous contents seed the exact 1-NN search.  flags: 1 if accepted.
+hipError_t launch_correspond(const GridView& tgt, const float4* src, size_t p0, size_t p1, Xf34 T,
+                             double thr, int seeded, uint32_t* nn_pos, uint32_t* flags,
+                             hipStream_t s);
+// accepted correspondences -> compacted slots (pos = exclusive scan of flags), computing the
+// Mahalanobis matrices on the way
+hipError_t launch_compact(const float4* src, const float4* tpts, const Cov3& cov_s,
+                          const Cov3& cov_t, Rot33d R, const uint32_t* nn_pos,
                           const uint32_t* flags, const uint32_t* pos, size_t p0, size_t p1,
                           CorrSoA out, hipStream_t s);
 // objective pass over m compacted correspondences (+ in-launch finish)

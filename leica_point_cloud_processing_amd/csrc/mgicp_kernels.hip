@@ -18,6 +18,9 @@
 #ifndef MGICP_NN_UNROLL
 #define MGICP_NN_UNROLL 4  // candidate gathers in flight per lane in the 1-NN scans
 #endif
+#ifndef MGICP_CORR_WAVES
+#define MGICP_CORR_WAVES 1  // minimum resident waves per SIMD requested for the 1-NN kernel
+#endif
 
 #include "mgicp_internal.hpp"
 
@@ -496,12 +499,12 @@ __device__ __forceinline__ void load_cov(const Cov3& c, size_t i, double M[3][3]
   M[2][0] = b.x; M[2][1] = d.x; M[2][2] = d.y;
 }
 
-__global__ __launch_bounds__(256) void correspond_kernel(GridView tg, Cov3 cov_t,
-                                                         const float4* __restrict__ src,
-                                                         Cov3 cov_s, size_t p0, size_t p1,
-                                                         Xf34 T, Rot33d R, double thr,
-                                                         float4* __restrict__ qbuf, Cov3 mahal,
-                                                         int* dbg_nn, uint32_t* __restrict__ prev_pos,
+// Exact radius-gated 1-NN of T*s for every source point of the shard.  The search is
+// latency-bound on dependent candidate gathers, so this kernel does nothing else: it keeps a
+// small register footprint (occupancy) and leaves the fp64 Mahalanobis work to the compaction.
+__global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_kernel(GridView tg, const float4* __restrict__ src,
+                                                         size_t p0, size_t p1, Xf34 T, double thr,
+                                                         int seeded, uint32_t* __restrict__ nn_pos,
                                                          uint32_t* __restrict__ flags) {
   const size_t p = p0 + static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (p >= p1) return;
@@ -510,48 +513,54 @@ __global__ __launch_bounds__(256) void correspond_kernel(GridView tg, Cov3 cov_t
   xform(T, s.x, s.y, s.z, qx, qy, qz);
   NnVisitor vis;
   vis.init(qx, qy, qz, thr);
-  if (prev_pos) {
+  if (seeded) {
     // seed with last iteration's match: a real candidate, so the exact search only tightens it,
     // and the ball-cell pruning starts from a near-final radius
-    const uint32_t pp = prev_pos[p - p0];
+    const uint32_t pp = nn_pos[p - p0];
     if (pp != 0xffffffffu) vis.range(tg, pp, pp + 1);
   }
   ring_search(tg, qx, qy, qz, vis);
   const bool ok = vis.best != ~0ull &&
                   static_cast<double>(__uint_as_float(static_cast<uint32_t>(vis.best >> 32))) < thr;
-  if (prev_pos) prev_pos[p - p0] = ok ? vis.pos : 0xffffffffu;
-  if (flags) flags[p - p0] = ok ? 1u : 0u;
-  if (!ok) {
-    qbuf[p] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (dbg_nn) {
-      dbg_nn[p] = -1;
-      mahal.a[p] = make_double2(0.0, 0.0);
-      mahal.b[p] = make_double2(0.0, 0.0);
-      mahal.c[p] = make_double2(0.0, 0.0);
-    }
-    return;
-  }
-  const float4 t = tg.pts[vis.pos];
+  nn_pos[p - p0] = ok ? vis.pos : 0xffffffffu;
+  flags[p - p0] = ok ? 1u : 0u;
+}
+
+// Accepted correspondence p -> compacted slot pos[p]: the matched target point and the
+// Mahalanobis matrix M = (R Cs R' + Ct)^-1 in fp64 with Eigen's 3x3 cofactor inverse
+// (gicp.hpp computeTransformation), written straight into the SoA streams.
+__global__ __launch_bounds__(256) void compact_kernel(const float4* __restrict__ src,
+                                                      const float4* __restrict__ tpts, Cov3 cov_s,
+                                                      Cov3 cov_t, Rot33d R,
+                                                      const uint32_t* __restrict__ nn_pos,
+                                                      const uint32_t* __restrict__ flags,
+                                                      const uint32_t* __restrict__ pos, size_t p0,
+                                                      size_t p1, CorrSoA o) {
+  const size_t p = p0 + static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (p >= p1 || !flags[p - p0]) return;
+  const uint32_t j = nn_pos[p - p0];
+  const size_t i = pos[p - p0];
+  const float4 s = src[p], t = tpts[j];
   double C1[3][3], C2[3][3], RC[3][3], tm[3][3];
   load_cov(cov_s, p, C1);
-  load_cov(cov_t, vis.pos, C2);
+  load_cov(cov_t, j, C2);
 #pragma unroll
-  for (int i = 0; i < 3; ++i)
+  for (int r = 0; r < 3; ++r)
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      double a = R.m[3 * i + 0] * C1[0][j];
-      a = a + R.m[3 * i + 1] * C1[1][j];
-      a = a + R.m[3 * i + 2] * C1[2][j];
-      RC[i][j] = a;
+    for (int c = 0; c < 3; ++c) {
+      double a = R.m[3 * r + 0] * C1[0][c];
+      a = a + R.m[3 * r + 1] * C1[1][c];
+      a = a + R.m[3 * r + 2] * C1[2][c];
+      RC[r][c] = a;
     }
 #pragma unroll
-  for (int i = 0; i < 3; ++i)
+  for (int r = 0; r < 3; ++r)
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      double a = RC[i][0] * R.m[3 * j + 0];
-      a = a + RC[i][1] * R.m[3 * j + 1];
-      a = a + RC[i][2] * R.m[3 * j + 2];
-      tm[i][j] = a + C2[i][j];
+    for (int c = 0; c < 3; ++c) {
+      double a = RC[r][0] * R.m[3 * c + 0];
+      a = a + RC[r][1] * R.m[3 * c + 1];
+      a = a + RC[r][2] * R.m[3 * c + 2];
+      tm[r][c] = a + C2[r][c];
     }
 #define COF(i, j) (tm[((i) + 1) % 3][((j) + 1) % 3] * tm[((i) + 2) % 3][((j) + 2) % 3] - \
                    tm[((i) + 1) % 3][((j) + 2) % 3] * tm[((i) + 2) % 3][((j) + 1) % 3])
@@ -561,14 +570,15 @@ __global__ __launch_bounds__(256) void correspond_kernel(GridView tg, Cov3 cov_t
   det = det + c20 * tm[2][0];
   const double inv = 1.0 / det;
   // Eigen: result(i, j) = cofactor(j, i) / det; keep the upper triangle
-  const double m00 = c00 * inv, m01 = c10 * inv, m02 = c20 * inv;
-  const double m11 = COF(1, 1) * inv, m12 = COF(2, 1) * inv, m22 = COF(2, 2) * inv;
+  o.m00[i] = c00 * inv;
+  o.m01[i] = c10 * inv;
+  o.m02[i] = c20 * inv;
+  o.m11[i] = COF(1, 1) * inv;
+  o.m12[i] = COF(2, 1) * inv;
+  o.m22[i] = COF(2, 2) * inv;
 #undef COF
-  qbuf[p] = make_float4(t.x, t.y, t.z, 1.f);
-  mahal.a[p] = make_double2(m00, m01);
-  mahal.b[p] = make_double2(m02, m11);
-  mahal.c[p] = make_double2(m12, m22);
-  if (dbg_nn) dbg_nn[p] = static_cast<int>(__float_as_uint(t.w));
+  o.sx[i] = s.x; o.sy[i] = s.y; o.sz[i] = s.z;
+  o.qx[i] = t.x; o.qy[i] = t.y; o.qz[i] = t.z;
 }
 
 // ------------------------------------------------------------------------------------
@@ -663,20 +673,6 @@ __device__ __forceinline__ void finish_in_last_block(const double* partial, unsi
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (threadIdx.x == 0) __hip_atomic_store(done_flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-}
-
-__global__ void compact_kernel(const float4* __restrict__ src, const float4* __restrict__ qbuf,
-                               Cov3 mahal, const uint32_t* __restrict__ flags,
-                               const uint32_t* __restrict__ pos, size_t p0, size_t p1, CorrSoA o) {
-  const size_t p = p0 + static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (p >= p1 || !flags[p - p0]) return;
-  const size_t i = pos[p - p0];
-  const float4 s = src[p], q = qbuf[p];
-  const double2 a = mahal.a[p], b = mahal.b[p], c = mahal.c[p];
-  o.sx[i] = s.x; o.sy[i] = s.y; o.sz[i] = s.z;
-  o.qx[i] = q.x; o.qy[i] = q.y; o.qz[i] = q.z;
-  o.m00[i] = a.x; o.m01[i] = a.y; o.m02[i] = b.x;
-  o.m11[i] = b.y; o.m12[i] = c.x; o.m22[i] = c.y;
 }
 
 // one correspondence of OptimizationFunctorWithIndices::fdf: pp = A s (fp32, Eigen order),
@@ -910,21 +906,21 @@ hipError_t launch_knn_cov(const GridView& g, int k, double eps, size_t p0, size_
   }
 }
 
-hipError_t launch_correspond(const GridView& tgt, const Cov3& cov_t, const float4* src,
-                             const Cov3& cov_s, size_t p0, size_t p1, Xf34 T, Rot33d R,
-                             double thr, float4* qbuf, Cov3 mahal, int* dbg_nn,
-                             uint32_t* prev_pos, uint32_t* flags, hipStream_t s) {
+hipError_t launch_correspond(const GridView& tgt, const float4* src, size_t p0, size_t p1, Xf34 T,
+                             double thr, int seeded, uint32_t* nn_pos, uint32_t* flags,
+                             hipStream_t s) {
   if (p1 <= p0) return hipSuccess;
-  correspond_kernel<<<nblk(p1 - p0), 256, 0, s>>>(tgt, cov_t, src, cov_s, p0, p1, T, R, thr,
-                                                  qbuf, mahal, dbg_nn, prev_pos, flags);
+  correspond_kernel<<<nblk(p1 - p0), 256, 0, s>>>(tgt, src, p0, p1, T, thr, seeded, nn_pos, flags);
   return hipGetLastError();
 }
 
-hipError_t launch_compact(const float4* src, const float4* qbuf, const Cov3& mahal,
+hipError_t launch_compact(const float4* src, const float4* tpts, const Cov3& cov_s,
+                          const Cov3& cov_t, Rot33d R, const uint32_t* nn_pos,
                           const uint32_t* flags, const uint32_t* pos, size_t p0, size_t p1,
                           CorrSoA out, hipStream_t s) {
   if (p1 <= p0) return hipSuccess;
-  compact_kernel<<<nblk(p1 - p0), 256, 0, s>>>(src, qbuf, mahal, flags, pos, p0, p1, out);
+  compact_kernel<<<nblk(p1 - p0), 256, 0, s>>>(src, tpts, cov_s, cov_t, R, nn_pos, flags, pos, p0,
+                                               p1, out);
   return hipGetLastError();
 }
 

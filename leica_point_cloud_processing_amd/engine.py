@@ -267,9 +267,9 @@ class GICPEngine:
         self._check(self._lib.mgicp_set_profiling(self._h, int(on)), "set_profiling")
 
     def kernel_times(self):
-        ms = np.zeros(4, np.float64)
-        cnt = np.zeros(4, np.int32)
+        ms = np.zeros(5, np.float64)
+        cnt = np.zeros(5, np.int32)
         self._check(self._lib.mgicp_debug_kernel_times(self._h, _dp(ms), cnt.ctypes.data_as(ctypes.POINTER(ctypes.c_int))),
                     "kernel_times")
-        names = ["knn_cov", "correspond", "fdf", "reduce_finish"]
-        return {names[i]: {"avg_ms": float(ms[i]), "count": int(cnt[i])} for i in range(4)}
+        names = ["knn_cov", "correspond", "fdf", "reduce_finish", "compact"]
+        return {names[i]: {"avg_ms": float(ms[i]), "count": int(cnt[i])} for i in range(5)}
