@@ -18,10 +18,13 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/mi355x_gicp.h"
+#include "host_upload.hpp"
 #include "mgicp_internal.hpp"
 #include "pcl_bfgs.hpp"
 
@@ -30,6 +33,7 @@ using namespace mgicp;
 namespace {
 
 constexpr double kDefaultOccupancy = 12.0;          // mean points per non-empty cell
+constexpr size_t kSmallBytes = size_t(64) << 10;  // pinned readback scratch per context
 constexpr size_t kMaxCells = size_t(1) << 29;       // dense cell table cap (2 GiB of uint32)
 
 double now_ms() {
@@ -37,6 +41,19 @@ double now_ms() {
              std::chrono::steady_clock::now().time_since_epoch())
       .count();
 }
+
+// MGICP_TRACE=1: phase timestamps of uploads and grid builds on stderr (host-time diagnosis)
+bool trace_on() {
+  static const int on = [] {
+    const char* t = std::getenv("MGICP_TRACE");
+    return t && std::atoi(t) != 0 ? 1 : 0;
+  }();
+  return on != 0;
+}
+#define MGICP_TRACE_AT(label)                                                  \
+  do {                                                                         \
+    if (trace_on()) std::fprintf(stderr, "[mgicp] %10.3f ms  %s\n", now_ms(), label); \
+  } while (0)
 
 struct Mat4 {  // row-major float 4x4
   float m[4][4];
@@ -159,13 +176,16 @@ template <class T>
 struct DevBuf {
   T* p = nullptr;
   size_t cap = 0;
+  // grows by >= 1/4 so that a sequence of slightly larger requests (grid sizing iterations,
+  // the second cloud) does not pay a hipFree/hipMalloc pair each time
   hipError_t reserve(size_t n) {
     if (n <= cap && p) return hipSuccess;
+    const size_t want = std::max<size_t>(std::max<size_t>(n, 1), cap ? cap + cap / 4 : 0);
     if (p) (void)hipFree(p);
     p = nullptr;
     cap = 0;
-    hipError_t e = hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T));
-    if (e == hipSuccess) cap = std::max<size_t>(n, 1);
+    hipError_t e = hipMalloc(&p, want * sizeof(T));
+    if (e == hipSuccess) cap = want;
     return e;
   }
   void release() {
@@ -214,6 +234,9 @@ struct mgicp_ctx {
   // Infinity Cache, so each pass re-reads the previous pass's tail from it (73 -> 68 us)
   bool alt_sweep = true;                 // (env MGICP_FDF_ALT)
   double ms_upload_pending = 0;
+  // host uploads go through the process-wide HostUploader (host_upload.hpp)
+  int host_threads = 8;                  // packing workers (env MGICP_HOST_THREADS)
+  DevBuf<float> xyz_dev;                 // packed xyz landing zone
   // per source point (sorted), rank shard only
   DevBuf<float4> src_out;  // guess-applied source (only when guess != I)
   const float4* d_out = nullptr;
@@ -228,6 +251,8 @@ struct mgicp_ctx {
   bool seed_valid = false;
   DevBuf<double> partial;
   DevBuf<double> red;      // kRedVals
+  unsigned char* h_small = nullptr;  // pinned, mapped host scratch (kSmallBytes) for small readbacks
+  unsigned char* d_small = nullptr;  // its device address (kernels write results there directly)
   double* h_red = nullptr;   // pinned, mapped, coherent host memory
   double* d_h_red = nullptr; // its device address
   unsigned long long* h_flag = nullptr;  // pass-completion word (host / device views)
@@ -337,17 +362,27 @@ int upload_cloud(mgicp_ctx* ctx, Cloud& cl, const float* xyz, size_t n, size_t s
   if (n == 0 || !xyz || stride < 12 || (stride % 4) != 0)
     return fail(ctx, MGICP_E_INVALID, "invalid cloud (null, empty or stride not a multiple of 4 >= 12)");
   const double t0 = now_ms();
+  MGICP_TRACE_AT("upload: begin");
   HIPCK(cl.orig.reserve(n));
+  MGICP_TRACE_AT("upload: orig reserved");
   if (device_ptr) {
     HIPCK(launch_pack_points(xyz, n, stride, cl.orig.p, ctx->stream));
   } else {
-    HIPCK(cl.raw.reserve(n * stride));
-    HIPCK(hipMemcpyAsync(cl.raw.p, xyz, n * stride, hipMemcpyHostToDevice, ctx->stream));
-    HIPCK(launch_pack_points(cl.raw.p, n, stride, cl.orig.p, ctx->stream));
+    // host workers pack xyz into pinned slots while earlier slots are in flight
+    HostUploader& up = HostUploader::instance();
+    HIPCK(up.init(ctx->host_threads));
+    HIPCK(ctx->xyz_dev.reserve(3 * n));
+    MGICP_TRACE_AT("upload: staging ready");
+    {
+      std::lock_guard<std::mutex> lk(up.mu);
+      HIPCK(upload_xyz(*up.pool, up.ring, xyz, n, stride, ctx->xyz_dev.p, ctx->stream));
+    }
+    MGICP_TRACE_AT("upload: all chunks queued");
+    HIPCK(launch_pack_points(ctx->xyz_dev.p, n, 12, cl.orig.p, ctx->stream));
   }
   int rc = sync(ctx);
   if (rc) return rc;
-  cl.raw.release();
+  MGICP_TRACE_AT("upload: synced");
   cl.n = n;
   cl.dirty = true;
   cl.have_cov = false;
@@ -364,13 +399,14 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
   hipStream_t s = ctx->stream;
   // 1. bounding box + finiteness
   const int nb = static_cast<int>(std::min<size_t>((n + 255) / 256, 1024));
-  HIPCK(ctx->fpartial.reserve(static_cast<size_t>(nb) * 8));
-  HIPCK(launch_bbox(cl.orig.p, n, ctx->fpartial.p, nb, s));
-  std::vector<float> hp(static_cast<size_t>(nb) * 8);
-  HIPCK(hipMemcpyAsync(hp.data(), ctx->fpartial.p, hp.size() * sizeof(float),
-                       hipMemcpyDeviceToHost, s));
+  MGICP_TRACE_AT("grid: begin");
+  // block partials land straight in mapped host memory (nb * 8 floats <= 32 KiB): no copy
+  HIPCK(launch_bbox(cl.orig.p, n, reinterpret_cast<float*>(ctx->d_small), nb, s));
+  const float* hp = reinterpret_cast<const float*>(ctx->h_small);
+  MGICP_TRACE_AT("grid: bbox queued");
   int rc = sync(ctx);
   if (rc) return rc;
+  MGICP_TRACE_AT("grid: bbox synced");
   float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
   double bad = 0;
   for (int b = 0; b < nb; ++b) {
@@ -411,15 +447,18 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
       nc = dims(h, nd);
     }
     HIPCK(ctx->counts.reserve(nc + 1));
+    MGICP_TRACE_AT("grid: counts reserved");
     HIPCK(hipMemsetAsync(ctx->counts.p, 0, (nc + 1) * sizeof(uint32_t), s));
     HIPCK(hipMemsetAsync(ctx->u64.p, 0, sizeof(unsigned long long), s));
     HIPCK(launch_cell_hist(cl.orig.p, n, mn[0], mn[1], mn[2], static_cast<float>(1.0 / h), nd[0],
                            nd[1], nd[2], ctx->counts.p, nullptr, s));
     HIPCK(launch_count_nonzero(ctx->counts.p, nc, ctx->u64.p, s));
-    unsigned long long nonempty = 0;
-    HIPCK(hipMemcpyAsync(&nonempty, ctx->u64.p, sizeof(nonempty), hipMemcpyDeviceToHost, s));
+    HIPCK(hipMemcpyAsync(ctx->h_small, ctx->u64.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     rc = sync(ctx);
     if (rc) return rc;
+    unsigned long long nonempty = 0;
+    std::memcpy(&nonempty, ctx->h_small, sizeof(nonempty));
+    MGICP_TRACE_AT("grid: sizing histogram synced");
     const double occ = static_cast<double>(n) / std::max<unsigned long long>(nonempty, 1);
     if ((occ > 0.6 * ctx->occupancy && occ < 1.6 * ctx->occupancy) || nc >= kMaxCells / 2)
       break;
@@ -448,6 +487,7 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
   HIPCK(cl.perm.reserve(n));
   HIPCK(cl.cell_start.reserve(nc + 1));
   HIPCK(cl.pts.reserve(n));
+  MGICP_TRACE_AT("grid: final buffers reserved");
   HIPCK(hipMemsetAsync(ctx->counts.p, 0, (nc + 1) * sizeof(uint32_t), s));
   HIPCK(launch_cell_hist(cl.orig.p, n, mn[0], mn[1], mn[2], inv_h, nd[0], nd[1], nd[2],
                          ctx->counts.p, ctx->keys.p, s));
@@ -460,12 +500,12 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
   HIPCK(launch_sort_pairs(ctx->scratch.p, sb, ctx->keys.p, ctx->keys_sorted.p, ctx->vals.p,
                           cl.perm.p, n, bits, s));
   HIPCK(launch_gather_sorted(cl.orig.p, cl.perm.p, n, cl.pts.p, s));
+  MGICP_TRACE_AT("grid: sort queued");
   rc = sync(ctx);
   if (rc) return rc;
-  ctx->counts.release();
-  ctx->keys.release();
-  ctx->keys_sorted.release();
-  ctx->vals.release();
+  MGICP_TRACE_AT("grid: sorted");
+  // the build scratch stays allocated for the next build (hipFree + hipMalloc of these
+  // tens-of-MB buffers cost milliseconds of host time between the two clouds' builds)
   GridView& g = cl.view;
   g.ox = mn[0];
   g.oy = mn[1];
@@ -485,6 +525,7 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
     HIPCK(ctx->scratch.reserve(nc));
     HIPCK(launch_empty_map(cl.cell_start.p, nd[0], nd[1], nd[2], cl.empty_dist.p, ctx->scratch.p, s));
     if ((rc = sync(ctx))) return rc;
+    MGICP_TRACE_AT("grid: empty map done");
     g.empty_dist = cl.empty_dist.p;
   }
   cl.ncells = nc;
@@ -494,13 +535,16 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
 }
 
 int compute_cov(mgicp_ctx* ctx, Cloud& cl, size_t p0, size_t p1) {
+  MGICP_TRACE_AT("cov: begin");
   HIPCK(cl.cov.reserve(3 * cl.n));
+  MGICP_TRACE_AT("cov: reserved");
   {
     ProfScope ps(ctx, kFamCov);
     HIPCK(launch_knn_cov(cl.view, ctx->prm.k, ctx->prm.gicp_eps, p0, p1, cl.cov3(), ctx->stream));
   }
   int rc = sync(ctx);
   if (rc) return rc;
+  MGICP_TRACE_AT("cov: done");
   cl.have_cov = true;
   cl.cov_p0 = p0;
   cl.cov_p1 = p1;
@@ -637,10 +681,11 @@ int correspond(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
                          rot_of(T, G), ctx->prev_pos.p, ctx->flags.p, ctx->cpos.p, p0, p1,
                          corr_soa(ctx), s));
   }
-  uint32_t m = 0;
-  HIPCK(hipMemcpyAsync(&m, ctx->cpos.p + ns, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIPCK(hipMemcpyAsync(ctx->h_small, ctx->cpos.p + ns, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   int rc = sync(ctx);
   if (rc) return rc;
+  uint32_t m = 0;
+  std::memcpy(&m, ctx->h_small, sizeof(m));
   ctx->m_local = m;
   ctx->have_corr = true;
   return MGICP_OK;
@@ -834,6 +879,14 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
   if (const char* ff = std::getenv("MGICP_FUSED_FINISH")) ctx->fused_finish = std::atoi(ff) != 0;
   if (const char* fa = std::getenv("MGICP_FDF_ALT")) ctx->alt_sweep = std::atoi(fa) != 0;
   if (const char* po = std::getenv("MGICP_POLL")) ctx->poll = std::atoi(po) != 0;
+  {
+    const unsigned hc = std::thread::hardware_concurrency();
+    ctx->host_threads = static_cast<int>(std::max(1u, std::min(8u, hc ? hc : 1u)));
+    if (const char* ht = std::getenv("MGICP_HOST_THREADS")) {
+      const int v = std::atoi(ht);
+      if (v >= 1 && v <= 64) ctx->host_threads = v;
+    }
+  }
   if (const char* fb = std::getenv("MGICP_FDF_BLOCKS")) {
     const int v = std::atoi(fb);
     if (v >= 1 && v <= 65536) ctx->fdf_max_blocks = v;
@@ -863,6 +916,16 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
   ctx->tgt.want_empty_map = true;  // correspondence / fitness queries start off the surface
   if (const char* em = std::getenv("MGICP_EMPTY_MAP")) ctx->tgt.want_empty_map = std::atoi(em) != 0;
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete ctx;
+    return MGICP_E_HIP;
+  }
+  if (hipHostMalloc(reinterpret_cast<void**>(&ctx->h_small), kSmallBytes,
+                    hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->d_small), ctx->h_small, 0) != hipSuccess ||
+      preload_kernels(ctx->h_small, kSmallBytes, ctx->stream) != hipSuccess ||
+      HostUploader::instance().init(ctx->host_threads) != hipSuccess) {
+    if (ctx->h_small) (void)hipHostFree(ctx->h_small);
+    (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return MGICP_E_HIP;
   }
@@ -902,7 +965,9 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   ctx->ticket.release();
   ctx->prev_pos.release(); ctx->flags.release(); ctx->cpos.release();
   ctx->corr_f.release(); ctx->corr_d.release(); ctx->cscratch.release();
+  ctx->xyz_dev.release();
   if (ctx->h_red) (void)hipHostFree(ctx->h_red);
+  if (ctx->h_small) (void)hipHostFree(ctx->h_small);
   prof_resolve(ctx);
   for (hipEvent_t e : ctx->pool) (void)hipEventDestroy(e);
   if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
@@ -939,10 +1004,13 @@ int mgicp_align(mgicp_ctx* ctx, const float guess_cm[16], float out_T_cm[16], mg
   mgicp_result r;
   std::memset(&r, 0, sizeof(r));
   const double t0 = now_ms();
+  MGICP_TRACE_AT("align: begin");
   int rc = prepare(ctx, true);
   if (rc) return rc;
+  MGICP_TRACE_AT("align: prepared");
   rc = ensure_iter_buffers(ctx);
   if (rc) return rc;
+  MGICP_TRACE_AT("align: iteration buffers ready");
   const double t1 = now_ms();
   const Mat4 G = guess_cm ? Mat4::from_cm(guess_cm) : Mat4::identity();
   if ((rc = set_output(ctx, G))) return rc;

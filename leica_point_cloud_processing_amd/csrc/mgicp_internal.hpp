@@ -104,6 +104,9 @@ size_t scan_scratch_bytes(size_t n);
 hipError_t launch_exclusive_scan(void* scratch, size_t scratch_bytes, const uint32_t* in,
                                  uint32_t* out, size_t n, hipStream_t s);
 hipError_t launch_iota(uint32_t* v, size_t n, hipStream_t s);
+// resolve all kernels once (moves the code-object loading cost into mgicp_create)
+// and exercise both copy directions once, small and large (pinned: pinned host scratch)
+hipError_t preload_kernels(void* pinned, size_t pinned_bytes, hipStream_t s);
 // empty-space distance map of a grid (3 separable capped min-max passes); scratch: nc bytes
 hipError_t launch_empty_map(const uint32_t* cell_start, int nx, int ny, int nz, uint8_t* out,
                             uint8_t* scratch, hipStream_t s);
