@@ -145,7 +145,6 @@ def main():
     pg.barrier()
     dt = time.perf_counter() - t0
     kt = eng.kernel_times()
-    search = eng.search_stats()
     eng.set_profiling(False)
     dt = pg.allreduce_max(dt)
     T_final = eng.getFinalTransformation()
@@ -199,7 +198,7 @@ def main():
     kernels = {
         "knn_cov": {"avg_ms": cov_ms, "points": args.n_target,
                     "algorithmic_GBps": (args.n_target * (21 * 16 + 48)) / (cov_ms * 1e-3) / 1e9 if cov_ms else None},
-        "correspond": {**kt["correspond"], "search": search},
+        "correspond": kt["correspond"],
         "compact_mahalanobis": kt["compact"],
         # correspondence + Mahalanobis = 72 B per source point (s 12, Cs 24, NN 12, Ct 24)
         "correspond_plus_mahalanobis": {

@@ -145,10 +145,6 @@ int mgicp_debug_trace(mgicp_ctx* ctx, float* out, int max_iters);
 #define MGICP_KERNEL_FAMILIES 5
 int mgicp_debug_kernel_times(mgicp_ctx* ctx, double out_ms[MGICP_KERNEL_FAMILIES],
                              int out_counts[MGICP_KERNEL_FAMILIES]);
-/* tiled 1-NN search counters accumulated while profiling is on: [0] query waves, [1] waves whose
- * staged box exceeded the LDS budget, [2] staged points, [3] queries finished by the global grid
- * search (box too wide, uncertified or over budget) */
-int mgicp_debug_search_stats(mgicp_ctx* ctx, unsigned long long out[4]);
 /* enable (1) / disable (0) per-launch HIP event timing (off by default) */
 int mgicp_set_profiling(mgicp_ctx* ctx, int on);
 

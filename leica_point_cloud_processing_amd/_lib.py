@@ -88,7 +88,6 @@ _SIGNATURES = {
     "mgicp_debug_fdf_sums": (ctypes.c_int, [_P, _DP, _DP]),
     "mgicp_debug_trace": (ctypes.c_int, [_P, _FP, ctypes.c_int]),
     "mgicp_debug_kernel_times": (ctypes.c_int, [_P, _DP, _IP]),
-    "mgicp_debug_search_stats": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_ulonglong)]),
     "mgicp_set_profiling": (ctypes.c_int, [_P, ctypes.c_int]),
 }
 

@@ -242,14 +242,6 @@ struct mgicp_ctx {
   const float4* d_out = nullptr;
   // compacted accepted correspondences of the current outer iteration (shard-relative)
   DevBuf<uint32_t> prev_pos;  // matched target sorted position per shard point (also the next 1-NN seed)
-  // tiled 1-NN: shard source positions in Morton order of their source cells (env MGICP_TILE_CORR)
-  bool tile_corr = false;  // A/B at C4: slower than the global search (profiles/r01/tile_*)
-  DevBuf<uint32_t> qorder;
-  DevBuf<uint32_t> rest;            // queries left to the global search (ns)
-  DevBuf<unsigned int> rest_count;
-  bool qorder_valid = false;
-  size_t qorder_p0 = 0, qorder_p1 = 0;
-  DevBuf<unsigned int> corr_stats;  // blocks, fallback blocks, staged points (accumulated)
   DevBuf<uint32_t> flags, cpos;
   DevBuf<float> corr_f;    // 6 streams
   DevBuf<double> corr_d;   // 6 streams
@@ -351,7 +343,6 @@ void prof_resolve(mgicp_ctx* ctx) {
     if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
       ctx->fam_ms[p.fam] += ms;
       ctx->fam_cnt[p.fam] += 1;
-      if (trace_on() && p.fam != kFamFdf) std::fprintf(stderr, "[mgicp] kernel family %d: %.3f ms\n", p.fam, ms);
     }
     ctx->pool.push_back(p.a);
     ctx->pool.push_back(p.b);
@@ -540,35 +531,6 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
   cl.ncells = nc;
   cl.dirty = false;
   cl.have_cov = false;
-  if (&cl == &ctx->src) ctx->qorder_valid = false;
-  return MGICP_OK;
-}
-
-// Query order of the tiled 1-NN: the rank's shard of the grid-sorted source, stably sorted by the
-// Morton code of each point's source cell, so that 256 consecutive queries form a compact patch.
-int build_qorder(mgicp_ctx* ctx) {
-  const size_t p0 = ctx->shard_p0(), p1 = ctx->shard_p1(), ns = p1 - p0;
-  if (ctx->qorder_valid && ctx->qorder_p0 == p0 && ctx->qorder_p1 == p1) return MGICP_OK;
-  const GridView& g = ctx->src.view;
-  const int maxdim = std::max(g.nx, std::max(g.ny, g.nz));
-  int shift = 0;
-  while (((maxdim - 1) >> shift) >= 1024) ++shift;
-  HIPCK(ctx->qorder.reserve(ns + 1));
-  HIPCK(ctx->rest.reserve(ns + 1));
-  HIPCK(ctx->rest_count.reserve(1));
-  HIPCK(ctx->keys.reserve(ns + 1));
-  HIPCK(ctx->keys_sorted.reserve(ns + 1));
-  HIPCK(ctx->vals.reserve(ns + 1));
-  const size_t sb = sort_scratch_bytes(ns, 30);
-  HIPCK(ctx->scratch.reserve(sb));
-  HIPCK(launch_morton_keys(g, p0, ns, shift, ctx->keys.p, ctx->vals.p, ctx->stream));
-  HIPCK(launch_sort_pairs(ctx->scratch.p, sb, ctx->keys.p, ctx->keys_sorted.p, ctx->vals.p,
-                          ctx->qorder.p, ns, 30, ctx->stream));
-  int rc = sync(ctx);
-  if (rc) return rc;
-  ctx->qorder_valid = true;
-  ctx->qorder_p0 = p0;
-  ctx->qorder_p1 = p1;
   return MGICP_OK;
 }
 
@@ -600,7 +562,6 @@ int prepare(mgicp_ctx* ctx, bool need_cov) {
   int rc;
   if (ctx->tgt.dirty && (rc = build_grid(ctx, ctx->tgt))) return rc;
   if (ctx->src.dirty && (rc = build_grid(ctx, ctx->src))) return rc;
-  if (ctx->tile_corr && (rc = build_qorder(ctx))) return rc;
   if (!need_cov) return MGICP_OK;
   if (!ctx->tgt.have_cov && (rc = compute_cov(ctx, ctx->tgt, 0, ctx->tgt.n))) return rc;
   if (!ctx->src.have_cov || ctx->src.cov_p0 != ctx->shard_p0() || ctx->src.cov_p1 != ctx->shard_p1())
@@ -708,14 +669,8 @@ int correspond(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
   HIPCK(hipMemsetAsync(ctx->flags.p + ns, 0, sizeof(uint32_t), s));
   {
     ProfScope ps(ctx, kFamCorr);
-    if (ctx->tile_corr)
-      HIPCK(launch_correspond_tile(ctx->tgt.view, ctx->d_out, ctx->qorder.p, ns, p0, T.xf(), thr,
-                                   seeded ? 1 : 0, ctx->prev_pos.p, ctx->flags.p, ctx->rest.p,
-                                   ctx->rest_count.p, ctx->profiling ? ctx->corr_stats.p : nullptr,
-                                   s));
-    else
-      HIPCK(launch_correspond(ctx->tgt.view, ctx->d_out, p0, p1, T.xf(), thr, seeded ? 1 : 0,
-                              ctx->prev_pos.p, ctx->flags.p, s));
+    HIPCK(launch_correspond(ctx->tgt.view, ctx->d_out, p0, p1, T.xf(), thr, seeded ? 1 : 0,
+                            ctx->prev_pos.p, ctx->flags.p, s));
   }
   ctx->seed_valid = true;
   const size_t sb = scan_scratch_bytes(ns + 1);
@@ -924,7 +879,6 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
   if (const char* ff = std::getenv("MGICP_FUSED_FINISH")) ctx->fused_finish = std::atoi(ff) != 0;
   if (const char* fa = std::getenv("MGICP_FDF_ALT")) ctx->alt_sweep = std::atoi(fa) != 0;
   if (const char* po = std::getenv("MGICP_POLL")) ctx->poll = std::atoi(po) != 0;
-  if (const char* tc = std::getenv("MGICP_TILE_CORR")) ctx->tile_corr = std::atoi(tc) != 0;
   {
     const unsigned hc = std::thread::hardware_concurrency();
     ctx->host_threads = static_cast<int>(std::max(1u, std::min(8u, hc ? hc : 1u)));
@@ -1010,7 +964,6 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   ctx->fpartial.release();
   ctx->ticket.release();
   ctx->prev_pos.release(); ctx->flags.release(); ctx->cpos.release();
-  ctx->qorder.release(); ctx->corr_stats.release(); ctx->rest.release(); ctx->rest_count.release();
   ctx->corr_f.release(); ctx->corr_d.release(); ctx->cscratch.release();
   ctx->xyz_dev.release();
   if (ctx->h_red) (void)hipHostFree(ctx->h_red);
@@ -1364,29 +1317,12 @@ int mgicp_debug_kernel_times(mgicp_ctx* ctx, double out_ms[MGICP_KERNEL_FAMILIES
   return MGICP_OK;
 }
 
-int mgicp_debug_search_stats(mgicp_ctx* ctx, unsigned long long out[4]) {
-  if (!ctx || !out) return MGICP_E_INVALID;
-  out[0] = out[1] = out[2] = out[3] = 0;
-  if (!ctx->corr_stats.p) return MGICP_OK;
-  HIPCK(hipSetDevice(ctx->device));
-  unsigned int h[4] = {0, 0, 0, 0};
-  HIPCK(hipStreamSynchronize(ctx->stream));
-  HIPCK(hipMemcpy(h, ctx->corr_stats.p, sizeof(h), hipMemcpyDeviceToHost));
-  for (int i = 0; i < 4; ++i) out[i] = h[i];
-  return MGICP_OK;
-}
-
 int mgicp_set_profiling(mgicp_ctx* ctx, int on) {
   if (!ctx) return MGICP_E_INVALID;
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
   prof_resolve(ctx);
   ctx->profiling = on != 0;
-  if (ctx->profiling) {
-    if (ctx->corr_stats.reserve(4) != hipSuccess ||
-        hipMemset(ctx->corr_stats.p, 0, 4 * sizeof(unsigned int)) != hipSuccess)
-      return fail(ctx, MGICP_E_HIP, "profiling counters");
-  }
   for (int i = 0; i < kFams; ++i) {
     ctx->fam_ms[i] = 0;
     ctx->fam_cnt[i] = 0;

@@ -31,19 +31,6 @@ struct GridView {
 
 constexpr int kEmptyCap = 15;
 
-// LDS budget of the tiled 1-NN (correspond_tile_kernel): target points, box cells and box rows
-// one 256-query block may stage (~54 KB of LDS at 3072 points: two blocks per CU)
-#ifndef MGICP_TILE_PTS
-#define MGICP_TILE_PTS 3072
-#endif
-#ifndef MGICP_TILE_R0
-#define MGICP_TILE_R0 2.0f
-#endif
-constexpr int kTilePts = MGICP_TILE_PTS;
-constexpr int kTileCells = 2048;
-constexpr int kTileRows = 256;
-constexpr float kTileR0Cells = MGICP_TILE_R0;  // widest per-query ball staged (cells)
-
 struct Cov3 {  // SoA triple of double2 arrays
   double2* a;  // {m00, m01}
   double2* b;  // {m02, m11}
@@ -88,17 +75,6 @@ hipError_t launch_knn_cov(const GridView& g, int k, double eps, size_t p0, size_
 hipError_t launch_correspond(const GridView& tgt, const float4* src, size_t p0, size_t p1, Xf34 T,
                              double thr, int seeded, uint32_t* nn_pos, uint32_t* flags,
                              hipStream_t s);
-// tiled form of the same search over queries qorder[0..ns) (Morton order of their source cells);
-// stats (nullable, 4 counters): waves, waves whose box exceeded the LDS budget, staged points,
-// queries finished by the global search
-// rest: ns-long scratch list, rest_count: one device counter
-hipError_t launch_correspond_tile(const GridView& tgt, const float4* src, const uint32_t* qorder,
-                                  size_t ns, size_t p0, Xf34 T, double thr, int seeded,
-                                  uint32_t* nn_pos, uint32_t* flags, uint32_t* rest,
-                                  unsigned int* rest_count, unsigned int* stats, hipStream_t s);
-// Morton keys (10 bits per axis of cell >> shift) of points [p0, p0 + n) and vals = positions
-hipError_t launch_morton_keys(const GridView& g, size_t p0, size_t n, int shift, uint32_t* keys,
-                              uint32_t* vals, hipStream_t s);
 // accepted correspondences -> compacted slots (pos = exclusive scan of flags), computing the
 // Mahalanobis matrices on the way
 hipError_t launch_compact(const float4* src, const float4* tpts, const Cov3& cov_s,

@@ -18,9 +18,6 @@
 #ifndef MGICP_NN_UNROLL
 #define MGICP_NN_UNROLL 4  // candidate gathers in flight per lane in the 1-NN scans
 #endif
-#ifndef MGICP_RING_BATCH
-#define MGICP_RING_BATCH 0  // batched row-bound loads in the 1-NN ring search (A/B: slower, more VGPRs)
-#endif
 #ifndef MGICP_CORR_WAVES
 #define MGICP_CORR_WAVES 1  // minimum resident waves per SIMD requested for the 1-NN kernel
 #endif
@@ -153,93 +150,6 @@ __device__ __forceinline__ void ring_search(const GridView& g, float qx, float q
       }
     }
   }
-}
-
-// Same traversal and the same exactness argument as ring_search, but the cell-range bounds of up
-// to 4 rows (or row ends) are collected first and loaded together, so a ring costs one round trip
-// for its bounds instead of one per row.  The pruning radius used to collect a batch may be a
-// little stale (it only shrinks while the batch is scanned): stale = wider = still exact.
-template <class V>
-__device__ __forceinline__ void ring_search_batched(const GridView& g, float qx, float qy, float qz,
-                                                    V& vis) {
-  const int cx = qcell(qx, g.ox, g.inv_h), cy = qcell(qy, g.oy, g.inv_h),
-            cz = qcell(qz, g.oz, g.inv_h);
-  int rmin = max(max(dist_out(cx, g.nx), dist_out(cy, g.ny)), dist_out(cz, g.nz));
-  if (rmin == 0 && g.empty_dist) {
-    rmin = g.empty_dist[static_cast<size_t>(cx) +
-                        static_cast<size_t>(g.nx) * (static_cast<size_t>(cy) + static_cast<size_t>(g.ny) * cz)];
-  }
-  const uint32_t* cs = g.cell_start;
-  // up to four pending cell ranges [a, b) of the dense cell table (cells < 2^29 + 1)
-  uint32_t a0 = 0, b0 = 0, a1 = 0, b1 = 0, a2 = 0, b2 = 0, a3 = 0, b3 = 0;
-  int nb = 0;
-#define MGICP_PUSH(A, B)                                 \
-  do {                                                   \
-    const uint32_t pa_ = (A), pb_ = (B);                 \
-    a3 = nb == 3 ? pa_ : a3; b3 = nb == 3 ? pb_ : b3;    \
-    a2 = nb == 2 ? pa_ : a2; b2 = nb == 2 ? pb_ : b2;    \
-    a1 = nb == 1 ? pa_ : a1; b1 = nb == 1 ? pb_ : b1;    \
-    a0 = nb == 0 ? pa_ : a0; b0 = nb == 0 ? pb_ : b0;    \
-    ++nb;                                                \
-  } while (0)
-#define MGICP_FLUSH()                                                        \
-  do {                                                                       \
-    if (nb > 0) {                                                            \
-      const uint32_t s0 = cs[a0], e0 = cs[b0];                               \
-      const uint32_t s1 = nb > 1 ? cs[a1] : 0u, e1 = nb > 1 ? cs[b1] : 0u;   \
-      const uint32_t s2 = nb > 2 ? cs[a2] : 0u, e2 = nb > 2 ? cs[b2] : 0u;   \
-      const uint32_t s3 = nb > 3 ? cs[a3] : 0u, e3 = nb > 3 ? cs[b3] : 0u;   \
-      vis.range(g, s0, e0);                                                  \
-      vis.range(g, s1, e1);                                                  \
-      vis.range(g, s2, e2);                                                  \
-      vis.range(g, s3, e3);                                                  \
-      nb = 0;                                                                \
-    }                                                                        \
-  } while (0)
-  for (int r = rmin; r < (1 << 22); ++r) {
-    if (r > 0) {
-      const float L = fminf(fminf(axis_bound(qx, g.ox, g.h, cx, r - 1, g.nx),
-                                  axis_bound(qy, g.oy, g.h, cy, r - 1, g.ny)),
-                            axis_bound(qz, g.oz, g.h, cz, r - 1, g.nz));
-      if (L == INFINITY) return;  // every cell visited
-      const float Ls = L * 0.99999f - g.slop;
-      if (vis.done(Ls)) return;
-    }
-    const int x0 = cx - r, x1 = cx + r, y0 = cy - r, y1 = cy + r, z0 = cz - r, z1 = cz + r;
-    const int xlo = max(x0, 0), xhi = min(x1, g.nx - 1);
-    const int ylo = max(y0, 0), yhi = min(y1, g.ny - 1);
-    const int zlo = max(z0, 0), zhi = min(z1, g.nz - 1);
-    for (int z = zlo; z <= zhi; ++z) {
-      const bool zf = (z == z0) || (z == z1);
-      const float gz = cell_gap(qz, g.oz, g.h, z, g.slop);
-      for (int y = ylo; y <= yhi; ++y) {
-        const float w = vis.prune2() * 1.00001f;
-        const float gy = cell_gap(qy, g.oy, g.h, y, g.slop);
-        const float gyz = gy * gy + gz * gz;
-        if (gyz > w) continue;
-        const uint32_t row = (static_cast<uint32_t>(z) * g.ny + y) * g.nx;
-        if (zf || y == y0 || y == y1) {
-          const float rx = sqrtf(w - gyz) + g.slop;
-          const int xa = max(xlo, qcell(qx - rx, g.ox, g.inv_h));
-          const int xb = min(xhi, qcell(qx + rx, g.ox, g.inv_h));
-          if (xa <= xb) MGICP_PUSH(row + xa, row + xb + 1);
-        } else {
-          if (x0 >= 0) {
-            const float gx = cell_gap(qx, g.ox, g.h, x0, g.slop);
-            if (gx * gx + gyz <= w) MGICP_PUSH(row + x0, row + x0 + 1);
-          }
-          if (x1 < g.nx) {
-            const float gx = cell_gap(qx, g.ox, g.h, x1, g.slop);
-            if (gx * gx + gyz <= w) MGICP_PUSH(row + x1, row + x1 + 1);
-          }
-        }
-        if (nb >= 3) MGICP_FLUSH();
-      }
-    }
-    MGICP_FLUSH();
-  }
-#undef MGICP_PUSH
-#undef MGICP_FLUSH
 }
 
 // exact k-NN visitor: register-resident sorted list of (d2, index) keys
@@ -609,306 +519,11 @@ __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_kernel(GridV
     const uint32_t pp = nn_pos[p - p0];
     if (pp != 0xffffffffu) vis.range(tg, pp, pp + 1);
   }
-#if MGICP_RING_BATCH
-  ring_search_batched(tg, qx, qy, qz, vis);
-#else
   ring_search(tg, qx, qy, qz, vis);
-#endif
   const bool ok = vis.best != ~0ull &&
                   static_cast<double>(__uint_as_float(static_cast<uint32_t>(vis.best >> 32))) < thr;
   nn_pos[p - p0] = ok ? vis.pos : 0xffffffffu;
   flags[p - p0] = ok ? 1u : 0u;
-}
-
-// ------------------------------------------------------------------------------------
-// LDS-tiled exact 1-NN (the correspondence sweep's search)
-// ------------------------------------------------------------------------------------
-// Queries are taken in Morton order of their source cell (qorder), so the 256 queries of a
-// block form a compact patch.  Each query has a search ball whose float d2 bound w is
-//   min(d2 to last iteration's match, R0^2, gate) with R0 = kTileR0Cells cells -- the match is a
-//   real target point, so the nearest point is no farther; beyond the gate the query is rejected
-//   anyway; the result is certified when the best d2 found lies inside the staged ball.
-// The block stages the target points of the union of the balls' cell boxes in LDS (rows of cells
-// are contiguous ranges of the sorted target array: coalesced row copies) and every query scans
-// its own box there with ball-cell pruning.  A query that found nothing within its staged ball,
-// or every query of a block whose union box exceeds the LDS budget, goes to a compacted list that correspond_rest_kernel finishes with the
-// global ring search, seeded with the best candidate found so far.  Exact in every case: same
-// float d2, same (d2, original index) key and tie rule as ring_search.
-__device__ __forceinline__ uint32_t spread10(uint32_t v) {
-  v &= 0x3ffu;
-  v = (v | (v << 16)) & 0x030000FFu;
-  v = (v | (v << 8)) & 0x0300F00Fu;
-  v = (v | (v << 4)) & 0x030C30C3u;
-  v = (v | (v << 2)) & 0x09249249u;
-  return v;
-}
-
-__global__ void morton_keys_kernel(GridView g, size_t p0, size_t n, int shift,
-                                   uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
-  const size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const float4 p = g.pts[p0 + i];
-  const uint32_t cx = static_cast<uint32_t>(bcell(p.x, g.ox, g.inv_h, g.nx)) >> shift;
-  const uint32_t cy = static_cast<uint32_t>(bcell(p.y, g.oy, g.inv_h, g.ny)) >> shift;
-  const uint32_t cz = static_cast<uint32_t>(bcell(p.z, g.oz, g.inv_h, g.nz)) >> shift;
-  keys[i] = spread10(cx) | (spread10(cy) << 1) | (spread10(cz) << 2);
-  vals[i] = static_cast<uint32_t>(p0 + i);
-}
-
-__device__ __forceinline__ int wave_min(int v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off, 64));
-  return v;
-}
-__device__ __forceinline__ int wave_max(int v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off, 64));
-  return v;
-}
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t t = __shfl_up(v, off, 64);
-    if (lane >= off) v += t;
-  }
-  return v;
-}
-
-// inclusive scan of one value per thread over a 256-thread block (wsum: 4 LDS slots)
-__device__ __forceinline__ uint32_t block_scan256(uint32_t v, uint32_t* wsum) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t t = __shfl_up(v, off, 64);
-    if (lane >= off) v += t;
-  }
-  if (lane == 63) wsum[wid] = v;
-  __syncthreads();
-  uint32_t add = 0;
-  for (int w = 0; w < wid; ++w) add += wsum[w];
-  return v + add;
-}
-
-// center-out visiting order over [lo, hi] around c (c inside the range): c, c-1, c+1, c-2, ...
-__device__ __forceinline__ int co_steps(int c, int lo, int hi) {
-  return 2 * max(c - lo, hi - c) + 1;
-}
-__device__ __forceinline__ int co_at(int c, int k) {
-  return c + ((k & 1) ? -((k + 1) >> 1) : (k >> 1));
-}
-
-__global__ __launch_bounds__(256) void correspond_tile_kernel(
-    GridView tg, const float4* __restrict__ src, const uint32_t* __restrict__ qorder, size_t ns,
-    size_t p0, Xf34 T, double thr, int seeded, uint32_t* __restrict__ nn_pos,
-    uint32_t* __restrict__ flags, uint32_t* __restrict__ rest, unsigned int* __restrict__ rest_count,
-    unsigned int* __restrict__ stats) {
-  __shared__ float4 tile[kTilePts];
-  __shared__ uint16_t lcs[kTileCells + 1];
-  __shared__ uint32_t row_g[kTileRows];
-  __shared__ uint32_t row_o[kTileRows + 1];
-  __shared__ int box[6];
-  __shared__ uint32_t wsum[4];
-  const int tid = threadIdx.x, lane = tid & 63;
-  if (tid < 3) box[tid] = 0x7fffffff;
-  else if (tid < 6) box[tid] = -0x7fffffff;
-  const size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + tid;
-  const bool valid = i < ns;
-  size_t p = 0;
-  float qx = 0.f, qy = 0.f, qz = 0.f;
-  NnVisitor vis;
-  vis.init(0.f, 0.f, 0.f, thr);
-  float wbox = 0.f;  // every point that can still win / be accepted has float d2 <= wbox
-  int xa = 0, xb = -1, ya = 0, yb = -1, za = 0, zb = -1;
-  if (valid) {
-    p = qorder[i];
-    const float4 s = src[p];
-    xform(T, s.x, s.y, s.z, qx, qy, qz);
-    vis.init(qx, qy, qz, thr);
-    if (seeded) {
-      const uint32_t pp = nn_pos[p - p0];
-      if (pp != 0xffffffffu) vis.range(tg, pp, pp + 1);
-    }
-    // stage at most the R0 ball (a stale seed after a large transform update can be centimetres
-    // away); the result is certified below when it lies inside the staged ball
-    const float r0 = kTileR0Cells * tg.h;
-    wbox = fminf(vis.prune2(), r0 * r0);
-    const float rad = sqrtf(wbox * 1.00001f) + tg.slop;
-    xa = max(0, qcell(qx - rad, tg.ox, tg.inv_h));
-    xb = min(tg.nx - 1, qcell(qx + rad, tg.ox, tg.inv_h));
-    ya = max(0, qcell(qy - rad, tg.oy, tg.inv_h));
-    yb = min(tg.ny - 1, qcell(qy + rad, tg.oy, tg.inv_h));
-    za = max(0, qcell(qz - rad, tg.oz, tg.inv_h));
-    zb = min(tg.nz - 1, qcell(qz + rad, tg.oz, tg.inv_h));
-  }
-  const bool boxed = valid && xa <= xb && ya <= yb && za <= zb;
-  {
-    const int wx0 = wave_min(boxed ? xa : 0x7fffffff), wx1 = wave_max(boxed ? xb : -0x7fffffff);
-    const int wy0 = wave_min(boxed ? ya : 0x7fffffff), wy1 = wave_max(boxed ? yb : -0x7fffffff);
-    const int wz0 = wave_min(boxed ? za : 0x7fffffff), wz1 = wave_max(boxed ? zb : -0x7fffffff);
-    __syncthreads();  // box initialised
-    if (lane == 0 && wx0 <= wx1) {
-      atomicMin(&box[0], wx0); atomicMin(&box[1], wy0); atomicMin(&box[2], wz0);
-      atomicMax(&box[3], wx1); atomicMax(&box[4], wy1); atomicMax(&box[5], wz1);
-    }
-  }
-  __syncthreads();
-  const int X0 = box[0], Y0 = box[1], Z0 = box[2], X1 = box[3], Y1 = box[4], Z1 = box[5];
-  const bool any = X0 <= X1;
-  const long long bnx = any ? X1 - X0 + 1 : 0, bny = any ? Y1 - Y0 + 1 : 0,
-                  bnz = any ? Z1 - Z0 + 1 : 0;
-  const long long nrows = bny * bnz, ncell = bnx * nrows;
-  bool tiled = ncell <= kTileCells && nrows <= kTileRows;
-  uint32_t total = 0;
-  if (any && tiled) {
-    // one row per thread: its cell range in the sorted target array, block prefix -> LDS offsets
-    uint32_t len = 0;
-    if (tid < nrows) {
-      const int y = Y0 + static_cast<int>(tid % bny), z = Z0 + static_cast<int>(tid / bny);
-      const uint32_t* row = tg.cell_start + (static_cast<size_t>(z) * tg.ny + y) * tg.nx;
-      const uint32_t a = row[X0], b = row[X1 + 1];
-      row_g[tid] = a;
-      len = b - a;
-    }
-    const uint32_t inc = block_scan256(len, wsum);
-    if (tid < nrows) row_o[tid + 1] = inc;
-    if (tid == 0) row_o[0] = 0;
-    __syncthreads();
-    total = row_o[nrows];
-    tiled = total <= kTilePts;
-    if (tiled) {
-      const int nr = static_cast<int>(nrows), bx = static_cast<int>(bnx), by = static_cast<int>(bny);
-      // gathers four at a time per thread (independent loads in flight), then the LDS stores
-      const uint32_t tg_last = tg.cell_start[static_cast<size_t>(tg.nx) * tg.ny * tg.nz] - 1;
-      for (int c0 = tid; c0 < ncell; c0 += 4 * 256) {
-        uint32_t cv[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int c = min(c0 + u * 256, static_cast<int>(ncell) - 1);
-          const int r = c / bx, x = X0 + c - r * bx;
-          const int y = Y0 + r % by, z = Z0 + r / by;
-          cv[u] = tg.cell_start[(static_cast<size_t>(z) * tg.ny + y) * tg.nx + x];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int c = c0 + u * 256;
-          if (c < ncell) {
-            const int r = c / bx;
-            lcs[c] = static_cast<uint16_t>(row_o[r] + (cv[u] - row_g[r]));
-          }
-        }
-      }
-      for (uint32_t g0 = tid; g0 < total; g0 += 4 * 256) {
-        float4 pv[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const uint32_t gI = min(g0 + u * 256, total - 1);
-          int lo = 0;  // last row with row_o[r] <= gI (fixed-trip branchless search)
-#pragma unroll
-          for (int step = kTileRows / 2; step >= 1; step >>= 1)
-            if (lo + step < nr && row_o[lo + step] <= gI) lo += step;
-          pv[u] = tg.pts[min(row_g[lo] + (gI - row_o[lo]), tg_last)];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const uint32_t gI = g0 + u * 256;
-          if (gI < total) tile[gI] = pv[u];
-        }
-      }
-      if (tid == 0) lcs[ncell] = static_cast<uint16_t>(total);
-      __syncthreads();
-    }
-  }
-  if (stats && tid == 0) {
-    atomicAdd(&stats[0], 1u);
-    if (!tiled) atomicAdd(&stats[1], 1u);
-    else atomicAdd(&stats[2], total);
-  }
-  bool done = false;
-  if (valid && tiled) {
-    if (boxed) {
-      const int bx = static_cast<int>(bnx), by = static_cast<int>(bny);
-      const int ccz = min(max(qcell(qz, tg.oz, tg.inv_h), za), zb);
-      const int ccy = min(max(qcell(qy, tg.oy, tg.inv_h), ya), yb);
-      const int nkz = co_steps(ccz, za, zb), nky = co_steps(ccy, ya, yb);
-      for (int kz = 0; kz < nkz; ++kz) {
-        const int z = co_at(ccz, kz);
-        if (z < za || z > zb) continue;
-        const float gz = cell_gap(qz, tg.oz, tg.h, z, tg.slop);
-        for (int ky = 0; ky < nky; ++ky) {
-          const int y = co_at(ccy, ky);
-          if (y < ya || y > yb) continue;
-          const float w = fminf(vis.prune2(), wbox) * 1.00001f;
-          const float gy = cell_gap(qy, tg.oy, tg.h, y, tg.slop);
-          const float gyz = gy * gy + gz * gz;
-          if (gyz > w) continue;
-          const float rx = sqrtf(w - gyz) + tg.slop;
-          const int xl = max(xa, qcell(qx - rx, tg.ox, tg.inv_h));
-          const int xh = min(xb, qcell(qx + rx, tg.ox, tg.inv_h));
-          if (xl > xh) continue;
-          const int r = (y - Y0) + by * (z - Z0);
-          const int base = r * bx - X0;
-          const uint32_t j0 = lcs[base + xl], j1 = lcs[base + xh + 1];
-          const uint32_t gbase = row_g[r] - row_o[r];
-          for (uint32_t j = j0; j < j1; ++j) {
-            const float4 c = tile[j];
-            const unsigned long long key = mkkey(dist2(qx, qy, qz, c), c.w);
-            if (key < vis.best) {
-              vis.best = key;
-              vis.pos = gbase + j;
-            }
-          }
-        }
-      }
-    }
-    // certified when no point outside the box can beat the result: the best (or, with nothing
-    // found, the gate) lies within the staged ball
-    const float bd = vis.best == ~0ull ? vis.thr_f
-                                       : __uint_as_float(static_cast<uint32_t>(vis.best >> 32));
-    done = bd <= wbox || wbox >= vis.thr_f;  // (the whole gate ball staged: exact either way)
-  }
-  if (valid && !done) {
-    // leave the best candidate so far as the seed of the global search
-    nn_pos[p - p0] = vis.best == ~0ull ? 0xffffffffu : vis.pos;
-    const unsigned long long need = __ballot(1);
-    const unsigned int nwave = __popcll(need);
-    unsigned int base = 0;
-    const int leader = __ffsll(static_cast<long long>(need)) - 1;
-    if (lane == leader) base = atomicAdd(rest_count, nwave);
-    base = __shfl(base, leader, 64);
-    rest[base + __popcll(need & ((1ull << lane) - 1ull))] = static_cast<uint32_t>(p);
-    return;
-  }
-  if (!valid) return;
-  const bool ok = vis.best != ~0ull &&
-                  static_cast<double>(__uint_as_float(static_cast<uint32_t>(vis.best >> 32))) < thr;
-  nn_pos[p - p0] = ok ? vis.pos : 0xffffffffu;
-  flags[p - p0] = ok ? 1u : 0u;
-}
-
-// the queries the tiled pass could not certify: global ring search from the best seed so far
-__global__ __launch_bounds__(256) void correspond_rest_kernel(
-    GridView tg, const float4* __restrict__ src, const uint32_t* __restrict__ rest,
-    const unsigned int* __restrict__ rest_count, size_t p0, Xf34 T, double thr,
-    uint32_t* __restrict__ nn_pos, uint32_t* __restrict__ flags, unsigned int* __restrict__ stats) {
-  const unsigned int n = *rest_count;
-  if (stats && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&stats[3], n);
-  for (size_t k = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; k < n;
-       k += static_cast<size_t>(gridDim.x) * blockDim.x) {
-    const size_t p = rest[k];
-    const float4 s = src[p];
-    float qx, qy, qz;
-    xform(T, s.x, s.y, s.z, qx, qy, qz);
-    NnVisitor vis;
-    vis.init(qx, qy, qz, thr);
-    const uint32_t pp = nn_pos[p - p0];
-    if (pp != 0xffffffffu) vis.range(tg, pp, pp + 1);
-    ring_search(tg, qx, qy, qz, vis);
-    const bool ok = vis.best != ~0ull &&
-                    static_cast<double>(__uint_as_float(static_cast<uint32_t>(vis.best >> 32))) < thr;
-    nn_pos[p - p0] = ok ? vis.pos : 0xffffffffu;
-    flags[p - p0] = ok ? 1u : 0u;
-  }
 }
 
 // Accepted correspondence p -> compacted slot pos[p]: the matched target point and the
@@ -1299,29 +914,6 @@ hipError_t launch_correspond(const GridView& tgt, const float4* src, size_t p0, 
   return hipGetLastError();
 }
 
-hipError_t launch_correspond_tile(const GridView& tgt, const float4* src, const uint32_t* qorder,
-                                  size_t ns, size_t p0, Xf34 T, double thr, int seeded,
-                                  uint32_t* nn_pos, uint32_t* flags, uint32_t* rest,
-                                  unsigned int* rest_count, unsigned int* stats, hipStream_t s) {
-  if (!ns) return hipSuccess;
-  hipError_t e = hipMemsetAsync(rest_count, 0, sizeof(unsigned int), s);
-  if (e != hipSuccess) return e;
-  correspond_tile_kernel<<<nblk(ns), 256, 0, s>>>(tgt, src, qorder, ns, p0, T, thr, seeded,
-                                                  nn_pos, flags, rest, rest_count, stats);
-  // the rest list is at most ns long: one thread per possible entry, the device-side count
-  // decides which ones work
-  correspond_rest_kernel<<<nblk(ns), 256, 0, s>>>(
-      tgt, src, rest, rest_count, p0, T, thr, nn_pos, flags, stats);
-  return hipGetLastError();
-}
-
-hipError_t launch_morton_keys(const GridView& g, size_t p0, size_t n, int shift, uint32_t* keys,
-                              uint32_t* vals, hipStream_t s) {
-  if (!n) return hipSuccess;
-  morton_keys_kernel<<<nblk(n), 256, 0, s>>>(g, p0, n, shift, keys, vals);
-  return hipGetLastError();
-}
-
 hipError_t launch_compact(const float4* src, const float4* tpts, const Cov3& cov_s,
                           const Cov3& cov_t, Rot33d R, const uint32_t* nn_pos,
                           const uint32_t* flags, const uint32_t* pos, size_t p0, size_t p1,
@@ -1416,9 +1008,6 @@ hipError_t preload_kernels(void* pinned, size_t pinned_bytes, hipStream_t s) {
       reinterpret_cast<const void*>(&knn_cov_kernel<25>),
       reinterpret_cast<const void*>(&knn_cov_kernel<30>),
       reinterpret_cast<const void*>(&correspond_kernel),
-      reinterpret_cast<const void*>(&correspond_tile_kernel),
-      reinterpret_cast<const void*>(&correspond_rest_kernel),
-      reinterpret_cast<const void*>(&morton_keys_kernel),
       reinterpret_cast<const void*>(&compact_kernel),
       reinterpret_cast<const void*>(&fdf_soa_kernel),
       reinterpret_cast<const void*>(&fitness_kernel),

@@ -266,13 +266,6 @@ class GICPEngine:
     def set_profiling(self, on: bool):
         self._check(self._lib.mgicp_set_profiling(self._h, int(on)), "set_profiling")
 
-    def search_stats(self):
-        """Tiled 1-NN counters accumulated while profiling is on."""
-        out = (ctypes.c_ulonglong * 4)()
-        self._check(self._lib.mgicp_debug_search_stats(self._h, out), "search_stats")
-        return {"waves": int(out[0]), "over_budget_waves": int(out[1]), "staged_points": int(out[2]),
-                "global_search_queries": int(out[3])}
-
     def kernel_times(self):
         ms = np.zeros(5, np.float64)
         cnt = np.zeros(5, np.int32)
