@@ -61,6 +61,8 @@ def parse():
                     help="points per cloud of the bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=1)
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01_pmc_fdf.json"))
+    ap.add_argument("--gn-steps", type=int, default=5,
+                    help="timed aligns of the opt-in Gauss-Newton mode (MGICP_SOLVER_GN; 0 = skip)")
     ap.add_argument("--no-events", action="store_true",
                     help="time the steps without per-launch HIP events (A/B of the event overhead)")
     args = ap.parse_args()
@@ -150,6 +152,47 @@ def main():
     T_final = eng.getFinalTransformation()
     result = dict(eng.last_result)
 
+    # opt-in Gauss-Newton mode on the same cached grids / covariances (every rank takes part:
+    # one 80-double all-reduce per outer iteration)
+    gn = None
+    if args.gn_steps > 0:
+        from leica_point_cloud_processing_amd import _lib
+
+        eng.setSolver(_lib.MGICP_SOLVER_GN)
+        eng.align()  # warmup
+        eng.set_profiling(not args.no_events)
+        pg.barrier()
+        t0 = time.perf_counter()
+        gn_iters = 0
+        for _ in range(args.gn_steps):
+            eng.align()
+            gn_iters += eng.last_result["iterations"]
+        pg.barrier()
+        gdt = pg.allreduce_max(time.perf_counter() - t0)
+        gkt = eng.kernel_times()
+        eng.set_profiling(False)
+        T_gn = eng.getFinalTransformation()
+        mom_ms = gkt["gn_moments"]["avg_ms"]
+        n_sh = args.n_source // world
+        gn = {
+            "solver": "MGICP_SOLVER_GN (moment pass + host Gauss-Newton; not PCL's trajectory)",
+            "value": round(gn_iters / gdt, 3),
+            "unit": "iterations/s",
+            "ms_per_align": round(1e3 * gdt / args.gn_steps, 3),
+            "iterations_per_align": eng.last_result["iterations"],
+            "device_passes_per_align": eng.last_result["n_evals"],
+            "frob_vs_pcl_bfgs_mode": float(np.linalg.norm(T_gn.astype(np.float64) - T_final.astype(np.float64))),
+            "err_vs_truth_gn": float(np.abs(T_gn.astype(np.float64) @ T_true - np.eye(4)).max()),
+            "err_vs_truth_pcl_bfgs": float(np.abs(T_final.astype(np.float64) @ T_true - np.eye(4)).max()),
+            "kernels": {
+                "correspond": gkt["correspond"],
+                # per source point of the shard: src 16 + flag 4 + nn 4 + Cs 48 + tgt 16 + Ct 48
+                "gn_moments": {**gkt["gn_moments"], "algorithmic_bytes": 136 * n_sh,
+                               "achieved_GBps": (136 * n_sh / (mom_ms * 1e-3) / 1e9) if mom_ms else None},
+            },
+        }
+        eng.setSolver(_lib.MGICP_SOLVER_PCL_BFGS)
+
     # a fresh engine in this (now warm) process: set_target + set_source + align wall time from
     # host buffers to T on the host -- what a long-running caller pays for every new cloud pair --
     # with covariance-kernel events on (the timed region above runs with cached covariances)
@@ -236,6 +279,18 @@ def main():
         e3.set_target_xyz(s_cad)
         T_gpu = e3.align()
         frob_sample = float(np.linalg.norm(T_gpu.astype(np.float64) - T_cpu.astype(np.float64)))
+        if gn is not None:
+            # GN mode against the oracle's GN restatement on the same sample
+            from leica_point_cloud_processing_amd import _lib
+            from oracle import ref
+
+            og = ref.RefGICP(threads=max(1, args.cpu_threads), solver=1)
+            og.set_source(s_scan)
+            og.set_target(s_cad)
+            T_ogn, _ = og.align()
+            e3.setSolver(_lib.MGICP_SOLVER_GN)
+            T_egn = e3.align()
+            gn["frob_vs_oracle_gn_sample"] = float(np.linalg.norm(T_egn.astype(np.float64) - T_ogn.astype(np.float64)))
         e3.close()
 
     line = {
@@ -271,6 +326,7 @@ def main():
         "roofline": roofline,
         "kernels": kernels,
         "cpu_baseline": cpu,
+        "gn_mode": gn,
         "data_gen_s": round(t_gen, 2),
         "grid_occupancy": float(os.environ.get("MGICP_GRID_OCC", "0") or 0) or None,
     }

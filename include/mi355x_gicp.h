@@ -38,6 +38,12 @@ extern "C" {
 #define MGICP_E_NOMEM          -7  /* device allocation failed / grid too large */
 
 #define MGICP_SOLVER_PCL_BFGS   0  /* PCL 1.8.1 BFGS trajectory (parity mode, default) */
+#define MGICP_SOLVER_GN         1  /* opt-in fast mode (SURVEY.md 8b "solver"): one device pass
+                                      per outer iteration collects the 74 moments of the
+                                      quadratic objective, Gauss-Newton on SE(3) runs on the host;
+                                      multi-GPU: one 80-double all-reduce per outer iteration.
+                                      Not in PCL 1.8.1: reported against the fixed-point protocol
+                                      and the oracle's GN restatement, not the BFGS trajectory */
 
 typedef struct {
     int    max_iter;        /* Registration::setMaximumIterations  (GICPAlignment.cpp:50; default 100) */
@@ -137,12 +143,18 @@ int mgicp_debug_fdf(mgicp_ctx* ctx, const double x[6], double* f, double g6[6]);
  * NULL) (a "detached" shard, no RCCL) they cover rank r's source range only, so sharding can
  * be verified on one device; align/fitness refuse to run in that mode. */
 int mgicp_debug_fdf_sums(mgicp_ctx* ctx, const double x[6], double out16[16]);
+/* MGICP_SOLVER_GN's moment pass at T (col-major) over the last correspondence sweep
+ * (mgicp_debug_correspondences or an align): out80[0] sum r'Mr, [1..12] sum (Mr) w' (row-major
+ * 3x4), [13..72] sum M_p (w w')_q (p: m00 m01 m02 m11 m12 m22; q: upper triangle of the 4x4
+ * w w'), [73] count, with r = fl(fl(T s) - q), w = (s - c, 1), c = bbox midpoint of the source */
+int mgicp_debug_moments(mgicp_ctx* ctx, const float T_cm[16], double out80[80]);
 /* per-iteration transformation_ of the last align (col-major, iterations x 16) */
 int mgicp_debug_trace(mgicp_ctx* ctx, float* out, int max_iters);
 /* average device time (ms) of each kernel family while profiling is on, for roofline
  * reporting: [0] covariance kNN, [1] correspondence 1-NN, [2] BFGS objective pass,
- * [3] separate reduction finish, [4] compaction + Mahalanobis; counts in out_counts (optional) */
-#define MGICP_KERNEL_FAMILIES 5
+ * [3] separate reduction finish, [4] compaction + Mahalanobis, [5] Gauss-Newton moment pass (+ its
+ * finish); counts in out_counts (optional) */
+#define MGICP_KERNEL_FAMILIES 6
 int mgicp_debug_kernel_times(mgicp_ctx* ctx, double out_ms[MGICP_KERNEL_FAMILIES],
                              int out_counts[MGICP_KERNEL_FAMILIES]);
 /* enable (1) / disable (0) per-launch HIP event timing (off by default) */

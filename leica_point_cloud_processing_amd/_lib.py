@@ -22,6 +22,10 @@ MGICP_E_HIP = -5
 MGICP_E_COMM = -6
 MGICP_E_NOMEM = -7
 
+MGICP_SOLVER_PCL_BFGS = 0
+MGICP_SOLVER_GN = 1
+MGICP_KERNEL_FAMILIES = 6
+
 
 class MgicpParams(ctypes.Structure):
     _fields_ = [
@@ -86,6 +90,7 @@ _SIGNATURES = {
     "mgicp_debug_correspondences": (ctypes.c_int, [_P, _FP, _IP, _DP]),
     "mgicp_debug_fdf": (ctypes.c_int, [_P, _DP, _DP, _DP]),
     "mgicp_debug_fdf_sums": (ctypes.c_int, [_P, _DP, _DP]),
+    "mgicp_debug_moments": (ctypes.c_int, [_P, _FP, _DP]),
     "mgicp_debug_trace": (ctypes.c_int, [_P, _FP, ctypes.c_int]),
     "mgicp_debug_kernel_times": (ctypes.c_int, [_P, _DP, _IP]),
     "mgicp_set_profiling": (ctypes.c_int, [_P, ctypes.c_int]),

@@ -26,6 +26,7 @@
 #include "../../include/mi355x_gicp.h"
 #include "host_upload.hpp"
 #include "mgicp_internal.hpp"
+#include "gn_solver.hpp"
 #include "pcl_bfgs.hpp"
 
 using namespace mgicp;
@@ -208,12 +209,13 @@ struct Cloud {
   DevBuf<uint8_t> empty_dist; // empty-space map (target only: 1-NN queries leave the surface)
   bool want_empty_map = false;
   DevBuf<double2> cov;        // 3 * n
+  float lo[3] = {0.f, 0.f, 0.f}, hi[3] = {0.f, 0.f, 0.f};  // bounding box (original coordinates)
   GridView view{};
   size_t ncells = 0;
   Cov3 cov3() const { return Cov3{cov.p, cov.p + n, cov.p + 2 * n}; }
 };
 
-enum { kFamCov = 0, kFamCorr = 1, kFamFdf = 2, kFamRed = 3, kFamCompact = 4, kFams = 5 };
+enum { kFamCov = 0, kFamCorr = 1, kFamFdf = 2, kFamRed = 3, kFamCompact = 4, kFamMoments = 5, kFams = 6 };
 
 }  // namespace
 
@@ -251,6 +253,10 @@ struct mgicp_ctx {
   bool seed_valid = false;
   DevBuf<double> partial;
   DevBuf<double> red;      // kRedVals
+  // Gauss-Newton mode: block partials / finished moments of one pass, and their host copy
+  DevBuf<double> mpartial, mred;
+  double mom[kMomVals] = {};
+  double out_ctr[3] = {0, 0, 0};  // moment expansion centre: bbox midpoint of the guess-applied source
   unsigned char* h_small = nullptr;  // pinned, mapped host scratch (kSmallBytes) for small readbacks
   unsigned char* d_small = nullptr;  // its device address (kernels write results there directly)
   double* h_red = nullptr;   // pinned, mapped, coherent host memory
@@ -417,6 +423,10 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
     bad += hp[b * 8 + 6];
   }
   if (bad > 0) return fail(ctx, MGICP_E_NONFINITE, "cloud contains NaN/Inf coordinates");
+  for (int d = 0; d < 3; ++d) {
+    cl.lo[d] = mn[d];
+    cl.hi[d] = mx[d];
+  }
   float ext[3];
   float maxext = 0.f, maxabs = 0.f;
   for (int d = 0; d < 3; ++d) {
@@ -625,13 +635,35 @@ int ensure_iter_buffers(mgicp_ctx* ctx) {
 
 // guess-applied source cloud ("output" after transformPointCloud(output, output, guess))
 int set_output(mgicp_ctx* ctx, const Mat4& G) {
+  float lo[3], hi[3];
   if (G.is_identity()) {
     ctx->d_out = ctx->src.pts.p;  // x*1 + y*0 + z*0 + 0 == x: identity leaves points intact
+    for (int d = 0; d < 3; ++d) {
+      lo[d] = ctx->src.lo[d];
+      hi[d] = ctx->src.hi[d];
+    }
   } else {
     HIPCK(ctx->src_out.reserve(ctx->src.n));
     HIPCK(launch_xform_points(ctx->src.pts.p, ctx->src.n, G.xf(), ctx->src_out.p, ctx->stream));
     ctx->d_out = ctx->src_out.p;
+    // bbox of the transformed cloud (the Gauss-Newton expansion centre)
+    const size_t n = ctx->src.n;
+    const int nb = static_cast<int>(std::min<size_t>((n + 255) / 256, 1024));
+    HIPCK(launch_bbox(ctx->src_out.p, n, reinterpret_cast<float*>(ctx->d_small), nb, ctx->stream));
+    int rc = sync(ctx);
+    if (rc) return rc;
+    const float* hp = reinterpret_cast<const float*>(ctx->h_small);
+    for (int d = 0; d < 3; ++d) {
+      lo[d] = INFINITY;
+      hi[d] = -INFINITY;
+    }
+    for (int b = 0; b < nb; ++b)
+      for (int d = 0; d < 3; ++d) {
+        lo[d] = std::min(lo[d], hp[b * 8 + d]);
+        hi[d] = std::max(hi[d], hp[b * 8 + 3 + d]);
+      }
   }
+  for (int d = 0; d < 3; ++d) ctx->out_ctr[d] = static_cast<double>(0.5f * (lo[d] + hi[d]));
   ctx->last_guess = G;
   return MGICP_OK;
 }
@@ -832,12 +864,78 @@ int estimate_bfgs(mgicp_ctx* ctx, Mat4& T, int* n_corr) {
   return MGICP_E_SOLVER;  // SolverDidntConvergeException
 }
 
+// Gauss-Newton mode, one device pass per outer iteration: the 74 moments of the objective over
+// the accepted correspondences of the last sweep at T (Mahalanobis computed on the fly), finished
+// in a fixed block order, all-reduced across ranks (one 80-double RCCL call), copied to the host.
+int moments_pass(mgicp_ctx* ctx, const Mat4& T, const Mat4& G) {
+  const size_t p0 = ctx->shard_p0(), p1 = ctx->shard_p1();
+  hipStream_t s = ctx->stream;
+  const int nb = gn_grid_blocks(p1 - p0);
+  HIPCK(ctx->mpartial.reserve(static_cast<size_t>(nb) * kMomVals));
+  HIPCK(ctx->mred.reserve(kMomVals));
+  {
+    ProfScope ps(ctx, kFamMoments);
+    HIPCK(launch_gn_moments(ctx->d_out, ctx->tgt.view.pts, ctx->src.cov3(), ctx->tgt.cov3(),
+                            rot_of(T, G), T.xf(), ctx->out_ctr, ctx->prev_pos.p, ctx->flags.p, p0,
+                            p1, ctx->mpartial.p, nb, s));
+    HIPCK(launch_reduce_finish_moments(ctx->mpartial.p, nb, ctx->mred.p, s));
+  }
+  if (ctx->comm)
+    NCCLCK(ncclAllReduce(ctx->mred.p, ctx->mred.p, kMomVals, ncclDouble, ncclSum, ctx->comm, s));
+  HIPCK(hipMemcpyAsync(ctx->h_small, ctx->mred.p, kMomVals * sizeof(double), hipMemcpyDeviceToHost, s));
+  int rc = sync(ctx);
+  if (rc) return rc;
+  std::memcpy(ctx->mom, ctx->h_small, kMomVals * sizeof(double));
+  ctx->n_evals++;
+  return MGICP_OK;
+}
+
+// the correspondence sweep of the Gauss-Newton mode: exact 1-NN (same kernel as the BFGS mode),
+// then the moment pass; no scan / compaction (the moment pass reads the flags directly)
+int correspond_gn(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
+  const double thr = ctx->prm.max_corr_dist * ctx->prm.max_corr_dist;
+  const size_t p0 = ctx->shard_p0(), p1 = ctx->shard_p1();
+  const bool seeded = seed && ctx->seed_valid;
+  {
+    ProfScope ps(ctx, kFamCorr);
+    HIPCK(launch_correspond(ctx->tgt.view, ctx->d_out, p0, p1, T.xf(), thr, seeded ? 1 : 0,
+                            ctx->prev_pos.p, ctx->flags.p, ctx->stream));
+  }
+  ctx->seed_valid = true;
+  ctx->have_corr = false;  // the SoA streams of the BFGS mode are not refreshed
+  return moments_pass(ctx, T, G);
+}
+
+// Gauss-Newton estimate on the moments of the last sweep (taken at T); T <- solution.
+// 0 = accepted, MGICP_E_SOLVER = fewer than 4 correspondences or a singular normal matrix.
+int estimate_gn(mgicp_ctx* ctx, Mat4& T, int* n_corr) {
+  *n_corr = static_cast<int>(ctx->mom[73]);
+  if (ctx->mom[73] < 4) return MGICP_E_SOLVER;
+  gn::Problem pb;
+  pb.mom = ctx->mom;
+  gn::Pose P;
+  for (int a = 0; a < 3; ++a) {
+    pb.c[a] = ctx->out_ctr[a];
+    for (int k = 0; k < 4; ++k) pb.T0[a][k] = static_cast<double>(T.m[a][k]);
+    for (int k = 0; k < 3; ++k) P.R[a][k] = pb.T0[a][k];
+    P.t[a] = pb.T0[a][3];
+  }
+  int host_evals = 0;
+  if (!gn::solve(pb, P, ctx->prm.max_inner_iter, &host_evals)) return MGICP_E_SOLVER;
+  for (int a = 0; a < 3; ++a) {
+    for (int k = 0; k < 3; ++k) T.m[a][k] = static_cast<float>(P.R[a][k]);
+    T.m[a][3] = static_cast<float>(P.t[a]);
+  }
+  return MGICP_OK;
+}
+
 int check_params(mgicp_ctx* ctx, const mgicp_params& p) {
   const int k = p.k;
   if (!(k == 5 || k == 10 || k == 15 || k == 20 || k == 25 || k == 30))
     return fail(ctx, MGICP_E_INVALID, "k must be one of 5, 10, 15, 20, 25, 30");
   if (p.max_iter < 1 || p.max_inner_iter < 1 || !(p.max_corr_dist >= 0) || !(p.rot_eps > 0) ||
-      !(p.tf_eps >= 0) || p.solver != MGICP_SOLVER_PCL_BFGS)
+      !(p.tf_eps >= 0) ||
+      (p.solver != MGICP_SOLVER_PCL_BFGS && p.solver != MGICP_SOLVER_GN))
     return fail(ctx, MGICP_E_INVALID, "invalid GICP parameters");
   return MGICP_OK;
 }
@@ -959,7 +1057,7 @@ void mgicp_destroy(mgicp_ctx* ctx) {
     c->cell_start.release(); c->cov.release(); c->empty_dist.release();
   }
   ctx->src_out.release();
-  ctx->partial.release(); ctx->red.release(); ctx->counts.release(); ctx->keys.release();
+  ctx->partial.release(); ctx->red.release(); ctx->mpartial.release(); ctx->mred.release(); ctx->counts.release(); ctx->keys.release();
   ctx->keys_sorted.release(); ctx->vals.release(); ctx->scratch.release(); ctx->u64.release();
   ctx->fpartial.release();
   ctx->ticket.release();
@@ -1022,10 +1120,13 @@ int mgicp_align(mgicp_ctx* ctx, const float guess_cm[16], float out_T_cm[16], mg
   bool converged = false;
   int solver_rc = MGICP_OK;
   while (!converged) {
-    if ((rc = correspond(ctx, T, G, nr_iterations > 0))) return rc;
+    const bool gn_mode = ctx->prm.solver == MGICP_SOLVER_GN;
+    rc = gn_mode ? correspond_gn(ctx, T, G, nr_iterations > 0)
+                 : correspond(ctx, T, G, nr_iterations > 0);
+    if (rc) return rc;
     prev = T;
     int ncorr = 0;
-    rc = estimate_bfgs(ctx, T, &ncorr);
+    rc = gn_mode ? estimate_gn(ctx, T, &ncorr) : estimate_bfgs(ctx, T, &ncorr);
     r.n_corr = ncorr;
     if (rc == MGICP_E_SOLVER) {  // PCLException caught: converged_ stays false
       T = prev;
@@ -1296,6 +1397,15 @@ int mgicp_debug_fdf_sums(mgicp_ctx* ctx, const double x[6], double out16[16]) {
   Vec6 xv;
   for (int i = 0; i < 6; ++i) xv[i] = x[i];
   return fn.pass(xv, out16);
+}
+
+int mgicp_debug_moments(mgicp_ctx* ctx, const float T_cm[16], double out80[80]) {
+  if (!ctx || !T_cm || !out80 || !ctx->seed_valid) return MGICP_E_INVALID;
+  HIPCK(hipSetDevice(ctx->device));
+  int rc = moments_pass(ctx, Mat4::from_cm(T_cm), ctx->last_guess);
+  if (rc) return rc;
+  std::memcpy(out80, ctx->mom, kMomVals * sizeof(double));
+  return MGICP_OK;
 }
 
 int mgicp_debug_trace(mgicp_ctx* ctx, float* out, int max_iters) {

@@ -49,6 +49,9 @@ struct CorrSoA {
 //   [0] f-sum  [1..3] g_t sum  [4..12] Rsum (row-major)  [13] count  [14..15] pad
 constexpr int kRedVals = 16;
 constexpr int kRedThreads = 256;
+// Number of values reduced per Gauss-Newton moment pass (MGICP_SOLVER_GN):
+//   [0] sum r0'M r0  [1..12] sum (M r0) w'  [13..72] sum M_p (w w')_q  [73] count  [74..79] pad
+constexpr int kMomVals = 80;
 
 // Xform as 3x4 row-major float (the top three rows of an Eigen::Matrix4f).
 struct Xf34 { float m[12]; };
@@ -88,6 +91,14 @@ hipError_t launch_fdf_soa(const CorrSoA& c, size_t m, Xf34 A, double* partial, i
                           unsigned int* ticket, double* out, int reverse,
                           unsigned long long* done_flag, unsigned long long seq, hipStream_t s);
 int        fdf_grid_blocks(size_t n, int max_blocks = 2048);
+// Gauss-Newton moments of the accepted correspondences of [p0, p1) at T0 (R = rot(T0 * guess),
+// ctr = expansion centre): nb block partials of kMomVals doubles, then a one-block finish
+int        gn_grid_blocks(size_t n);
+hipError_t launch_gn_moments(const float4* src, const float4* tpts, const Cov3& cov_s,
+                             const Cov3& cov_t, Rot33d R, Xf34 T0, const double ctr[3],
+                             const uint32_t* nn_pos, const uint32_t* flags, size_t p0, size_t p1,
+                             double* partial, int nb, hipStream_t s);
+hipError_t launch_reduce_finish_moments(const double* partial, int nb, double* out, hipStream_t s);
 hipError_t launch_fitness(const GridView& tgt, const float4* src, size_t p0, size_t p1,
                           Xf34 T, double max_range, double* partial, int nb, hipStream_t s);
 hipError_t launch_reduce_finish(const double* partial, int nb, double* out, hipStream_t s);

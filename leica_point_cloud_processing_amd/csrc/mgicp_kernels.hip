@@ -526,24 +526,11 @@ __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_kernel(GridV
   flags[p - p0] = ok ? 1u : 0u;
 }
 
-// Accepted correspondence p -> compacted slot pos[p]: the matched target point and the
-// Mahalanobis matrix M = (R Cs R' + Ct)^-1 in fp64 with Eigen's 3x3 cofactor inverse
-// (gicp.hpp computeTransformation), written straight into the SoA streams.
-__global__ __launch_bounds__(256) void compact_kernel(const float4* __restrict__ src,
-                                                      const float4* __restrict__ tpts, Cov3 cov_s,
-                                                      Cov3 cov_t, Rot33d R,
-                                                      const uint32_t* __restrict__ nn_pos,
-                                                      const uint32_t* __restrict__ flags,
-                                                      const uint32_t* __restrict__ pos, size_t p0,
-                                                      size_t p1, CorrSoA o) {
-  const size_t p = p0 + static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (p >= p1 || !flags[p - p0]) return;
-  const uint32_t j = nn_pos[p - p0];
-  const size_t i = pos[p - p0];
-  const float4 s = src[p], t = tpts[j];
-  double C1[3][3], C2[3][3], RC[3][3], tm[3][3];
-  load_cov(cov_s, p, C1);
-  load_cov(cov_t, j, C2);
+// M = (R Cs R' + Ct)^-1 in fp64 with Eigen's 3x3 cofactor inverse (gicp.hpp
+// computeTransformation): the upper triangle {m00, m01, m02, m11, m12, m22}.
+__device__ __forceinline__ void mahalanobis(const Rot33d& R, const double (&C1)[3][3],
+                                            const double (&C2)[3][3], double (&m6)[6]) {
+  double RC[3][3], tm[3][3];
 #pragma unroll
   for (int r = 0; r < 3; ++r)
 #pragma unroll
@@ -570,13 +557,35 @@ __global__ __launch_bounds__(256) void compact_kernel(const float4* __restrict__
   det = det + c20 * tm[2][0];
   const double inv = 1.0 / det;
   // Eigen: result(i, j) = cofactor(j, i) / det; keep the upper triangle
-  o.m00[i] = c00 * inv;
-  o.m01[i] = c10 * inv;
-  o.m02[i] = c20 * inv;
-  o.m11[i] = COF(1, 1) * inv;
-  o.m12[i] = COF(2, 1) * inv;
-  o.m22[i] = COF(2, 2) * inv;
+  m6[0] = c00 * inv;
+  m6[1] = c10 * inv;
+  m6[2] = c20 * inv;
+  m6[3] = COF(1, 1) * inv;
+  m6[4] = COF(2, 1) * inv;
+  m6[5] = COF(2, 2) * inv;
 #undef COF
+}
+
+// Accepted correspondence p -> compacted slot pos[p]: the matched target point and its
+// Mahalanobis matrix, written straight into the SoA streams.
+__global__ __launch_bounds__(256) void compact_kernel(const float4* __restrict__ src,
+                                                      const float4* __restrict__ tpts, Cov3 cov_s,
+                                                      Cov3 cov_t, Rot33d R,
+                                                      const uint32_t* __restrict__ nn_pos,
+                                                      const uint32_t* __restrict__ flags,
+                                                      const uint32_t* __restrict__ pos, size_t p0,
+                                                      size_t p1, CorrSoA o) {
+  const size_t p = p0 + static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (p >= p1 || !flags[p - p0]) return;
+  const uint32_t j = nn_pos[p - p0];
+  const size_t i = pos[p - p0];
+  const float4 s = src[p], t = tpts[j];
+  double C1[3][3], C2[3][3], m6[6];
+  load_cov(cov_s, p, C1);
+  load_cov(cov_t, j, C2);
+  mahalanobis(R, C1, C2, m6);
+  o.m00[i] = m6[0]; o.m01[i] = m6[1]; o.m02[i] = m6[2];
+  o.m11[i] = m6[3]; o.m12[i] = m6[4]; o.m22[i] = m6[5];
   o.sx[i] = s.x; o.sy[i] = s.y; o.sz[i] = s.z;
   o.qx[i] = t.x; o.qy[i] = t.y; o.qz[i] = t.z;
 }
@@ -748,6 +757,94 @@ __global__ __launch_bounds__(256) void fdf_soa_kernel(CorrSoA c, size_t m, Xf34 
   } else {
     block_reduce_store(acc, partial + static_cast<size_t>(blockIdx.x) * kRedVals);
   }
+}
+
+// ------------------------------------------------------------------------------------
+// Gauss-Newton moment pass (MGICP_SOLVER_GN)
+// ------------------------------------------------------------------------------------
+// NV doubles reduced across a 256-thread block; threads < NV write dst[0..NV-1]
+template <int NV>
+__device__ __forceinline__ void block_reduce_store_n(double (&acc)[NV], double* dst) {
+  __shared__ double sm[4][NV];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const double w = wave_sum(acc[v]);
+    if (lane == 0) sm[wid][v] = w;
+  }
+  __syncthreads();
+  if (threadIdx.x < NV) {
+    const int v = threadIdx.x;
+    double s = sm[0][v];
+    s = s + sm[1][v];
+    s = s + sm[2][v];
+    s = s + sm[3][v];
+    dst[v] = s;
+  }
+}
+
+// For a fixed correspondence set the GICP objective is an exact quadratic in A = [R | t]
+// (DESIGN.md "The moment form"), so ONE pass per outer iteration collects everything the host
+// Gauss-Newton solve needs: with the correspondence transform T0, r0 = fl(fl(T0 s) - q) and
+// w = (s - c, 1),
+//   [0] sum r0' M r0   [1 + 4a + k] sum (M r0)_a w_k   [13 + 10p + q] sum M_p (w w')_q   [73] count
+// (p over the 6 upper-triangle entries of M, q over the 10 of w w').  The Mahalanobis matrix is
+// computed on the fly (no compaction, no SoA streams): 136 B read per source point of the shard.
+__global__ __launch_bounds__(256) void gn_moments_kernel(
+    const float4* __restrict__ src, const float4* __restrict__ tpts, Cov3 cov_s, Cov3 cov_t,
+    Rot33d R, Xf34 T0, double cx, double cy, double cz, const uint32_t* __restrict__ nn_pos,
+    const uint32_t* __restrict__ flags, size_t p0, size_t p1, double* __restrict__ partial) {
+  double acc[kMomVals];
+#pragma unroll
+  for (int v = 0; v < kMomVals; ++v) acc[v] = 0.0;
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  for (size_t p = p0 + static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; p < p1;
+       p += stride) {
+    if (!flags[p - p0]) continue;
+    const uint32_t j = nn_pos[p - p0];
+    const float4 s = src[p], t = tpts[j];
+    double C1[3][3], C2[3][3], m6[6];
+    load_cov(cov_s, p, C1);
+    load_cov(cov_t, j, C2);
+    mahalanobis(R, C1, C2, m6);
+    float px, py, pz;
+    xform(T0, s.x, s.y, s.z, px, py, pz);
+    const double r0 = static_cast<double>(px - t.x);
+    const double r1 = static_cast<double>(py - t.y);
+    const double r2 = static_cast<double>(pz - t.z);
+    double mr[3];
+    mr[0] = m6[0] * r0; mr[0] = mr[0] + m6[1] * r1; mr[0] = mr[0] + m6[2] * r2;
+    mr[1] = m6[1] * r0; mr[1] = mr[1] + m6[3] * r1; mr[1] = mr[1] + m6[4] * r2;
+    mr[2] = m6[2] * r0; mr[2] = mr[2] + m6[4] * r1; mr[2] = mr[2] + m6[5] * r2;
+    double d = r0 * mr[0]; d = d + r1 * mr[1]; d = d + r2 * mr[2];
+    acc[0] += d;
+    const double w[4] = {static_cast<double>(s.x) - cx, static_cast<double>(s.y) - cy,
+                         static_cast<double>(s.z) - cz, 1.0};
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[1 + 4 * a + k] += mr[a] * w[k];
+    const double ww[10] = {w[0] * w[0], w[0] * w[1], w[0] * w[2], w[0],        w[1] * w[1],
+                           w[1] * w[2], w[1],        w[2] * w[2], w[2],        1.0};
+#pragma unroll
+    for (int pp = 0; pp < 6; ++pp)
+#pragma unroll
+      for (int q = 0; q < 10; ++q) acc[13 + 10 * pp + q] += m6[pp] * ww[q];
+    acc[73] += 1.0;
+  }
+  block_reduce_store_n<kMomVals>(acc, partial + static_cast<size_t>(blockIdx.x) * kMomVals);
+}
+
+__global__ __launch_bounds__(256) void reduce_finish_moments_kernel(const double* __restrict__ partial,
+                                                                    int nb, double* __restrict__ out) {
+  double acc[kMomVals];
+#pragma unroll
+  for (int v = 0; v < kMomVals; ++v) acc[v] = 0.0;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+#pragma unroll
+    for (int v = 0; v < kMomVals; ++v) acc[v] += partial[static_cast<size_t>(b) * kMomVals + v];
+  }
+  block_reduce_store_n<kMomVals>(acc, out);
 }
 
 __global__ __launch_bounds__(256) void fitness_kernel(GridView tg, const float4* __restrict__ src,
@@ -931,6 +1028,26 @@ hipError_t launch_fdf_soa(const CorrSoA& c, size_t m, Xf34 A, double* partial, i
   return hipGetLastError();
 }
 
+int gn_grid_blocks(size_t n) {
+  // ~16 source points per thread, at most 1024 blocks (the finish reads nb x 80 doubles)
+  const size_t want = (n + 256 * 16 - 1) / (256 * 16);
+  return static_cast<int>(std::max<size_t>(1, std::min<size_t>(want, 1024)));
+}
+
+hipError_t launch_gn_moments(const float4* src, const float4* tpts, const Cov3& cov_s,
+                             const Cov3& cov_t, Rot33d R, Xf34 T0, const double ctr[3],
+                             const uint32_t* nn_pos, const uint32_t* flags, size_t p0, size_t p1,
+                             double* partial, int nb, hipStream_t s) {
+  gn_moments_kernel<<<nb, 256, 0, s>>>(src, tpts, cov_s, cov_t, R, T0, ctr[0], ctr[1], ctr[2],
+                                       nn_pos, flags, p0, p1, partial);
+  return hipGetLastError();
+}
+
+hipError_t launch_reduce_finish_moments(const double* partial, int nb, double* out, hipStream_t s) {
+  reduce_finish_moments_kernel<<<1, 256, 0, s>>>(partial, nb, out);
+  return hipGetLastError();
+}
+
 int fdf_grid_blocks(size_t n, int max_blocks) {
   // ~8 points per thread keeps >= 8 waves per CU resident on 256 CUs at 5M points
   const size_t want = (n + 256 * 8 - 1) / (256 * 8);
@@ -1014,6 +1131,8 @@ hipError_t preload_kernels(void* pinned, size_t pinned_bytes, hipStream_t s) {
       reinterpret_cast<const void*>(&resolution_kernel),
       reinterpret_cast<const void*>(&radius_keep_kernel),
       reinterpret_cast<const void*>(&reduce_finish_kernel),
+      reinterpret_cast<const void*>(&gn_moments_kernel),
+      reinterpret_cast<const void*>(&reduce_finish_moments_kernel),
   };
   for (const void* f : fns) {
     hipFuncAttributes attr;

@@ -111,6 +111,12 @@ class GICPEngine:
         self.params.rot_eps = float(eps)
         self._push_params()
 
+    def setSolver(self, solver: int):
+        """MGICP_SOLVER_PCL_BFGS (default, PCL 1.8.1 trajectory) or MGICP_SOLVER_GN (fast mode).
+        Grids and covariances stay cached (PCL's dirty-flag semantics)."""
+        self.params.solver = int(solver)
+        self._push_params()
+
     def setRANSACOutlierRejectionThreshold(self, th: float):
         self.ransac_outlier_threshold = float(th)  # stored; GICP never uses it (PCL 1.8.1)
 
@@ -266,10 +272,17 @@ class GICPEngine:
     def set_profiling(self, on: bool):
         self._check(self._lib.mgicp_set_profiling(self._h, int(on)), "set_profiling")
 
+    def debug_moments(self, T) -> np.ndarray:
+        """MGICP_SOLVER_GN's 74 moments (+ pad) at T over the last correspondence sweep."""
+        out = np.zeros(80, np.float64)
+        self._check(self._lib.mgicp_debug_moments(self._h, _fp(_cm(T)), _dp(out)), "debug_moments")
+        return out
+
     def kernel_times(self):
-        ms = np.zeros(5, np.float64)
-        cnt = np.zeros(5, np.int32)
+        nf = _lib.MGICP_KERNEL_FAMILIES
+        ms = np.zeros(nf, np.float64)
+        cnt = np.zeros(nf, np.int32)
         self._check(self._lib.mgicp_debug_kernel_times(self._h, _dp(ms), cnt.ctypes.data_as(ctypes.POINTER(ctypes.c_int))),
                     "kernel_times")
-        names = ["knn_cov", "correspond", "fdf", "reduce_finish", "compact"]
-        return {names[i]: {"avg_ms": float(ms[i]), "count": int(cnt[i])} for i in range(5)}
+        names = ["knn_cov", "correspond", "fdf", "reduce_finish", "compact", "gn_moments"]
+        return {names[i]: {"avg_ms": float(ms[i]), "count": int(cnt[i])} for i in range(nf)}

@@ -371,6 +371,7 @@ void ref_default_params(ref_params* p) {
     p->fixed_iterations = 0;
     p->threads = 1;
     p->objective = 0;
+    p->solver = 0;
 }
 
 ref_gicp* ref_create(const ref_params* p) {
@@ -677,6 +678,201 @@ static void moments_eval(ref_gicp* g, const double x[6], double* f, double grad[
             for (int b = 0; b < 3; ++b) R[a][b] = (G[b][a] + g->ctr[a] * G[b][3]) * s;
         r_derivative(x, R, grad);
     }
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Gauss-Newton solver on the moment form (ref_params.solver = 1): checker for the engine's  */
+/* MGICP_SOLVER_GN.  Not a PCL 1.8.1 algorithm: PCL only has the BFGS solver; GN is the      */
+/* north-star's "6x6 J'WJ / J'Wr" solve, held to PCL by SURVEY 8c's fixed-point protocol.    */
+/* Pose update about the centre c: p^ = T s - c, r = p^ + c - q, T <- [Exp(w) | v] * T,      */
+/* J_i = [-[p^_i]x | I].  J'MJ and J'Mr at any pose are linear in the 74 moments.            */
+/* ------------------------------------------------------------------------------------ */
+static void gn_pose_from_float(const float T[4][4], double R[3][3], double t[3]) {
+    for (int a = 0; a < 3; ++a) {
+        for (int k = 0; k < 3; ++k) R[a][k] = (double)T[a][k];
+        t[a] = (double)T[a][3];
+    }
+}
+
+/* f*m, and (when H != NULL) H = sum J'MJ, gv = sum J'Mr (half gradient) at pose (R, t) */
+static double gn_eval(const ref_gicp* g, const double R[3][3], const double t[3], double H[6][6],
+                      double gv[6]) {
+    const double* mo = g->mom;
+    const double* c = g->ctr;
+    double Y[3][4], E[3][4];
+    for (int a = 0; a < 3; ++a) {
+        double u = t[a] - (double)g->T0[a][3];
+        double e = t[a] - c[a];
+        for (int k = 0; k < 3; ++k) {
+            Y[a][k] = R[a][k] - (double)g->T0[a][k];
+            u += Y[a][k] * c[k];
+            E[a][k] = R[a][k];
+            e += R[a][k] * c[k];
+        }
+        Y[a][3] = u;
+        E[a][3] = e;
+    }
+    double G[3][4]; /* sum (M r)_b w_i */
+    for (int b = 0; b < 3; ++b)
+        for (int i = 0; i < 4; ++i) {
+            double acc = mo[1 + 4 * b + i];
+            for (int cc = 0; cc < 3; ++cc)
+                for (int j = 0; j < 4; ++j) acc += Y[cc][j] * mo[13 + 10 * sym_a(b, cc) + sym_w(i, j)];
+            G[b][i] = acc;
+        }
+    double fm = mo[0];
+    for (int a = 0; a < 3; ++a)
+        for (int i = 0; i < 4; ++i) fm += Y[a][i] * (mo[1 + 4 * a + i] + G[a][i]);
+    if (!H) return fm;
+    /* Z[e][a] = sum p^_e (M r)_a ; N[e][a][b] = sum p^_e M_ab ; K[e][f][a][b] = sum p^_e p^_f M_ab */
+    double Z[3][3], N[3][3][3], K[3][3][3][3];
+    for (int e = 0; e < 3; ++e)
+        for (int a = 0; a < 3; ++a) {
+            double z = 0.0;
+            for (int i = 0; i < 4; ++i) z += E[e][i] * G[a][i];
+            Z[e][a] = z;
+        }
+    for (int e = 0; e < 3; ++e)
+        for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 3; ++b) {
+                double s = 0.0;
+                for (int i = 0; i < 4; ++i) s += E[e][i] * mo[13 + 10 * sym_a(a, b) + sym_w(i, 3)];
+                N[e][a][b] = s;
+            }
+    for (int e = 0; e < 3; ++e)
+        for (int f = 0; f < 3; ++f)
+            for (int a = 0; a < 3; ++a)
+                for (int b = 0; b < 3; ++b) {
+                    double s = 0.0;
+                    for (int i = 0; i < 4; ++i)
+                        for (int j = 0; j < 4; ++j)
+                            s += E[e][i] * E[f][j] * mo[13 + 10 * sym_a(a, b) + sym_w(i, j)];
+                    K[e][f][a][b] = s;
+                }
+    static const int eps[3][3][3] = {{{0, 0, 0}, {0, 0, 1}, {0, -1, 0}},
+                                     {{0, 0, -1}, {0, 0, 0}, {1, 0, 0}},
+                                     {{0, 1, 0}, {-1, 0, 0}, {0, 0, 0}}};
+    /* rotation rows: J_w = -[p^]x, so J_w' M r = p^ x (M r), J_w' M J_v = [p^]x M,
+     * J_w' M J_w = -[p^]x M [p^]x */
+    for (int i = 0; i < 3; ++i) {
+        double s = 0.0;
+        for (int j = 0; j < 3; ++j)
+            for (int k = 0; k < 3; ++k) s += eps[i][j][k] * Z[j][k];
+        gv[i] = s;
+        gv[3 + i] = G[i][3];
+    }
+    for (int i = 0; i < 3; ++i)
+        for (int l = 0; l < 3; ++l) {
+            double wv = 0.0, ww = 0.0;
+            for (int j = 0; j < 3; ++j)
+                for (int k = 0; k < 3; ++k) {
+                    if (!eps[i][j][k]) continue;
+                    wv += eps[i][j][k] * N[j][k][l];
+                    for (int mm = 0; mm < 3; ++mm)
+                        for (int n = 0; n < 3; ++n)
+                            if (eps[mm][n][l]) ww -= eps[i][j][k] * eps[mm][n][l] * K[j][n][k][mm];
+                }
+            H[i][3 + l] = wv;
+            H[3 + l][i] = wv;
+            H[i][l] = ww;
+            H[3 + i][3 + l] = mo[13 + 10 * sym_a(i, l) + 9];
+        }
+    return fm;
+}
+
+/* Cholesky solve of H x = -b; 0 on success */
+static int gn_chol_solve(double H[6][6], const double b[6], double x[6]) {
+    double L[6][6];
+    memset(L, 0, sizeof(L));
+    for (int j = 0; j < 6; ++j) {
+        double d = H[j][j];
+        for (int k = 0; k < j; ++k) d -= L[j][k] * L[j][k];
+        if (!(d > 0.0)) return -1;
+        L[j][j] = sqrt(d);
+        for (int i = j + 1; i < 6; ++i) {
+            double s = H[i][j];
+            for (int k = 0; k < j; ++k) s -= L[i][k] * L[j][k];
+            L[i][j] = s / L[j][j];
+        }
+    }
+    double y[6];
+    for (int i = 0; i < 6; ++i) {
+        double s = -b[i];
+        for (int k = 0; k < i; ++k) s -= L[i][k] * y[k];
+        y[i] = s / L[i][i];
+    }
+    for (int i = 5; i >= 0; --i) {
+        double s = y[i];
+        for (int k = i + 1; k < 6; ++k) s -= L[k][i] * x[k];
+        x[i] = s / L[i][i];
+    }
+    return 0;
+}
+
+/* Exp of a rotation vector (Rodrigues) */
+static void gn_exp(const double w[3], double Rx[3][3]) {
+    double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+    double th = sqrt(th2);
+    double a, b;
+    if (th < 1e-8) {
+        a = 1.0 - th2 / 6.0;
+        b = 0.5 - th2 / 24.0;
+    } else {
+        a = sin(th) / th;
+        b = (1.0 - cos(th)) / th2;
+    }
+    double W[3][3] = {{0, -w[2], w[1]}, {w[2], 0, -w[0]}, {-w[1], w[0], 0}};
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            double w2 = W[i][0] * W[0][j] + W[i][1] * W[1][j] + W[i][2] * W[2][j];
+            Rx[i][j] = (i == j ? 1.0 : 0.0) + a * W[i][j] + b * w2;
+        }
+}
+
+static void gn_apply(const double R[3][3], const double t[3], const double c[3], const double xi[6],
+                     double s, double R2[3][3], double t2[3]) {
+    double w[3] = {s * xi[0], s * xi[1], s * xi[2]};
+    double Rx[3][3];
+    gn_exp(w, Rx);
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) R2[i][j] = Rx[i][0] * R[0][j] + Rx[i][1] * R[1][j] + Rx[i][2] * R[2][j];
+        t2[i] = Rx[i][0] * (t[0] - c[0]) + Rx[i][1] * (t[1] - c[1]) + Rx[i][2] * (t[2] - c[2]) + c[i] + s * xi[3 + i];
+    }
+}
+
+/* Inner GN solve on the correspondence set of the moments (taken at T = T0); T <- solution.
+ * 0 = accepted, -1 = too few correspondences / singular normal matrix (PCL would throw). */
+static int estimate_gn(ref_gicp* g, float T[4][4]) {
+    if (g->mom[73] < 4) return -1;
+    double R[3][3], t[3];
+    gn_pose_from_float(T, R, t);
+    double H[6][6], gv[6];
+    double fm = gn_eval(g, R, t, H, gv);
+    g->n_evals++;
+    for (int it = 0; it < g->prm.max_inner_iterations; ++it) {
+        double xi[6];
+        if (gn_chol_solve(H, gv, xi)) return -1;
+        double R2[3][3], t2[3], f2 = 0.0, s = 1.0;
+        int ok = 0;
+        for (int h = 0; h < 8; ++h, s *= 0.5) {
+            gn_apply(R, t, g->ctr, xi, s, R2, t2);
+            f2 = gn_eval(g, R2, t2, NULL, NULL);
+            if (f2 <= fm) { ok = 1; break; }
+        }
+        if (!ok) break; /* no descent along the GN direction: at the minimum to rounding */
+        memcpy(R, R2, sizeof(R));
+        memcpy(t, t2, sizeof(t));
+        double step = 0.0;
+        for (int k = 0; k < 6; ++k) step = fmax(step, fabs(s * xi[k]));
+        if (step < 1e-12) break;
+        fm = gn_eval(g, R, t, H, gv);
+        g->n_evals++;
+    }
+    for (int a = 0; a < 3; ++a) {
+        for (int k = 0; k < 3; ++k) T[a][k] = (float)R[a][k];
+        T[a][3] = (float)t[a];
+    }
+    return 0;
 }
 
 static void functor_eval(ref_gicp* g, const double x[6], double* f, double grad[6]) {
@@ -1216,9 +1412,10 @@ int ref_align(ref_gicp* g, const float guess_cm[16], float out_T_cm[16], ref_res
     while (!converged) {
         correspondence_sweep(g, T, G, NULL, NULL);
         r.n_corr_last = g->m;
-        if (g->prm.objective == 1) moments_build(g, T);
+        if (g->prm.objective == 1 || g->prm.solver == 1) moments_build(g, T);
         memcpy(prev, T, sizeof(T));
-        if (estimate_bfgs(g, T) != 0) break; /* PCLException: converged_ stays false */
+        if ((g->prm.solver == 1 ? estimate_gn(g, T) : estimate_bfgs(g, T)) != 0)
+            break; /* PCLException: converged_ stays false */
         double delta = 0.;
         for (int k = 0; k < 4; ++k)
             for (int l = 0; l < 4; ++l) {

@@ -39,6 +39,8 @@ typedef struct {
                                       1: moment form -- the same quadratic objective evaluated from
                                       74 fp64 moments taken once per outer iteration (checker for the
                                       engine's MGICP_OBJ_MOMENTS mode) */
+    int    solver;                 /* 0: PCL BFGS (default); 1: Gauss-Newton on the moment form
+                                      (checker for the engine's MGICP_SOLVER_GN; not in PCL) */
 } ref_params;
 
 typedef struct {
