@@ -604,8 +604,9 @@ static int sym_w(int i, int j) {
     return t[i][j];
 }
 
-/* One pass over the correspondences at T0: the 74 moments of the quadratic objective. */
-static void moments_build(ref_gicp* g, const float T0[4][4]) {
+/* One pass over correspondences [c0, c1) at T0: the 74 moments of the quadratic objective
+ * (a contiguous range is one rank's share in the N > 1 decomposition). */
+static void moments_build_range(ref_gicp* g, const float T0[4][4], int c0, int c1) {
     memcpy(g->T0, T0, sizeof(g->T0));
     float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int i = 0; i < g->ns; ++i)
@@ -617,7 +618,7 @@ static void moments_build(ref_gicp* g, const float T0[4][4]) {
     for (int a = 0; a < 3; ++a) g->ctr[a] = (double)(0.5f * (lo[a] + hi[a]));
     double* mo = g->mom;
     memset(mo, 0, sizeof(g->mom));
-    for (int c = 0; c < g->m; ++c) {
+    for (int c = c0; c < c1; ++c) {
         int i = g->corr_src[c], j = g->corr_tgt[c];
         const float* ps = g->out + 3 * (size_t)i;
         const float* pt = g->tgt + 3 * (size_t)j;
@@ -638,6 +639,8 @@ static void moments_build(ref_gicp* g, const float T0[4][4]) {
         mo[73] += 1.0;
     }
 }
+
+static void moments_build(ref_gicp* g, const float T0[4][4]) { moments_build_range(g, T0, 0, g->m); }
 
 /* f / grad at x from the moments: r(x) = r0 + Y w, Y = [dR | dR ctr + dt], dA = A(x) - T0 */
 static void moments_eval(ref_gicp* g, const double x[6], double* f, double grad[6]) {
@@ -936,6 +939,15 @@ int ref_moments(ref_gicp* g, const float T0_cm[16], double out74[74]) {
     cm_to_rm(T0_cm, T0);
     moments_build(g, T0);
     if (out74) memcpy(out74, g->mom, sizeof(g->mom));
+    return REF_OK;
+}
+
+int ref_moments_range(ref_gicp* g, const float T0_cm[16], int c0, int c1, double out74[74]) {
+    if (!g || !g->out || g->m <= 0 || c0 < 0 || c1 < c0 || c1 > g->m || !out74) return REF_E_INVALID;
+    float T0[4][4];
+    cm_to_rm(T0_cm, T0);
+    moments_build_range(g, T0, c0, c1);
+    memcpy(out74, g->mom, sizeof(g->mom));
     return REF_OK;
 }
 

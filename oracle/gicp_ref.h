@@ -89,6 +89,7 @@ int ref_correspondences(ref_gicp* g, const float T_cm[16], const float guess_cm[
 /* Moment-form objective (ref_params.objective = 1): build the 74 moments of the last
  * correspondence set at transform T0 (col-major); out74 optional. */
 int ref_moments(ref_gicp* g, const float T0_cm[16], double out74[74]);
+int ref_moments_range(ref_gicp* g, const float T0_cm[16], int c0, int c1, double out74[74]);
 /* OptimizationFunctorWithIndices::fdf at state x for the last correspondence set. */
 int ref_fdf(ref_gicp* g, const double x[6], double* f, double g6[6]);
 /* raw sums of the functor over correspondences [c0, c1): f, g_t[3], Rsum[9] row-major, count

@@ -74,6 +74,7 @@ def load():
         "ref_correspondences": (ctypes.c_int, [P, FP, FP, IP, FP, DP]),
         "ref_fdf": (ctypes.c_int, [P, DP, DP, DP]),
         "ref_moments": (ctypes.c_int, [P, FP, DP]),
+        "ref_moments_range": (ctypes.c_int, [P, FP, ctypes.c_int, ctypes.c_int, DP]),
         "ref_fdf_sums": (ctypes.c_int, [P, DP, ctypes.c_int, ctypes.c_int, DP]),
         "ref_apply_state": (None, [DP, FP]),
     }
@@ -186,6 +187,12 @@ class RefGICP:
     def moments(self, T0):
         out = np.zeros(74, np.float64)
         rc = self.lib.ref_moments(self.h, _fp(cm(T0)), _dp(out))
+        assert rc == 0
+        return out
+
+    def moments_range(self, T0, c0, c1):
+        out = np.zeros(74, np.float64)
+        rc = self.lib.ref_moments_range(self.h, _fp(cm(T0)), int(c0), int(c1), _dp(out))
         assert rc == 0
         return out
 

@@ -49,7 +49,15 @@ def _gloo_worker(rank, world, port, q):
     f_ref, g_ref = o.fdf(x)
     s = part.numpy()
     f = s[0] / s[13]
-    q.put((rank, float(np.abs(s - full).max() / np.abs(full).max()), abs(f - f_ref) / abs(f_ref), int(s[13]), m))
+    # Gauss-Newton mode: one all-reduce of the 74 moments per outer iteration
+    T0 = np.eye(4, dtype=np.float32)
+    mom = torch.tensor(o.moments_range(T0, c0, c1), dtype=torch.float64)
+    dist.all_reduce(mom, op=dist.ReduceOp.SUM)
+    mfull = o.moments(T0)
+    rel_mom = max(float(np.abs(mom.numpy()[a:b] - mfull[a:b]).max() / np.abs(mfull[a:b]).max())
+                  for a, b in ((0, 1), (1, 13), (13, 74)))
+    q.put((rank, float(np.abs(s - full).max() / np.abs(full).max()), abs(f - f_ref) / abs(f_ref), int(s[13]), m,
+           rel_mom))
     dist.destroy_process_group()
 
 
@@ -64,10 +72,11 @@ def test_sharded_objective_gloo_world2():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, rel_sums, rel_f, cnt, m in res:
+    for rank, rel_sums, rel_f, cnt, m, rel_mom in res:
         assert cnt == m
         assert rel_sums <= 1e-12
         assert rel_f <= 1e-12
+        assert rel_mom <= 1e-12
 
 
 def _rdv_worker(rank, world, port, q):
@@ -121,6 +130,8 @@ def test_detached_shards_sum_to_full(part_small):
     m_full, tj_full, _ = full.debug_correspondences(T, len(scan))
     x = np.array([0.001, -0.002, 0.0005, 0.0003, -0.0002, 0.0004])
     s_full = full.debug_fdf_sums(x)
+    mom_full = full.debug_moments(T)
+    mom_total = np.zeros(80)
     total = np.zeros(16)
     tj = np.full(len(scan), -1, np.int32)
     m_sum = 0
@@ -135,6 +146,7 @@ def test_detached_shards_sum_to_full(part_small):
         own = tj_r >= 0
         tj[own] = tj_r[own]
         total += e.debug_fdf_sums(x)
+        mom_total += e.debug_moments(T)
         with pytest.raises(Exception):
             e.align()  # detached shards cannot run the collective path
         e.close()
@@ -142,3 +154,7 @@ def test_detached_shards_sum_to_full(part_small):
     np.testing.assert_array_equal(tj, tj_full)
     assert total[13] == s_full[13] == m_full
     assert np.abs(total - s_full).max() <= 1e-11 * np.abs(s_full).max()
+    # Gauss-Newton mode: the shards' moments add up to the unsharded moment pass
+    assert mom_total[73] == mom_full[73] == m_full
+    for a, b in ((0, 1), (1, 13), (13, 73)):
+        assert np.abs(mom_total[a:b] - mom_full[a:b]).max() <= 1e-11 * np.abs(mom_full[a:b]).max()
