@@ -84,6 +84,10 @@ _SIGNATURES = {
     "mgicp_transform_cloud": (ctypes.c_int, [_P, _FP, _P, _SZ, _SZ, _P, _SZ]),
     "mgicp_cloud_resolution": (ctypes.c_int, [_P, _P, _SZ, _SZ, _DP]),
     "mgicp_radius_filter": (ctypes.c_int, [_P, _P, _SZ, _SZ, ctypes.c_double, ctypes.c_int, _P]),
+    "mgicp_segment_differences": (ctypes.c_int, [_P, _FP, _P, _SZ, _SZ, _P, _SZ, _SZ, ctypes.c_double, _P,
+                                                  ctypes.POINTER(_SZ)]),
+    "mgicp_voxel_grid": (ctypes.c_int, [_P, _P, _SZ, _SZ, ctypes.c_int, _DP, ctypes.c_int, _P, _SZ,
+                                         ctypes.POINTER(_SZ)]),
     "mgicp_get_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
     "mgicp_comm_init": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]),
     "mgicp_debug_covariances": (ctypes.c_int, [_P, ctypes.c_int, _DP]),

@@ -208,6 +208,7 @@ struct Cloud {
   DevBuf<uint32_t> cell_start;
   DevBuf<uint8_t> empty_dist; // empty-space map (target only: 1-NN queries leave the surface)
   bool want_empty_map = false;
+  bool drop_nonfinite = false; // build the grid over the finite points only (KdTreeFLANN semantics)
   DevBuf<double2> cov;        // 3 * n
   float lo[3] = {0.f, 0.f, 0.f}, hi[3] = {0.f, 0.f, 0.f};  // bounding box (original coordinates)
   GridView view{};
@@ -225,7 +226,13 @@ struct mgicp_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   Cloud src, tgt;
-  Cloud aux;  // scratch cloud of the resolution / radius helpers
+  Cloud aux;  // scratch cloud of the resolution / radius / segment-differences helpers
+  Cloud qry;  // query points of the FOD-side helpers (packed only, no grid)
+  // FOD-side helper buffers (SegmentDifferences, VoxelGrid)
+  DevBuf<uint32_t> f_flags, f_pos, f_rgba_in, f_rgba, f_rgba2;
+  DevBuf<float4> f_vox, f_vox2;
+  DevBuf<unsigned char> f_keep;
+  DevBuf<unsigned int> f_count;
   double occupancy = kDefaultOccupancy;  // grid cell sizing target (env MGICP_GRID_OCC)
   // objective-pass launch shape, A/B-measured on MI355X at 5M points (profiles/r01/ab3_*.json):
   // fence-free in-launch finish at 256 blocks (one per CU) beats 128..2048 blocks and a
@@ -392,7 +399,7 @@ int upload_cloud(mgicp_ctx* ctx, Cloud& cl, const float* xyz, size_t n, size_t s
   cl.n = n;
   cl.dirty = true;
   cl.have_cov = false;
-  if (&cl != &ctx->aux) {
+  if (&cl == &ctx->src || &cl == &ctx->tgt) {
     ctx->have_corr = false;
     ctx->ms_upload_pending += now_ms() - t0;
   }
@@ -421,6 +428,26 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
       mx[d] = std::max(mx[d], hp[b * 8 + 3 + d]);
     }
     bad += hp[b * 8 + 6];
+  }
+  if (bad > 0 && cl.drop_nonfinite) {
+    // keep the finite points (original indices stay in w) and rebuild from them
+    HIPCK(ctx->f_flags.reserve(n + 1));
+    HIPCK(ctx->f_pos.reserve(n + 1));
+    HIPCK(cl.pts.reserve(n));
+    const size_t sb = scan_scratch_bytes(n + 1);
+    HIPCK(ctx->scratch.reserve(sb));
+    HIPCK(launch_finite_compact(cl.orig.p, n, ctx->f_flags.p, ctx->f_pos.p, ctx->scratch.p, sb, cl.pts.p, s));
+    HIPCK(hipMemcpyAsync(ctx->h_small, ctx->f_pos.p + n, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    if ((rc = sync(ctx))) return rc;
+    uint32_t kept = 0;
+    std::memcpy(&kept, ctx->h_small, sizeof(kept));
+    if (kept > 0) HIPCK(hipMemcpyAsync(cl.orig.p, cl.pts.p, kept * sizeof(float4), hipMemcpyDeviceToDevice, s));
+    cl.n = kept;
+    if (kept == 0) {
+      cl.dirty = false;
+      return MGICP_OK;  // empty cloud: callers check cl.n
+    }
+    return build_grid(ctx, cl);
   }
   if (bad > 0) return fail(ctx, MGICP_E_NONFINITE, "cloud contains NaN/Inf coordinates");
   for (int d = 0; d < 3; ++d) {
@@ -1052,7 +1079,10 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
-  for (Cloud* c : {&ctx->src, &ctx->tgt, &ctx->aux}) {
+  ctx->f_flags.release(); ctx->f_pos.release(); ctx->f_rgba_in.release(); ctx->f_rgba.release();
+  ctx->f_rgba2.release(); ctx->f_vox.release(); ctx->f_vox2.release(); ctx->f_keep.release();
+  ctx->f_count.release();
+  for (Cloud* c : {&ctx->src, &ctx->tgt, &ctx->aux, &ctx->qry}) {
     c->raw.release(); c->orig.release(); c->pts.release(); c->perm.release();
     c->cell_start.release(); c->cov.release(); c->empty_dist.release();
   }
@@ -1290,6 +1320,160 @@ int mgicp_radius_filter(mgicp_ctx* ctx, const float* xyz, size_t n, size_t strid
   rc = sync(ctx);
   d_keep.release();
   return rc;
+}
+
+int mgicp_segment_differences(mgicp_ctx* ctx, const float T_cm[16], const float* in, size_t n,
+                              size_t in_stride, const float* sub, size_t n_sub, size_t sub_stride,
+                              double sqr_threshold, unsigned char* keep, size_t* n_keep) {
+  if (!ctx || !n_keep || (n && (!in || !keep)) || (n_sub && !sub) || !(sqr_threshold == sqr_threshold))
+    return MGICP_E_INVALID;
+  HIPCK(hipSetDevice(ctx->device));
+  *n_keep = 0;
+  if (n == 0) return MGICP_OK;
+  if (n_sub == 0) {  // "input - empty target = input": every record, finite or not
+    std::memset(keep, 1, n);
+    *n_keep = n;
+    return MGICP_OK;
+  }
+  int rc = upload_cloud(ctx, ctx->aux, sub, n_sub, sub_stride, false);
+  if (rc) return rc;
+  ctx->aux.drop_nonfinite = true;
+  rc = build_grid(ctx, ctx->aux);
+  ctx->aux.drop_nonfinite = false;
+  if (rc) return rc;
+  if (ctx->aux.n == 0) {  // no finite target point: nearestKSearch finds nothing, nothing kept
+    std::memset(keep, 0, n);
+    return MGICP_OK;
+  }
+  if ((rc = upload_cloud(ctx, ctx->qry, in, n, in_stride, false))) return rc;
+  hipStream_t s = ctx->stream;
+  HIPCK(ctx->f_keep.reserve(n));
+  HIPCK(ctx->f_count.reserve(1));
+  HIPCK(hipMemsetAsync(ctx->f_count.p, 0, sizeof(unsigned int), s));
+  const Mat4 T = T_cm ? Mat4::from_cm(T_cm) : Mat4::identity();
+  HIPCK(launch_segdiff(ctx->aux.view, ctx->qry.orig.p, n, T.xf(), T_cm ? 1 : 0, sqr_threshold,
+                       ctx->f_keep.p, ctx->f_count.p, s));
+  HIPCK(hipMemcpyAsync(keep, ctx->f_keep.p, n, hipMemcpyDeviceToHost, s));
+  HIPCK(hipMemcpyAsync(ctx->h_small, ctx->f_count.p, sizeof(unsigned int), hipMemcpyDeviceToHost, s));
+  if ((rc = sync(ctx))) return rc;
+  unsigned int cnt = 0;
+  std::memcpy(&cnt, ctx->h_small, sizeof(cnt));
+  *n_keep = cnt;
+  return MGICP_OK;
+}
+
+int mgicp_voxel_grid(mgicp_ctx* ctx, const float* in, size_t n, size_t stride, int rgb_offset,
+                     const double leaf[3], int min_points_per_voxel, float* out, size_t out_stride,
+                     size_t* n_out) {
+  if (!ctx || !n_out || !leaf || (n && (!in || !out)) || out_stride < 12 || (out_stride % 4) ||
+      (rgb_offset >= 0 && (static_cast<size_t>(rgb_offset) + 4 > stride ||
+                           static_cast<size_t>(rgb_offset) + 4 > out_stride || (rgb_offset % 4))))
+    return MGICP_E_INVALID;
+  for (int d = 0; d < 3; ++d)
+    if (!(leaf[d] > 0)) return fail(ctx, MGICP_E_INVALID, "leaf size must be > 0");
+  HIPCK(hipSetDevice(ctx->device));
+  *n_out = 0;
+  if (n == 0) return MGICP_OK;
+  int rc = upload_cloud(ctx, ctx->qry, in, n, stride, false);
+  if (rc) return rc;
+  hipStream_t s = ctx->stream;
+  const bool rgb = rgb_offset >= 0;
+  if (rgb) {  // the packed colour word of every record (host marshalling of one field)
+    std::vector<uint32_t> h(n);
+    const unsigned char* base = reinterpret_cast<const unsigned char*>(in);
+    for (size_t i = 0; i < n; ++i) std::memcpy(&h[i], base + i * stride + rgb_offset, 4);
+    HIPCK(ctx->f_rgba_in.reserve(n));
+    HIPCK(hipMemcpyAsync(ctx->f_rgba_in.p, h.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    if ((rc = sync(ctx))) return rc;
+  }
+  // getMinMax3D over the finite points
+  const int nb = static_cast<int>(std::min<size_t>((n + 255) / 256, 1024));
+  HIPCK(launch_bbox(ctx->qry.orig.p, n, reinterpret_cast<float*>(ctx->d_small), nb, s));
+  if ((rc = sync(ctx))) return rc;
+  const float* hp = reinterpret_cast<const float*>(ctx->h_small);
+  float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int b = 0; b < nb; ++b)
+    for (int d = 0; d < 3; ++d) {
+      mn[d] = std::min(mn[d], hp[b * 8 + d]);
+      mx[d] = std::max(mx[d], hp[b * 8 + 3 + d]);
+    }
+  if (!(mn[0] <= mx[0])) return MGICP_OK;  // no finite point
+  float inv[3];
+  for (int d = 0; d < 3; ++d) inv[d] = 1.0f / static_cast<float>(leaf[d]);
+  int64_t dd[3];
+  for (int d = 0; d < 3; ++d) dd[d] = static_cast<int64_t>((mx[d] - mn[d]) * inv[d]) + 1;
+  auto put = [&](size_t i, float x, float y, float z, const uint32_t* c) {
+    unsigned char* r = reinterpret_cast<unsigned char*>(out) + i * out_stride;
+    std::memset(r, 0, out_stride);
+    float* f = reinterpret_cast<float*>(r);
+    f[0] = x; f[1] = y; f[2] = z;
+    if (out_stride >= 16) f[3] = 1.0f;
+    if (c) std::memcpy(r + rgb_offset, c, 4);
+  };
+  if (dd[0] * dd[1] * dd[2] > static_cast<int64_t>(INT32_MAX)) {
+    // "Leaf size is too small for the input dataset": output = input
+    const unsigned char* base = reinterpret_cast<const unsigned char*>(in);
+    for (size_t i = 0; i < n; ++i) {
+      const float* p = reinterpret_cast<const float*>(base + i * stride);
+      uint32_t c = 0;
+      if (rgb) std::memcpy(&c, base + i * stride + rgb_offset, 4);
+      put(i, p[0], p[1], p[2], rgb ? &c : nullptr);
+    }
+    *n_out = n;
+    return MGICP_OK;
+  }
+  int min_b[3], div_b[3];
+  for (int d = 0; d < 3; ++d) {
+    min_b[d] = static_cast<int>(std::floor(mn[d] * inv[d]));
+    div_b[d] = static_cast<int>(std::floor(mx[d] * inv[d])) - min_b[d] + 1;
+  }
+  Cloud& q = ctx->qry;
+  HIPCK(ctx->keys.reserve(n));
+  HIPCK(ctx->keys_sorted.reserve(n));
+  HIPCK(ctx->vals.reserve(n));
+  HIPCK(q.perm.reserve(n));
+  HIPCK(ctx->f_flags.reserve(n + 1));
+  HIPCK(ctx->f_pos.reserve(n + 1));
+  const size_t sb = std::max(sort_scratch_bytes(n, 32), scan_scratch_bytes(n + 1));
+  HIPCK(ctx->scratch.reserve(sb));
+  HIPCK(launch_voxel_keys(q.orig.p, n, inv, min_b, div_b[0], div_b[0] * div_b[1], ctx->keys.p, s));
+  HIPCK(launch_iota(ctx->vals.p, n, s));
+  HIPCK(launch_sort_pairs(ctx->scratch.p, sb, ctx->keys.p, ctx->keys_sorted.p, ctx->vals.p, q.perm.p, n, 32, s));
+  HIPCK(launch_voxel_heads(ctx->keys_sorted.p, n, ctx->f_flags.p, s));
+  HIPCK(launch_exclusive_scan(ctx->scratch.p, sb, ctx->f_flags.p, ctx->f_pos.p, n + 1, s));
+  HIPCK(hipMemcpyAsync(ctx->h_small, ctx->f_pos.p + n, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  if ((rc = sync(ctx))) return rc;
+  uint32_t nv = 0;
+  std::memcpy(&nv, ctx->h_small, sizeof(nv));
+  HIPCK(ctx->f_vox.reserve(nv + 1));
+  if (rgb) HIPCK(ctx->f_rgba.reserve(nv + 1));
+  HIPCK(launch_voxel_centroids(ctx->keys_sorted.p, q.perm.p, ctx->f_flags.p, ctx->f_pos.p, n, q.orig.p,
+                               rgb ? ctx->f_rgba_in.p : nullptr, ctx->f_vox.p, rgb ? ctx->f_rgba.p : nullptr, s));
+  const float4* vox = ctx->f_vox.p;
+  const uint32_t* vrgb = rgb ? ctx->f_rgba.p : nullptr;
+  if (min_points_per_voxel > 1) {
+    HIPCK(ctx->f_vox2.reserve(nv + 1));
+    if (rgb) HIPCK(ctx->f_rgba2.reserve(nv + 1));
+    const size_t sb2 = scan_scratch_bytes(nv + 1);
+    HIPCK(ctx->scratch.reserve(std::max(sb, sb2)));
+    HIPCK(launch_voxel_minpts(ctx->f_vox.p, vrgb, nv, static_cast<uint32_t>(min_points_per_voxel), ctx->f_flags.p,
+                              ctx->f_pos.p, ctx->scratch.p, sb2, ctx->f_vox2.p, rgb ? ctx->f_rgba2.p : nullptr, s));
+    HIPCK(hipMemcpyAsync(ctx->h_small, ctx->f_pos.p + nv, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    if ((rc = sync(ctx))) return rc;
+    std::memcpy(&nv, ctx->h_small, sizeof(nv));
+    vox = ctx->f_vox2.p;
+    vrgb = rgb ? ctx->f_rgba2.p : nullptr;
+  }
+  std::vector<float4> hv(nv);
+  std::vector<uint32_t> hc(rgb ? nv : 0);
+  if (nv) {
+    HIPCK(hipMemcpyAsync(hv.data(), vox, nv * sizeof(float4), hipMemcpyDeviceToHost, s));
+    if (rgb) HIPCK(hipMemcpyAsync(hc.data(), vrgb, nv * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  }
+  if ((rc = sync(ctx))) return rc;
+  for (size_t v = 0; v < nv; ++v) put(v, hv[v].x, hv[v].y, hv[v].z, rgb ? &hc[v] : nullptr);
+  *n_out = nv;
+  return MGICP_OK;
 }
 
 int mgicp_get_unique_id(unsigned char id[128]) {

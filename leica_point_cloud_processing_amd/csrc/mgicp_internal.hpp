@@ -106,6 +106,26 @@ hipError_t launch_resolution(const GridView& g, size_t n, double* partial, int n
 hipError_t launch_radius_keep(const GridView& g, size_t n, float r2, int need, unsigned char* keep,
                               hipStream_t s);
 
+// ---- FOD-side callers ----
+// finite points of `in` -> out (order kept, w = original index kept); flags/pos: n + 1 each,
+// scratch: scan_scratch_bytes(n + 1); the count is pos[n]
+hipError_t launch_finite_compact(const float4* in, size_t n, uint32_t* flags, uint32_t* pos,
+                                 void* scratch, size_t scratch_bytes, float4* out, hipStream_t s);
+// SegmentDifferences: keep[i] = finite(T in_i) && 1-NN float d2 > thr; *count += kept
+hipError_t launch_segdiff(const GridView& g, const float4* in, size_t n, Xf34 T, int has_T, double thr,
+                          unsigned char* keep, unsigned int* count, hipStream_t s);
+// VoxelGrid: leaf keys (non-finite -> 0xffffffff), run heads of the sorted keys (n + 1 flags),
+// per-leaf centroids at the scanned head positions, min_points_per_voxel compaction
+hipError_t launch_voxel_keys(const float4* pts, size_t n, const float inv[3], const int min_b[3],
+                             int mul1, int mul2, uint32_t* keys, hipStream_t s);
+hipError_t launch_voxel_heads(const uint32_t* keys_sorted, size_t n, uint32_t* flags, hipStream_t s);
+hipError_t launch_voxel_centroids(const uint32_t* keys_sorted, const uint32_t* perm, const uint32_t* flags,
+                                  const uint32_t* pos, size_t n, const float4* pts, const uint32_t* rgba,
+                                  float4* out, uint32_t* out_rgba, hipStream_t s);
+hipError_t launch_voxel_minpts(const float4* vox, const uint32_t* vox_rgba, size_t nv, uint32_t need,
+                               uint32_t* flags, uint32_t* pos, void* scratch, size_t scratch_bytes,
+                               float4* out, uint32_t* out_rgba, hipStream_t s);
+
 // radix sort / scan scratch (hipcub)
 size_t sort_scratch_bytes(size_t n, int bits);
 hipError_t launch_sort_pairs(void* scratch, size_t scratch_bytes, const uint32_t* keys_in,

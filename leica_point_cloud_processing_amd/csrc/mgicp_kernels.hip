@@ -916,6 +916,145 @@ __global__ __launch_bounds__(256) void reduce_finish_kernel(const double* __rest
 }
 
 // ------------------------------------------------------------------------------------
+// FOD-side callers of the GICP path
+// ------------------------------------------------------------------------------------
+// 1 for finite points (cloud compaction before a grid build: KdTreeFLANN skips NaN points)
+__global__ void finite_flags_kernel(const float4* __restrict__ p, size_t n, uint32_t* __restrict__ flags) {
+  const size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i > n) return;
+  flags[i] = (i < n && isfinite(p[i].x) && isfinite(p[i].y) && isfinite(p[i].z)) ? 1u : 0u;
+}
+
+__global__ void scatter_flagged_kernel(const float4* __restrict__ in, const uint32_t* __restrict__ flags,
+                                       const uint32_t* __restrict__ pos, size_t n, float4* __restrict__ out) {
+  const size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < n && flags[i]) out[pos[i]] = in[i];
+}
+
+// "is there a point with float d2 <= thr?" -- stops at the first one (exact: the ring bound
+// proves absence before giving up)
+struct WithinVisitor {
+  float qx, qy, qz;
+  double thr;
+  float thr_f;  // float upper bound of thr (pruning radius)
+  bool found;
+  __device__ __forceinline__ bool done(float Ls) const {
+    if (found) return true;
+    return Ls > 0.f && static_cast<double>(Ls) * static_cast<double>(Ls) > thr;
+  }
+  __device__ __forceinline__ float prune2() const { return found ? -1.f : thr_f; }
+  __device__ __forceinline__ void range(const GridView& g, uint32_t a, uint32_t b) {
+    for (uint32_t j = a; j < b && !found; ++j)
+      if (static_cast<double>(dist2(qx, qy, qz, g.pts[j])) <= thr) found = true;
+  }
+};
+
+// pcl::getPointCloudDifference: keep[i] = 1 iff input point i, transformed by T, is finite and
+// its nearest neighbour in the grid has float d2 > thr (src/Filter.cpp:176-189); counts kept points
+__global__ __launch_bounds__(256) void segdiff_kernel(GridView g, const float4* __restrict__ in,
+                                                      size_t n, Xf34 T, int has_T, double thr,
+                                                      unsigned char* __restrict__ keep,
+                                                      unsigned int* __restrict__ count) {
+  const size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  bool k = false;
+  if (i < n) {
+    const float4 p = in[i];
+    float qx = p.x, qy = p.y, qz = p.z;
+    if (has_T) xform(T, p.x, p.y, p.z, qx, qy, qz);
+    if (isfinite(qx) && isfinite(qy) && isfinite(qz)) {
+      WithinVisitor vis{qx, qy, qz, thr, thr >= 3.0e38 ? INFINITY : __double2float_ru(thr), false};
+      ring_search(g, qx, qy, qz, vis);
+      k = !vis.found;
+    }
+    keep[i] = k ? 1 : 0;
+  }
+  // one integer atomic per wave (order-independent: the count is exact)
+  const unsigned long long ballot = __ballot(k);
+  if ((threadIdx.x & 63) == 0 && ballot) atomicAdd(count, static_cast<unsigned int>(__popcll(ballot)));
+}
+
+// VoxelGrid leaf index of every point (voxel_grid.hpp applyFilter, first pass); non-finite
+// points get the sentinel 0xffffffff and sort behind every leaf
+__global__ void voxel_key_kernel(const float4* __restrict__ p, size_t n, float ix, float iy, float iz,
+                                 int bx, int by, int bz, int mul1, int mul2, uint32_t* __restrict__ keys) {
+  const size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float4 q = p[i];
+  if (!isfinite(q.x) || !isfinite(q.y) || !isfinite(q.z)) {
+    keys[i] = 0xffffffffu;
+    return;
+  }
+  const int i0 = static_cast<int>(floorf(q.x * ix) - static_cast<float>(bx));
+  const int i1 = static_cast<int>(floorf(q.y * iy) - static_cast<float>(by));
+  const int i2 = static_cast<int>(floorf(q.z * iz) - static_cast<float>(bz));
+  keys[i] = static_cast<uint32_t>(i0 + i1 * mul1 + i2 * mul2);
+}
+
+// run heads of the sorted leaf keys (sentinel excluded); flags[n] = 0 closes the scan
+__global__ void voxel_head_kernel(const uint32_t* __restrict__ keys, size_t n, uint32_t* __restrict__ flags) {
+  const size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i > n) return;
+  if (i == n) {
+    flags[n] = 0;
+    return;
+  }
+  const uint32_t k = keys[i];
+  flags[i] = (k != 0xffffffffu && (i == 0 || keys[i - 1] != k)) ? 1u : 0u;
+}
+
+// CentroidPoint<PointXYZRGB> of one leaf per head thread, summed sequentially in the sorted
+// order (stable in the input index): xyz fp32 sums / float(count); r, g, b, a float sums,
+// truncated after the division.  out[v] = (cx, cy, cz, bit_cast(count)).
+__global__ void voxel_centroid_kernel(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ perm,
+                                      const uint32_t* __restrict__ flags, const uint32_t* __restrict__ pos,
+                                      size_t n, const float4* __restrict__ pts, const uint32_t* __restrict__ rgba,
+                                      float4* __restrict__ out, uint32_t* __restrict__ out_rgba) {
+  const size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n || !flags[i]) return;
+  const uint32_t k = keys[i];
+  float sx = 0.f, sy = 0.f, sz = 0.f, r = 0.f, g = 0.f, b = 0.f, a = 0.f;
+  size_t l = i;
+  for (; l < n && keys[l] == k; ++l) {
+    const uint32_t j = perm[l];
+    const float4 q = pts[j];
+    sx = sx + q.x;
+    sy = sy + q.y;
+    sz = sz + q.z;
+    if (rgba) {
+      const uint32_t c = rgba[j];
+      b = b + static_cast<float>(c & 0xffu);
+      g = g + static_cast<float>((c >> 8) & 0xffu);
+      r = r + static_cast<float>((c >> 16) & 0xffu);
+      a = a + static_cast<float>(c >> 24);
+    }
+  }
+  const uint32_t cnt = static_cast<uint32_t>(l - i);
+  const float fc = static_cast<float>(cnt);
+  const uint32_t v = pos[i];
+  out[v] = make_float4(sx / fc, sy / fc, sz / fc, __uint_as_float(cnt));
+  if (rgba)
+    out_rgba[v] = (static_cast<uint32_t>(a / fc) << 24) | (static_cast<uint32_t>(r / fc) << 16) |
+                  (static_cast<uint32_t>(g / fc) << 8) | static_cast<uint32_t>(b / fc);
+}
+
+// min_points_per_voxel: 1 for leaves with at least `need` points (flags[nv] = 0)
+__global__ void voxel_minpts_kernel(const float4* __restrict__ vox, size_t nv, uint32_t need,
+                                    uint32_t* __restrict__ flags) {
+  const size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i > nv) return;
+  flags[i] = (i < nv && __float_as_uint(vox[i].w) >= need) ? 1u : 0u;
+}
+
+__global__ void scatter_voxels_kernel(const float4* __restrict__ in, const uint32_t* __restrict__ in_rgba,
+                                      const uint32_t* __restrict__ flags, const uint32_t* __restrict__ pos,
+                                      size_t nv, float4* __restrict__ out, uint32_t* __restrict__ out_rgba) {
+  const size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= nv || !flags[i]) return;
+  out[pos[i]] = in[i];
+  if (in_rgba) out_rgba[pos[i]] = in_rgba[i];
+}
+
+// ------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------
 static inline unsigned nblk(size_t n, unsigned t = 256) {
@@ -1077,6 +1216,56 @@ hipError_t launch_reduce_finish(const double* partial, int nb, double* out, hipS
   return hipGetLastError();
 }
 
+hipError_t launch_finite_compact(const float4* in, size_t n, uint32_t* flags, uint32_t* pos,
+                                 void* scratch, size_t scratch_bytes, float4* out, hipStream_t s) {
+  finite_flags_kernel<<<nblk(n + 1), 256, 0, s>>>(in, n, flags);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  if ((e = launch_exclusive_scan(scratch, scratch_bytes, flags, pos, n + 1, s)) != hipSuccess) return e;
+  scatter_flagged_kernel<<<nblk(n), 256, 0, s>>>(in, flags, pos, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_segdiff(const GridView& g, const float4* in, size_t n, Xf34 T, int has_T, double thr,
+                          unsigned char* keep, unsigned int* count, hipStream_t s) {
+  if (!n) return hipSuccess;
+  segdiff_kernel<<<nblk(n), 256, 0, s>>>(g, in, n, T, has_T, thr, keep, count);
+  return hipGetLastError();
+}
+
+hipError_t launch_voxel_keys(const float4* pts, size_t n, const float inv[3], const int min_b[3],
+                             int mul1, int mul2, uint32_t* keys, hipStream_t s) {
+  if (!n) return hipSuccess;
+  voxel_key_kernel<<<nblk(n), 256, 0, s>>>(pts, n, inv[0], inv[1], inv[2], min_b[0], min_b[1], min_b[2],
+                                           mul1, mul2, keys);
+  return hipGetLastError();
+}
+
+hipError_t launch_voxel_heads(const uint32_t* keys_sorted, size_t n, uint32_t* flags, hipStream_t s) {
+  voxel_head_kernel<<<nblk(n + 1), 256, 0, s>>>(keys_sorted, n, flags);
+  return hipGetLastError();
+}
+
+hipError_t launch_voxel_centroids(const uint32_t* keys_sorted, const uint32_t* perm, const uint32_t* flags,
+                                  const uint32_t* pos, size_t n, const float4* pts, const uint32_t* rgba,
+                                  float4* out, uint32_t* out_rgba, hipStream_t s) {
+  if (!n) return hipSuccess;
+  voxel_centroid_kernel<<<nblk(n), 256, 0, s>>>(keys_sorted, perm, flags, pos, n, pts, rgba, out, out_rgba);
+  return hipGetLastError();
+}
+
+hipError_t launch_voxel_minpts(const float4* vox, const uint32_t* vox_rgba, size_t nv, uint32_t need,
+                               uint32_t* flags, uint32_t* pos, void* scratch, size_t scratch_bytes,
+                               float4* out, uint32_t* out_rgba, hipStream_t s) {
+  voxel_minpts_kernel<<<nblk(nv + 1), 256, 0, s>>>(vox, nv, need, flags);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  if ((e = launch_exclusive_scan(scratch, scratch_bytes, flags, pos, nv + 1, s)) != hipSuccess) return e;
+  if (!nv) return hipSuccess;
+  scatter_voxels_kernel<<<nblk(nv), 256, 0, s>>>(vox, vox_rgba, flags, pos, nv, out, out_rgba);
+  return hipGetLastError();
+}
+
 size_t sort_scratch_bytes(size_t n, int bits) {
   size_t bytes = 0;
   (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, static_cast<const uint32_t*>(nullptr),
@@ -1133,6 +1322,14 @@ hipError_t preload_kernels(void* pinned, size_t pinned_bytes, hipStream_t s) {
       reinterpret_cast<const void*>(&reduce_finish_kernel),
       reinterpret_cast<const void*>(&gn_moments_kernel),
       reinterpret_cast<const void*>(&reduce_finish_moments_kernel),
+      reinterpret_cast<const void*>(&finite_flags_kernel),
+      reinterpret_cast<const void*>(&scatter_flagged_kernel),
+      reinterpret_cast<const void*>(&segdiff_kernel),
+      reinterpret_cast<const void*>(&voxel_key_kernel),
+      reinterpret_cast<const void*>(&voxel_head_kernel),
+      reinterpret_cast<const void*>(&voxel_centroid_kernel),
+      reinterpret_cast<const void*>(&voxel_minpts_kernel),
+      reinterpret_cast<const void*>(&scatter_voxels_kernel),
   };
   for (const void* f : fns) {
     hipFuncAttributes attr;

@@ -224,6 +224,35 @@ class GICPEngine:
                                                   int(min_neighbors), keep.ctypes.data), "radius_filter")
         return keep.astype(bool)
 
+    # -- FOD-side callers ------------------------------------------
+    def segment_differences(self, cloud_in, cloud_sub, sqr_threshold: float, T=None):
+        """pcl::SegmentDifferences (Filter::removeFromCloud): bool keep mask over cloud_in (after T)
+        and the kept count."""
+        keep_in, pin, n, sin_ = self._cloud_arg(cloud_in)
+        keep_sub, psub, ns, ssub = self._cloud_arg(cloud_sub)
+        keep = np.zeros(max(n, 1), np.uint8)
+        cnt = ctypes.c_size_t()
+        tcm = _cm(T) if T is not None else None
+        self._check(self._lib.mgicp_segment_differences(
+            self._h, _fp(tcm) if tcm is not None else None, ctypes.c_void_p(pin), n, sin_, ctypes.c_void_p(psub),
+            ns, ssub, float(sqr_threshold), keep.ctypes.data, ctypes.byref(cnt)), "segment_differences")
+        return keep[:n].astype(bool), int(cnt.value)
+
+    def voxel_grid(self, cloud: PointCloudRGB, leaf, min_points_per_voxel: int = 0) -> PointCloudRGB:
+        """pcl::VoxelGrid<PointXYZRGB>::filter (Filter::downsampleCloud) -> a new cloud."""
+        from .cloud import POINT_XYZRGB
+
+        leaf = np.broadcast_to(np.asarray(leaf, np.float64), (3,)).copy()
+        _, ptr, n, stride = self._cloud_arg(cloud)
+        out = PointCloudRGB(max(n, 1))
+        nout = ctypes.c_size_t()
+        self._check(self._lib.mgicp_voxel_grid(
+            self._h, ctypes.c_void_p(ptr), n, stride, int(POINT_XYZRGB.fields["rgb"][1]), _dp(leaf),
+            int(min_points_per_voxel), out.points.ctypes.data, POINT_XYZRGB.itemsize, ctypes.byref(nout)),
+            "voxel_grid")
+        out.points = out.points[:nout.value].copy()
+        return out
+
     # -- multi-GPU ------------------------------------------------------------------------
     @staticmethod
     def unique_id() -> bytes:

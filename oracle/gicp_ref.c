@@ -1521,3 +1521,165 @@ int ref_knn(const float* xyz, size_t n, size_t stride, const float* queries, siz
     free(pts);
     return REF_OK;
 }
+
+/* ------------------------------------------------------------------------------------ */
+/* The FOD-side callers either side of the GICP path          */
+/* ------------------------------------------------------------------------------------ */
+
+/* pcl::SegmentDifferences<PointXYZRGB>::segment -> pcl::getPointCloudDifference (PCL 1.8.1
+ * segmentation/impl/segment_differences.hpp), as called by Filter::removeFromCloud
+ * (src/Filter.cpp:176-189) with threshold = 4e-3 * voxelize_factor
+ * (src/LeicaStateMachine.cpp:186-187).  setDistanceThreshold stores the value compared
+ * against the SQUARED nearest-neighbour distance: input point i is kept iff it is finite and
+ * its float 1-NN d^2 in `sub` is > sqr_threshold.  An empty `sub` returns the input unchanged
+ * (every point kept, finite or not).  Non-finite `sub` points never enter the search tree
+ * (KdTreeFLANN::setInputCloud skips them). */
+int ref_segment_differences(const float* in, size_t n, size_t in_stride, const float* sub,
+                            size_t ns, size_t sub_stride, double sqr_threshold,
+                            unsigned char* keep, size_t* n_keep) {
+    if ((!in && n) || (!sub && ns) || (!keep && n) || !n_keep || in_stride < 12 || sub_stride < 12)
+        return REF_E_INVALID;
+    *n_keep = 0;
+    if (ns == 0) {
+        for (size_t i = 0; i < n; ++i) keep[i] = 1;
+        *n_keep = n;
+        return REF_OK;
+    }
+    float* pts = (float*)malloc(ns * 3 * sizeof(float));
+    size_t m = 0;
+    for (size_t j = 0; j < ns; ++j) {
+        const float* p = (const float*)((const char*)sub + j * sub_stride);
+        if (!isfinite(p[0]) || !isfinite(p[1]) || !isfinite(p[2])) continue;
+        pts[3 * m] = p[0]; pts[3 * m + 1] = p[1]; pts[3 * m + 2] = p[2];
+        ++m;
+    }
+    kdtree t;
+    kd_build(&t, pts, (int)m);
+    size_t cnt = 0;
+    for (size_t i = 0; i < n; ++i) {
+        const float* p = (const float*)((const char*)in + i * in_stride);
+        keep[i] = 0;
+        if (!isfinite(p[0]) || !isfinite(p[1]) || !isfinite(p[2])) continue;
+        if (m == 0) continue; /* nearestKSearch finds nothing: PCL warns and skips the point */
+        int j;
+        float d2;
+        kd_knn(&t, p, 1, &j, &d2);
+        if ((double)d2 > sqr_threshold) {
+            keep[i] = 1;
+            ++cnt;
+        }
+    }
+    kd_free(&t);
+    free(pts);
+    *n_keep = cnt;
+    return REF_OK;
+}
+
+typedef struct { uint32_t idx, pt; } vg_entry;
+static int vg_cmp(const void* a, const void* b) {
+    const vg_entry* x = (const vg_entry*)a;
+    const vg_entry* y = (const vg_entry*)b;
+    if (x->idx != y->idx) return x->idx < y->idx ? -1 : 1;
+    return x->pt < y->pt ? -1 : (x->pt > y->pt ? 1 : 0);
+}
+
+/* pcl::VoxelGrid<PointXYZRGB>::applyFilter (PCL 1.8.1 filters/impl/voxel_grid.hpp) with the
+ * defaults Filter::downsampleCloud uses (src/Filter.cpp:91-105): no filter field,
+ * downsample_all_data = true (CentroidPoint: xyz summed in fp32 and divided by float(n);
+ * r, g, b, a summed as floats and truncated after the division), min_points_per_voxel as given.
+ *   inverse_leaf = 1.0f / leaf (float);  min_b = (int)floor(min_p * inv);  div = max_b - min_b + 1;
+ *   ijk = (int)(floor(p * inv) - (float)min_b);  idx = i + j div_x + k div_x div_y;
+ *   points sorted by idx; output = one centroid per voxel in ascending idx.
+ * PCL sorts with std::sort (not stable), so the fp32 summation order inside a voxel is
+ * unspecified there; this restatement sums in ascending input index (the engine does the
+ * same, so the two agree bit for bit; against PCL itself centroids agree to fp32 rounding).
+ * Non-finite points are skipped (is_dense = false path).  Returns REF_OK with *overflow = 1
+ * and the input copied when div_x*div_y*div_z exceeds INT32_MAX (PCL's "leaf size too small"
+ * path: output = input).  out_xyz: 3 * n floats; out_rgba (optional): n uint32. */
+int ref_voxel_grid(const float* in, size_t n, size_t stride, int rgb_offset, const float leaf[3],
+                   int min_points, float* out_xyz, uint32_t* out_rgba, size_t* n_out, int* overflow) {
+    if ((!in && n) || !leaf || !n_out || !overflow || stride < 12 || (n && !out_xyz)) return REF_E_INVALID;
+    *n_out = 0;
+    *overflow = 0;
+    float inv[3];
+    for (int d = 0; d < 3; ++d) inv[d] = 1.0f / leaf[d];
+    float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+    size_t nf = 0;
+    for (size_t i = 0; i < n; ++i) {
+        const float* p = (const float*)((const char*)in + i * stride);
+        if (!isfinite(p[0]) || !isfinite(p[1]) || !isfinite(p[2])) continue;
+        for (int d = 0; d < 3; ++d) {
+            if (p[d] < mn[d]) mn[d] = p[d];
+            if (p[d] > mx[d]) mx[d] = p[d];
+        }
+        ++nf;
+    }
+    if (nf == 0) return REF_OK;
+    int64_t dd[3];
+    for (int d = 0; d < 3; ++d) dd[d] = (int64_t)((mx[d] - mn[d]) * inv[d]) + 1;
+    if (dd[0] * dd[1] * dd[2] > (int64_t)INT32_MAX) {
+        *overflow = 1;
+        for (size_t i = 0; i < n; ++i) {
+            const char* rec = (const char*)in + i * stride;
+            memcpy(out_xyz + 3 * i, rec, 3 * sizeof(float));
+            if (out_rgba && rgb_offset >= 0) memcpy(out_rgba + i, rec + rgb_offset, sizeof(uint32_t));
+        }
+        *n_out = n;
+        return REF_OK;
+    }
+    int min_b[3], max_b[3], div_b[3];
+    for (int d = 0; d < 3; ++d) {
+        min_b[d] = (int)floorf(mn[d] * inv[d]);
+        max_b[d] = (int)floorf(mx[d] * inv[d]);
+        div_b[d] = max_b[d] - min_b[d] + 1;
+    }
+    const int mul[3] = {1, div_b[0], div_b[0] * div_b[1]};
+    vg_entry* iv = (vg_entry*)malloc((nf ? nf : 1) * sizeof(vg_entry));
+    size_t k = 0;
+    for (size_t i = 0; i < n; ++i) {
+        const float* p = (const float*)((const char*)in + i * stride);
+        if (!isfinite(p[0]) || !isfinite(p[1]) || !isfinite(p[2])) continue;
+        int idx = 0;
+        for (int d = 0; d < 3; ++d) {
+            int ijk = (int)(floorf(p[d] * inv[d]) - (float)min_b[d]);
+            idx += ijk * mul[d];
+        }
+        iv[k].idx = (uint32_t)idx;
+        iv[k].pt = (uint32_t)i;
+        ++k;
+    }
+    qsort(iv, k, sizeof(vg_entry), vg_cmp);
+    size_t out = 0;
+    for (size_t a = 0; a < k;) {
+        size_t b = a + 1;
+        while (b < k && iv[b].idx == iv[a].idx) ++b;
+        if (b - a >= (size_t)(min_points > 0 ? min_points : 0)) {
+            float sx = 0.f, sy = 0.f, sz = 0.f, r = 0.f, g = 0.f, bl = 0.f, al = 0.f;
+            for (size_t l = a; l < b; ++l) {
+                const char* rec = (const char*)in + (size_t)iv[l].pt * stride;
+                const float* p = (const float*)rec;
+                sx += p[0]; sy += p[1]; sz += p[2];
+                if (rgb_offset >= 0) {
+                    uint32_t c;
+                    memcpy(&c, rec + rgb_offset, sizeof(c));
+                    bl += (float)(c & 0xffu);
+                    g += (float)((c >> 8) & 0xffu);
+                    r += (float)((c >> 16) & 0xffu);
+                    al += (float)(c >> 24);
+                }
+            }
+            const float cnt = (float)(b - a);
+            out_xyz[3 * out] = sx / cnt;
+            out_xyz[3 * out + 1] = sy / cnt;
+            out_xyz[3 * out + 2] = sz / cnt;
+            if (out_rgba && rgb_offset >= 0)
+                out_rgba[out] = ((uint32_t)(al / cnt) << 24) | ((uint32_t)(r / cnt) << 16) |
+                                ((uint32_t)(g / cnt) << 8) | (uint32_t)(bl / cnt);
+            ++out;
+        }
+        a = b;
+    }
+    free(iv);
+    *n_out = out;
+    return REF_OK;
+}

@@ -20,6 +20,7 @@
 #define GICP_REF_H
 
 #include <stddef.h>
+#include <stdint.h>
 
 #ifdef __cplusplus
 extern "C" {
@@ -97,6 +98,13 @@ int ref_fdf(ref_gicp* g, const double x[6], double* f, double g6[6]);
 int ref_fdf_sums(ref_gicp* g, const double x[6], int c0, int c1, double out14[14]);
 /* applyState(I, x): column-major float 4x4. */
 void ref_apply_state(const double x[6], float out_cm[16]);
+
+/* FOD-side callers around the GICP path; see gicp_ref.c */
+int ref_segment_differences(const float* in, size_t n, size_t in_stride, const float* sub,
+                            size_t ns, size_t sub_stride, double sqr_threshold,
+                            unsigned char* keep, size_t* n_keep);
+int ref_voxel_grid(const float* in, size_t n, size_t stride, int rgb_offset, const float leaf[3],
+                   int min_points, float* out_xyz, uint32_t* out_rgba, size_t* n_out, int* overflow);
 
 #ifdef __cplusplus
 }

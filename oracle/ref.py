@@ -77,6 +77,9 @@ def load():
         "ref_moments_range": (ctypes.c_int, [P, FP, ctypes.c_int, ctypes.c_int, DP]),
         "ref_fdf_sums": (ctypes.c_int, [P, DP, ctypes.c_int, ctypes.c_int, DP]),
         "ref_apply_state": (None, [DP, FP]),
+        "ref_segment_differences": (ctypes.c_int, [P, sz, sz, P, sz, sz, ctypes.c_double, P, ctypes.POINTER(sz)]),
+        "ref_voxel_grid": (ctypes.c_int, [P, sz, sz, ctypes.c_int, FP, ctypes.c_int, FP, P, ctypes.POINTER(sz),
+                                          ctypes.POINTER(ctypes.c_int)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -231,3 +234,43 @@ def apply_state(x) -> np.ndarray:
     out = np.zeros(16, np.float32)
     lib.ref_apply_state(_dp(x), _fp(out))
     return from_cm(out)
+
+
+def _records(a):
+    """(owner, pointer, n, stride) of an (n, 3) xyz array or an n-record structured array."""
+    a = np.ascontiguousarray(a)
+    if a.dtype.names:
+        return a, a.ctypes.data, len(a), a.dtype.itemsize
+    a = np.ascontiguousarray(a, dtype=np.float32).reshape(-1, 3)
+    return a, a.ctypes.data, len(a), 12
+
+
+def segment_differences(cloud_in, cloud_sub, sqr_threshold):
+    """pcl::getPointCloudDifference restatement: (keep mask, kept count)."""
+    lib = load()
+    a, pa, n, sa = _records(cloud_in)
+    b, pb, ns, sb = _records(cloud_sub)
+    keep = np.zeros(max(n, 1), np.uint8)
+    cnt = ctypes.c_size_t()
+    rc = lib.ref_segment_differences(pa, n, sa, pb, ns, sb, float(sqr_threshold), keep.ctypes.data, ctypes.byref(cnt))
+    assert rc == 0
+    return keep[:n].astype(bool), int(cnt.value)
+
+
+def voxel_grid(records, leaf, min_points=0, rgb_offset=16):
+    """pcl::VoxelGrid<PointXYZRGB> restatement over an n-record array (rgb word at rgb_offset,
+    -1 for none): (xyz (m, 3) float32, rgba (m,) uint32, overflow flag)."""
+    lib = load()
+    a, pa, n, stride = _records(records)
+    if not a.dtype.names:
+        rgb_offset = -1
+    leaf = np.broadcast_to(np.asarray(leaf, np.float32), (3,)).copy()
+    xyz = np.zeros((max(n, 1), 3), np.float32)
+    rgba = np.zeros(max(n, 1), np.uint32)
+    nout = ctypes.c_size_t()
+    ovf = ctypes.c_int()
+    rc = lib.ref_voxel_grid(pa, n, stride, rgb_offset, _fp(leaf), int(min_points), _fp(xyz), rgba.ctypes.data,
+                            ctypes.byref(nout), ctypes.byref(ovf))
+    assert rc == 0
+    m = nout.value
+    return xyz[:m].copy(), rgba[:m].copy(), bool(ovf.value)
