@@ -198,7 +198,7 @@ def test_voxel_grid_gpu_overflow_and_filter_class(eng):
     np.testing.assert_array_equal(out.points["rgb"], c.points["rgb"])
     # Filter::downsampleCloud / removeFromCloud drive the same kernels
     c = _rgb_cloud(20000)
-    f = Filter(0.012)
+    f = Filter(0.1)
     d = PointCloudRGB()
     f.downsampleCloud(c, d)
     assert 0 < len(d) < len(c)
