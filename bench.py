@@ -63,6 +63,8 @@ def parse():
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01_pmc_fdf.json"))
     ap.add_argument("--gn-steps", type=int, default=5,
                     help="timed aligns of the opt-in Gauss-Newton mode (MGICP_SOLVER_GN; 0 = skip)")
+    ap.add_argument("--fod-cpu-sample", type=int, default=500_000,
+                    help="points of the CPU-oracle sample for the FOD-side rows (0 = skip those rows)")
     ap.add_argument("--no-events", action="store_true",
                     help="time the steps without per-launch HIP events (A/B of the event overhead)")
     args = ap.parse_args()
@@ -102,6 +104,58 @@ def cpu_baseline(n, threads, occlusion=0.0):
     T, info = g.align()
     rate = info["iterations"] / info["t_loop_s"]
     return rate, info, T, (scan, cad)
+
+
+def fod_rows(eng, scan, cad, T_final, n_cpu):
+    """SURVEY 8f rows 2 and 4 around the GICP path, at the config's size, host buffers in/out:
+    VoxelGrid of the scan with the state machine's leaf (10 x max resolution,
+    LeicaStateMachine.cpp:61-65) and SegmentDifferences of the GICP-transformed scan against the
+    CAD cloud with the launch file's threshold (4e-3 * voxelize_factor 0.1,
+    LeicaStateMachine.cpp:184-188); CPU oracle timed on a bounded sample of each."""
+    from leica_point_cloud_processing_amd.cloud import PointCloudRGB
+    from oracle import ref
+
+    rows = {}
+    cloud = PointCloudRGB.from_xyz(scan, rgb=0xff808080)
+    t = time.perf_counter()
+    res = max(eng.cloud_resolution(scan), eng.cloud_resolution(cad))
+    ms_res = 1e3 * (time.perf_counter() - t) / 2
+    leaf = float(np.float32(10 * res))
+    ms = []
+    for _ in range(3):
+        t = time.perf_counter()
+        out = eng.voxel_grid(cloud, leaf)
+        ms.append(1e3 * (time.perf_counter() - t))
+    vg = {"ms": round(min(ms), 3), "points": len(scan), "leaf_m": leaf, "voxels": len(out),
+          "Mpts_per_s": round(len(scan) / min(ms) / 1e3, 1),
+          "note": "wall time from host records (32 B/pt) to host records, incl. PCIe both ways"}
+    thr = 4e-3 * 0.1
+    ms = []
+    for _ in range(3):
+        t = time.perf_counter()
+        keep, cnt = eng.segment_differences(scan, cad, thr, T=T_final)
+        ms.append(1e3 * (time.perf_counter() - t))
+    sd = {"ms": round(min(ms), 3), "points": len(scan), "target_points": len(cad), "sqr_threshold": thr,
+          "kept": cnt, "Mpts_per_s": round(len(scan) / min(ms) / 1e3, 1),
+          "note": "wall time incl. H2D of both clouds, target grid build and the keep-mask D2H"}
+    if n_cpu > 0:
+        n_cpu = min(n_cpu, len(scan))
+        sub = cloud.points[:n_cpu]
+        t = time.perf_counter()
+        ref.voxel_grid(sub, leaf)
+        vg["cpu_baseline"] = {"ms": round(1e3 * (time.perf_counter() - t), 3), "points": n_cpu, "cores": 1,
+                              "kind": "port", "Mpts_per_s": round(n_cpu / (time.perf_counter() - t) / 1e6, 2)}
+        moved = (scan[:n_cpu] @ T_final[:3, :3].T + T_final[:3, 3]).astype(np.float32)
+        csub = cad[: max(1, n_cpu * len(cad) // len(scan))]
+        t = time.perf_counter()
+        ref.segment_differences(moved, csub, thr)
+        dt = time.perf_counter() - t
+        sd["cpu_baseline"] = {"ms": round(1e3 * dt, 3), "points": n_cpu, "target_points": len(csub), "cores": 1,
+                              "kind": "port", "Mpts_per_s": round(n_cpu / dt / 1e6, 2)}
+    rows["voxel_grid"] = vg
+    rows["segment_differences"] = sd
+    rows["cloud_resolution_ms"] = round(ms_res, 3)
+    return rows
 
 
 def main():
@@ -254,6 +308,7 @@ def main():
         "reduce_finish": kt["reduce_finish"],
     }
 
+    fod = fod_rows(eng, scan, cad, T_final, args.fod_cpu_sample) if args.fod_cpu_sample > 0 and world == 1 else None
     cpu = None
     frob_sample = None
     if args.cpu_sample > 0:
@@ -327,6 +382,7 @@ def main():
         "kernels": kernels,
         "cpu_baseline": cpu,
         "gn_mode": gn,
+        "fod_rows": fod,
         "data_gen_s": round(t_gen, 2),
         "grid_occupancy": float(os.environ.get("MGICP_GRID_OCC", "0") or 0) or None,
     }

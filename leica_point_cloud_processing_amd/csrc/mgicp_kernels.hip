@@ -835,16 +835,18 @@ __global__ __launch_bounds__(256) void gn_moments_kernel(
   block_reduce_store_n<kMomVals>(acc, partial + static_cast<size_t>(blockIdx.x) * kMomVals);
 }
 
+// one block per moment: block v sums column v of the nb block partials (thread-strided, then a
+// fixed shuffle / LDS tree: deterministic)
 __global__ __launch_bounds__(256) void reduce_finish_moments_kernel(const double* __restrict__ partial,
                                                                     int nb, double* __restrict__ out) {
-  double acc[kMomVals];
-#pragma unroll
-  for (int v = 0; v < kMomVals; ++v) acc[v] = 0.0;
-  for (int b = threadIdx.x; b < nb; b += blockDim.x) {
-#pragma unroll
-    for (int v = 0; v < kMomVals; ++v) acc[v] += partial[static_cast<size_t>(b) * kMomVals + v];
-  }
-  block_reduce_store_n<kMomVals>(acc, out);
+  const int v = blockIdx.x;
+  double acc = 0.0;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) acc += partial[static_cast<size_t>(b) * kMomVals + v];
+  double one[1] = {acc};
+  __shared__ double res[1];
+  block_reduce_store_n<1>(one, res);
+  __syncthreads();
+  if (threadIdx.x == 0) out[v] = res[0];
 }
 
 __global__ __launch_bounds__(256) void fitness_kernel(GridView tg, const float4* __restrict__ src,
@@ -1183,7 +1185,7 @@ hipError_t launch_gn_moments(const float4* src, const float4* tpts, const Cov3& 
 }
 
 hipError_t launch_reduce_finish_moments(const double* partial, int nb, double* out, hipStream_t s) {
-  reduce_finish_moments_kernel<<<1, 256, 0, s>>>(partial, nb, out);
+  reduce_finish_moments_kernel<<<kMomVals, 256, 0, s>>>(partial, nb, out);
   return hipGetLastError();
 }
 

@@ -48,7 +48,8 @@ def main():
     }
     # the other kernels of the path, for DESIGN.md (same correction; gathers use 16 B/lane loads)
     others = {}
-    for k in ("correspond_kernel", "compact_kernel", "knn_cov_kernel", "xform_points", "fitness_kernel"):
+    for k in ("correspond_kernel", "compact_kernel", "knn_cov_kernel", "xform_points", "fitness_kernel",
+              "gn_moments_kernel", "segdiff_kernel", "voxel_key_kernel", "voxel_centroid_kernel"):
         fk, wk = per_dispatch(fdir, "FETCH_SIZE", k), per_dispatch(wdir, "WRITE_SIZE", k)
         if fk and wk:
             others[k] = {"dispatches": len(fk),
