@@ -732,6 +732,16 @@ int correspond(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
                             ctx->prev_pos.p, ctx->flags.p, s));
   }
   ctx->seed_valid = true;
+#if MGICP_CORR_STATS
+  {
+    unsigned long long st[8];
+    HIPCK(hipStreamSynchronize(s));
+    HIPCK(corr_stats_take(st));
+    std::fprintf(stderr, "[corr-stats] queries %llu accepted %llu rejected %llu | tests/query acc %.1f rej %.1f | ranges/query acc %.1f rej %.1f\n",
+                 st[0], st[1], st[2], st[1] ? double(st[3]) / st[1] : 0.0, st[2] ? double(st[4]) / st[2] : 0.0,
+                 st[1] ? double(st[5]) / st[1] : 0.0, st[2] ? double(st[6]) / st[2] : 0.0);
+  }
+#endif
   const size_t sb = scan_scratch_bytes(ns + 1);
   HIPCK(launch_exclusive_scan(ctx->cscratch.p, sb, ctx->flags.p, ctx->cpos.p, ns + 1, s));
   {

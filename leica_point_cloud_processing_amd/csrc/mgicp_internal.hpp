@@ -126,6 +126,10 @@ hipError_t launch_voxel_minpts(const float4* vox, const uint32_t* vox_rgba, size
                                uint32_t* flags, uint32_t* pos, void* scratch, size_t scratch_bytes,
                                float4* out, uint32_t* out_rgba, hipStream_t s);
 
+#if defined(MGICP_CORR_STATS) && MGICP_CORR_STATS
+hipError_t corr_stats_take(unsigned long long out[8]);  // diagnostic builds: read and reset
+#endif
+
 // radix sort / scan scratch (hipcub)
 size_t sort_scratch_bytes(size_t n, int bits);
 hipError_t launch_sort_pairs(void* scratch, size_t scratch_bytes, const uint32_t* keys_in,

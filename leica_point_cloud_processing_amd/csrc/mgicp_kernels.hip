@@ -21,6 +21,9 @@
 #ifndef MGICP_CORR_WAVES
 #define MGICP_CORR_WAVES 1  // minimum resident waves per SIMD requested for the 1-NN kernel
 #endif
+#ifndef MGICP_CORR_STATS
+#define MGICP_CORR_STATS 0  // 1: count 1-NN work per sweep (diagnostic builds only)
+#endif
 
 #include "mgicp_internal.hpp"
 
@@ -201,6 +204,12 @@ struct KnnVisitor {
   }
 };
 
+#if MGICP_CORR_STATS
+// [0] queries [1] accepted [2] rejected [3] candidates tested (accepted) [4] (rejected)
+// [5] cell ranges scanned (accepted) [6] (rejected)
+__device__ unsigned long long g_corr_stats[8];
+#endif
+
 // exact 1-NN visitor, optionally bounded by an acceptance threshold thr on d2
 struct NnVisitor {
   float qx, qy, qz;
@@ -208,6 +217,9 @@ struct NnVisitor {
   float thr_f;  // float upper bound of thr (pruning radius cap)
   unsigned long long best;
   uint32_t pos;
+#if MGICP_CORR_STATS
+  uint32_t ntest = 0, nrange = 0, nring = 0;
+#endif
 
   __device__ __forceinline__ void init(float x, float y, float z, double t) {
     qx = x; qy = y; qz = z; thr = t; best = ~0ull; pos = 0u;
@@ -229,6 +241,10 @@ struct NnVisitor {
   }
   __device__ __forceinline__ void range(const GridView& g, uint32_t a, uint32_t b) {
     uint32_t j = a;
+#if MGICP_CORR_STATS
+    ntest += b - a;
+    nrange += 1;
+#endif
 #if MGICP_NN_UNROLL >= 8
     for (; j + 8 <= b; j += 8) {  // eight gathers in flight per lane (latency-bound loop)
       float4 p[8];
@@ -524,7 +540,22 @@ __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_kernel(GridV
                   static_cast<double>(__uint_as_float(static_cast<uint32_t>(vis.best >> 32))) < thr;
   nn_pos[p - p0] = ok ? vis.pos : 0xffffffffu;
   flags[p - p0] = ok ? 1u : 0u;
+#if MGICP_CORR_STATS
+  atomicAdd(&g_corr_stats[0], 1ull);
+  atomicAdd(&g_corr_stats[ok ? 1 : 2], 1ull);
+  atomicAdd(&g_corr_stats[ok ? 3 : 4], static_cast<unsigned long long>(vis.ntest));
+  atomicAdd(&g_corr_stats[ok ? 5 : 6], static_cast<unsigned long long>(vis.nrange));
+#endif
 }
+
+#if MGICP_CORR_STATS
+hipError_t corr_stats_take(unsigned long long out[8]) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_corr_stats), 8 * sizeof(unsigned long long));
+  unsigned long long z[8] = {};
+  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_corr_stats), z, sizeof(z));
+  return e;
+}
+#endif
 
 // M = (R Cs R' + Ct)^-1 in fp64 with Eigen's 3x3 cofactor inverse (gicp.hpp
 // computeTransformation): the upper triangle {m00, m01, m02, m11, m12, m22}.
