@@ -149,7 +149,10 @@ int mgicp_voxel_grid(mgicp_ctx* ctx, const float* in, size_t n, size_t stride, i
 /* ---- multi-GPU: one process per GPU, point-range shards of the source cloud ----
  * Rank 0 calls mgicp_get_unique_id and broadcasts the 128 bytes out of band (bench.py uses
  * the TCP rendezvous of leica_point_cloud_processing_amd/parallel.py); every rank then calls
- * mgicp_comm_init before set_* / align.  Every objective pass then all-reduces 16 doubles. */
+ * mgicp_comm_init before set_* / align.  Every objective pass then all-reduces 16 doubles (GN
+ * mode: every outer iteration all-reduces the 80 moment doubles).  nranks = 1 with an id builds a
+ * one-rank communicator (the collective path on a single device); id = NULL makes a "detached"
+ * shard for the debug entry points. */
 int mgicp_get_unique_id(unsigned char id[128]);
 int mgicp_comm_init(mgicp_ctx* ctx, int nranks, int rank, const unsigned char id[128]);
 

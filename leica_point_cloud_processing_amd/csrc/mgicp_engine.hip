@@ -792,21 +792,26 @@ struct DeviceFunctor {
     const int reverse = ctx->alt_sweep ? (ctx->n_evals & 1) : 0;
     if (ctx->fused_finish) {
       // the last block writes the sums straight into mapped pinned host memory (single GPU)
-      // or device memory (multi-GPU: then one 16-double RCCL all-reduce and a D2H copy)
+      // or device memory (multi-GPU: then one 16-double RCCL all-reduce, and a one-wave kernel
+      // publishes the reduced sums plus the completion word into mapped host memory)
       double* out = ctx->comm ? ctx->red.p : ctx->d_h_red;
-      const bool poll = ctx->poll && !ctx->comm;
+      const bool poll = ctx->poll;
       const unsigned long long seq = ++ctx->pass_seq;
       {
         ProfScope ps(ctx, kFamFdf);
         HIPCK(launch_fdf_soa(corr_soa(ctx), ctx->m_local, A.xf(), ctx->partial.p, nb,
-                             ctx->ticket.p, out, reverse, poll ? ctx->d_flag : nullptr, seq,
-                             ctx->stream));
+                             ctx->ticket.p, out, reverse,
+                             (poll && !ctx->comm) ? ctx->d_flag : nullptr, seq, ctx->stream));
       }
       if (ctx->comm) {
         NCCLCK(ncclAllReduce(ctx->red.p, ctx->red.p, kRedVals, ncclDouble, ncclSum, ctx->comm,
                              ctx->stream));
-        HIPCK(hipMemcpyAsync(ctx->h_red, ctx->red.p, kRedVals * sizeof(double),
-                             hipMemcpyDeviceToHost, ctx->stream));
+        if (poll) {
+          HIPCK(launch_publish(ctx->red.p, kRedVals, ctx->d_h_red, ctx->d_flag, seq, ctx->stream));
+        } else {
+          HIPCK(hipMemcpyAsync(ctx->h_red, ctx->red.p, kRedVals * sizeof(double),
+                               hipMemcpyDeviceToHost, ctx->stream));
+        }
       }
       rc = poll ? wait_pass(ctx, seq) : sync(ctx);
     } else {
@@ -1506,7 +1511,9 @@ int mgicp_comm_init(mgicp_ctx* ctx, int nranks, int rank, const unsigned char id
   ctx->rank = rank;
   ctx->src.have_cov = false;
   ctx->have_corr = false;
-  if (nranks == 1 || !id) return MGICP_OK;  // id == NULL: detached shard (debug entry points only)
+  // id == NULL: detached shard (debug entry points only).  nranks == 1 with an id builds a real
+  // one-rank communicator, so the collective code path can be exercised on a single device.
+  if (!id) return MGICP_OK;
   ncclUniqueId uid;
   std::memcpy(&uid, id, 128);
   NCCLCK(ncclCommInitRank(&ctx->comm, nranks, uid, rank));

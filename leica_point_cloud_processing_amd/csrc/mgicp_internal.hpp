@@ -99,6 +99,9 @@ hipError_t launch_gn_moments(const float4* src, const float4* tpts, const Cov3& 
                              const uint32_t* nn_pos, const uint32_t* flags, size_t p0, size_t p1,
                              double* partial, int nb, hipStream_t s);
 hipError_t launch_reduce_finish_moments(const double* partial, int nb, double* out, hipStream_t s);
+// n (<= 64) doubles -> mapped host memory, then seq -> the host-polled completion word
+hipError_t launch_publish(const double* in, int n, double* host_out, unsigned long long* flag,
+                          unsigned long long seq, hipStream_t s);
 hipError_t launch_fitness(const GridView& tgt, const float4* src, size_t p0, size_t p1,
                           Xf34 T, double max_range, double* partial, int nb, hipStream_t s);
 hipError_t launch_reduce_finish(const double* partial, int nb, double* out, hipStream_t s);

@@ -880,6 +880,16 @@ __global__ __launch_bounds__(256) void reduce_finish_moments_kernel(const double
   if (threadIdx.x == 0) out[v] = res[0];
 }
 
+// n doubles of device memory -> mapped host memory, then `seq` into the host-polled completion
+// word with a system-scope release (multi-GPU passes: runs after the RCCL all-reduce)
+__global__ void publish_kernel(const double* __restrict__ in, int n, double* out,
+                               unsigned long long* flag, unsigned long long seq) {
+  if (threadIdx.x < n) out[threadIdx.x] = in[threadIdx.x];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ __launch_bounds__(256) void fitness_kernel(GridView tg, const float4* __restrict__ src,
                                                       size_t p0, size_t p1, Xf34 T,
                                                       double max_range,
@@ -1200,6 +1210,12 @@ hipError_t launch_fdf_soa(const CorrSoA& c, size_t m, Xf34 A, double* partial, i
   return hipGetLastError();
 }
 
+hipError_t launch_publish(const double* in, int n, double* host_out, unsigned long long* flag,
+                          unsigned long long seq, hipStream_t s) {
+  publish_kernel<<<1, 64, 0, s>>>(in, n, host_out, flag, seq);
+  return hipGetLastError();
+}
+
 int gn_grid_blocks(size_t n) {
   // ~16 source points per thread, at most 1024 blocks (the finish reads nb x 80 doubles)
   const size_t want = (n + 256 * 16 - 1) / (256 * 16);
@@ -1354,6 +1370,7 @@ hipError_t preload_kernels(void* pinned, size_t pinned_bytes, hipStream_t s) {
       reinterpret_cast<const void*>(&radius_keep_kernel),
       reinterpret_cast<const void*>(&reduce_finish_kernel),
       reinterpret_cast<const void*>(&gn_moments_kernel),
+      reinterpret_cast<const void*>(&publish_kernel),
       reinterpret_cast<const void*>(&reduce_finish_moments_kernel),
       reinterpret_cast<const void*>(&finite_flags_kernel),
       reinterpret_cast<const void*>(&scatter_flagged_kernel),
