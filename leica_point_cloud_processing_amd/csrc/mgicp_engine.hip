@@ -209,6 +209,7 @@ struct Cloud {
   DevBuf<uint8_t> empty_dist; // empty-space map (target only: 1-NN queries leave the surface)
   bool want_empty_map = false;
   bool drop_nonfinite = false; // build the grid over the finite points only (KdTreeFLANN semantics)
+  double occupancy = 0;        // grid sizing target (points per non-empty cell); 0 = context default
   DevBuf<double2> cov;        // 3 * n
   float lo[3] = {0.f, 0.f, 0.f}, hi[3] = {0.f, 0.f, 0.f};  // bounding box (original coordinates)
   GridView view{};
@@ -258,6 +259,10 @@ struct mgicp_ctx {
   size_t corr_cap = 0;     // elements per stream (multiple of 4)
   size_t m_local = 0;      // accepted correspondences of this rank
   bool seed_valid = false;
+  // query order of the 1-NN sweeps (Morton order of the shard; env MGICP_QUERY_ORDER)
+  bool query_order = true;
+  bool qperm_valid = false;
+  DevBuf<uint32_t> qperm;
   DevBuf<double> partial;
   DevBuf<double> red;      // kRedVals
   // Gauss-Newton mode: block partials / finished moments of one pass, and their host copy
@@ -399,6 +404,7 @@ int upload_cloud(mgicp_ctx* ctx, Cloud& cl, const float* xyz, size_t n, size_t s
   cl.n = n;
   cl.dirty = true;
   cl.have_cov = false;
+  if (&cl == &ctx->src) ctx->qperm_valid = false;
   if (&cl == &ctx->src || &cl == &ctx->tgt) {
     ctx->have_corr = false;
     ctx->ms_upload_pending += now_ms() - t0;
@@ -461,7 +467,8 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
     maxext = std::max(maxext, ext[d]);
     maxabs = std::max(maxabs, std::max(std::fabs(mn[d]), std::fabs(mx[d])));
   }
-  // 2. cell size: aim at ctx->occupancy points per non-empty cell
+  // 2. cell size: aim at `target_occ` points per non-empty cell
+  const double target_occ = cl.occupancy > 0 ? cl.occupancy : ctx->occupancy;
   auto dims = [&](double h, int* nd) {
     size_t nc = 1;
     for (int d = 0; d < 3; ++d) {
@@ -497,9 +504,9 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
     std::memcpy(&nonempty, ctx->h_small, sizeof(nonempty));
     MGICP_TRACE_AT("grid: sizing histogram synced");
     const double occ = static_cast<double>(n) / std::max<unsigned long long>(nonempty, 1);
-    if ((occ > 0.6 * ctx->occupancy && occ < 1.6 * ctx->occupancy) || nc >= kMaxCells / 2)
+    if ((occ > 0.6 * target_occ && occ < 1.6 * target_occ) || nc >= kMaxCells / 2)
       break;
-    if (nonempty <= 1 && occ < ctx->occupancy) break;  // everything in one cell already
+    if (nonempty <= 1 && occ < target_occ) break;  // everything in one cell already
     double dim = 2.0;
     if (h_prev > 0 && occ_prev > 0 && std::fabs(std::log(h / h_prev)) > 1e-3) {
       dim = std::log(occ / occ_prev) / std::log(h / h_prev);
@@ -507,7 +514,7 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
     }
     h_prev = h;
     occ_prev = occ;
-    h = h * std::pow(ctx->occupancy / occ, 1.0 / dim);
+    h = h * std::pow(target_occ / occ, 1.0 / dim);
     h = std::max(h, 1e-6);
   }
   size_t nc = dims(h, nd);
@@ -715,6 +722,31 @@ CorrSoA corr_soa(mgicp_ctx* ctx) {
                  d, d + c, d + 2 * c, d + 3 * c, d + 4 * c, d + 5 * c};
 }
 
+// Query order of the shard's 1-NN sweeps: a stable sort of 30-bit Morton codes (built once per
+// source cloud and shard; the sweeps' results stay indexed by grid-sorted position)
+const uint32_t* query_perm(mgicp_ctx* ctx) {
+  if (!ctx->query_order) return nullptr;
+  if (ctx->qperm_valid) return ctx->qperm.p;
+  const size_t p0 = ctx->shard_p0(), ns = ctx->shard_p1() - p0;
+  if (ns == 0) return nullptr;
+  hipStream_t s = ctx->stream;
+  const Cloud& c = ctx->src;
+  float ext = 0.f;
+  for (int d = 0; d < 3; ++d) ext = std::max(ext, c.hi[d] - c.lo[d]);
+  const float inv = ext > 0.f ? 1024.0f / (ext * 1.0001f) : 0.f;
+  if (ctx->qperm.reserve(ns) != hipSuccess || ctx->keys.reserve(ns) != hipSuccess ||
+      ctx->keys_sorted.reserve(ns) != hipSuccess || ctx->vals.reserve(ns) != hipSuccess)
+    return nullptr;
+  const size_t sb = sort_scratch_bytes(ns, 30);
+  if (ctx->scratch.reserve(sb) != hipSuccess) return nullptr;
+  if (launch_morton_keys(c.pts.p, p0, ns, c.lo, inv, ctx->keys.p, ctx->vals.p, s) != hipSuccess ||
+      launch_sort_pairs(ctx->scratch.p, sb, ctx->keys.p, ctx->keys_sorted.p, ctx->vals.p, ctx->qperm.p, ns,
+                        30, s) != hipSuccess)
+    return nullptr;
+  ctx->qperm_valid = true;
+  return ctx->qperm.p;
+}
+
 // One correspondence sweep (the loop body of computeTransformation before the BFGS call):
 // exact 1-NN per source point, then a deterministic compaction of the accepted ones (exclusive
 // scan of the flags, scatter in grid-sorted order) that computes their Mahalanobis matrices
@@ -726,10 +758,11 @@ int correspond(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
   hipStream_t s = ctx->stream;
   const bool seeded = seed && ctx->seed_valid;
   HIPCK(hipMemsetAsync(ctx->flags.p + ns, 0, sizeof(uint32_t), s));
+  const uint32_t* qp = query_perm(ctx);
   {
     ProfScope ps(ctx, kFamCorr);
     HIPCK(launch_correspond(ctx->tgt.view, ctx->d_out, p0, p1, T.xf(), thr, seeded ? 1 : 0,
-                            ctx->prev_pos.p, ctx->flags.p, s));
+                            ctx->prev_pos.p, ctx->flags.p, qp, s));
   }
   ctx->seed_valid = true;
 #if MGICP_CORR_STATS
@@ -938,10 +971,11 @@ int correspond_gn(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
   const double thr = ctx->prm.max_corr_dist * ctx->prm.max_corr_dist;
   const size_t p0 = ctx->shard_p0(), p1 = ctx->shard_p1();
   const bool seeded = seed && ctx->seed_valid;
+  const uint32_t* qp = query_perm(ctx);
   {
     ProfScope ps(ctx, kFamCorr);
     HIPCK(launch_correspond(ctx->tgt.view, ctx->d_out, p0, p1, T.xf(), thr, seeded ? 1 : 0,
-                            ctx->prev_pos.p, ctx->flags.p, ctx->stream));
+                            ctx->prev_pos.p, ctx->flags.p, qp, ctx->stream));
   }
   ctx->seed_valid = true;
   ctx->have_corr = false;  // the SoA streams of the BFGS mode are not refreshed
@@ -1019,6 +1053,11 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
   if (const char* ff = std::getenv("MGICP_FUSED_FINISH")) ctx->fused_finish = std::atoi(ff) != 0;
   if (const char* fa = std::getenv("MGICP_FDF_ALT")) ctx->alt_sweep = std::atoi(fa) != 0;
   if (const char* po = std::getenv("MGICP_POLL")) ctx->poll = std::atoi(po) != 0;
+  if (const char* qo = std::getenv("MGICP_QUERY_ORDER")) ctx->query_order = std::atoi(qo) != 0;
+  if (const char* so = std::getenv("MGICP_SRC_GRID_OCC")) {
+    const double v = std::atof(so);
+    if (v >= 1.0 && v <= 256.0) ctx->src.occupancy = v;
+  }
   {
     const unsigned hc = std::thread::hardware_concurrency();
     ctx->host_threads = static_cast<int>(std::max(1u, std::min(8u, hc ? hc : 1u)));
@@ -1102,6 +1141,7 @@ void mgicp_destroy(mgicp_ctx* ctx) {
     c->cell_start.release(); c->cov.release(); c->empty_dist.release();
   }
   ctx->src_out.release();
+  ctx->qperm.release();
   ctx->partial.release(); ctx->red.release(); ctx->mpartial.release(); ctx->mred.release(); ctx->counts.release(); ctx->keys.release();
   ctx->keys_sorted.release(); ctx->vals.release(); ctx->scratch.release(); ctx->u64.release();
   ctx->fpartial.release();
@@ -1509,6 +1549,7 @@ int mgicp_comm_init(mgicp_ctx* ctx, int nranks, int rank, const unsigned char id
   }
   ctx->nranks = nranks;
   ctx->rank = rank;
+  ctx->qperm_valid = false;
   ctx->src.have_cov = false;
   ctx->have_corr = false;
   // id == NULL: detached shard (debug entry points only).  nranks == 1 with an id builds a real

@@ -77,7 +77,10 @@ hipError_t launch_knn_cov(const GridView& g, int k, double eps, size_t p0, size_
 // rejected; with `seeded` its previous contents seed the exact 1-NN search.  flags: 1 if accepted.
 hipError_t launch_correspond(const GridView& tgt, const float4* src, size_t p0, size_t p1, Xf34 T,
                              double thr, int seeded, uint32_t* nn_pos, uint32_t* flags,
-                             hipStream_t s);
+                             const uint32_t* qperm /*nullable: query order*/, hipStream_t s);
+// Morton keys (30 bit, bbox lo, 1024 / extent = inv) of points [p0, p0 + n) and values 0..n-1
+hipError_t launch_morton_keys(const float4* pts, size_t p0, size_t n, const float lo[3], float inv,
+                              uint32_t* keys, uint32_t* vals, hipStream_t s);
 // accepted correspondences -> compacted slots (pos = exclusive scan of flags), computing the
 // Mahalanobis matrices on the way
 hipError_t launch_compact(const float4* src, const float4* tpts, const Cov3& cov_s,

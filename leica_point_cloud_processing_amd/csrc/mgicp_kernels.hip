@@ -518,12 +518,16 @@ __device__ __forceinline__ void load_cov(const Cov3& c, size_t i, double M[3][3]
 // Exact radius-gated 1-NN of T*s for every source point of the shard.  The search is
 // latency-bound on dependent candidate gathers, so this kernel does nothing else: it keeps a
 // small register footprint (occupancy) and leaves the fp64 Mahalanobis work to the compaction.
+// `qperm` (optional): the shard's query order -- thread t handles shard point qperm[t], a
+// Morton order of the source, so that a wave's queries form a compact 3-D patch.
 __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_kernel(GridView tg, const float4* __restrict__ src,
                                                          size_t p0, size_t p1, Xf34 T, double thr,
                                                          int seeded, uint32_t* __restrict__ nn_pos,
-                                                         uint32_t* __restrict__ flags) {
-  const size_t p = p0 + static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (p >= p1) return;
+                                                         uint32_t* __restrict__ flags,
+                                                         const uint32_t* __restrict__ qperm) {
+  const size_t t = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= p1 - p0) return;
+  const size_t p = p0 + (qperm ? qperm[t] : t);
   const float4 s = src[p];
   float qx, qy, qz;
   xform(T, s.x, s.y, s.z, qx, qy, qz);
@@ -556,6 +560,30 @@ hipError_t corr_stats_take(unsigned long long out[8]) {
   return e;
 }
 #endif
+
+// 10-bit spread for 3-D Morton codes
+__device__ __forceinline__ uint32_t spread3(uint32_t v) {
+  v &= 0x3ffu;
+  v = (v | (v << 16)) & 0x030000ffu;
+  v = (v | (v << 8)) & 0x0300f00fu;
+  v = (v | (v << 4)) & 0x030c30c3u;
+  v = (v | (v << 2)) & 0x09249249u;
+  return v;
+}
+
+// 30-bit Morton code of each shard point over the cloud's bbox (1024 steps per axis), value =
+// shard-relative position; a stable sort of (key, value) gives the query order of the 1-NN sweeps
+__global__ void morton_key_kernel(const float4* __restrict__ pts, size_t p0, size_t n, float ox, float oy,
+                                  float oz, float inv, uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+  const size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float4 q = pts[p0 + i];
+  const int ix = min(max(static_cast<int>((q.x - ox) * inv), 0), 1023);
+  const int iy = min(max(static_cast<int>((q.y - oy) * inv), 0), 1023);
+  const int iz = min(max(static_cast<int>((q.z - oz) * inv), 0), 1023);
+  keys[i] = spread3(ix) | (spread3(iy) << 1) | (spread3(iz) << 2);
+  vals[i] = static_cast<uint32_t>(i);
+}
 
 // M = (R Cs R' + Ct)^-1 in fp64 with Eigen's 3x3 cofactor inverse (gicp.hpp
 // computeTransformation): the upper triangle {m00, m01, m02, m11, m12, m22}.
@@ -1187,9 +1215,16 @@ hipError_t launch_knn_cov(const GridView& g, int k, double eps, size_t p0, size_
 
 hipError_t launch_correspond(const GridView& tgt, const float4* src, size_t p0, size_t p1, Xf34 T,
                              double thr, int seeded, uint32_t* nn_pos, uint32_t* flags,
-                             hipStream_t s) {
+                             const uint32_t* qperm, hipStream_t s) {
   if (p1 <= p0) return hipSuccess;
-  correspond_kernel<<<nblk(p1 - p0), 256, 0, s>>>(tgt, src, p0, p1, T, thr, seeded, nn_pos, flags);
+  correspond_kernel<<<nblk(p1 - p0), 256, 0, s>>>(tgt, src, p0, p1, T, thr, seeded, nn_pos, flags, qperm);
+  return hipGetLastError();
+}
+
+hipError_t launch_morton_keys(const float4* pts, size_t p0, size_t n, const float lo[3], float inv,
+                              uint32_t* keys, uint32_t* vals, hipStream_t s) {
+  if (!n) return hipSuccess;
+  morton_key_kernel<<<nblk(n), 256, 0, s>>>(pts, p0, n, lo[0], lo[1], lo[2], inv, keys, vals);
   return hipGetLastError();
 }
 
@@ -1363,6 +1398,7 @@ hipError_t preload_kernels(void* pinned, size_t pinned_bytes, hipStream_t s) {
       reinterpret_cast<const void*>(&knn_cov_kernel<25>),
       reinterpret_cast<const void*>(&knn_cov_kernel<30>),
       reinterpret_cast<const void*>(&correspond_kernel),
+      reinterpret_cast<const void*>(&morton_key_kernel),
       reinterpret_cast<const void*>(&compact_kernel),
       reinterpret_cast<const void*>(&fdf_soa_kernel),
       reinterpret_cast<const void*>(&fitness_kernel),
