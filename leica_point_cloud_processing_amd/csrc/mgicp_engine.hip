@@ -578,13 +578,44 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
   return MGICP_OK;
 }
 
+// Morton order of points [p0, p0 + n) of a grid-sorted cloud: a stable sort of 30-bit Morton codes
+// over the cloud's bbox.  Query order of the k-NN / 1-NN kernels (a wave's queries then form a
+// compact 3-D patch); results stay indexed by grid-sorted position.  false on failure.
+bool morton_perm(mgicp_ctx* ctx, const Cloud& c, size_t p0, size_t n, DevBuf<uint32_t>& out) {
+  hipStream_t s = ctx->stream;
+  float ext = 0.f;
+  for (int d = 0; d < 3; ++d) ext = std::max(ext, c.hi[d] - c.lo[d]);
+  const float inv = ext > 0.f ? 1024.0f / (ext * 1.0001f) : 0.f;
+  if (out.reserve(n) != hipSuccess || ctx->keys.reserve(n) != hipSuccess ||
+      ctx->keys_sorted.reserve(n) != hipSuccess || ctx->vals.reserve(n) != hipSuccess)
+    return false;
+  const size_t sb = sort_scratch_bytes(n, 30);
+  if (ctx->scratch.reserve(sb) != hipSuccess) return false;
+  return launch_morton_keys(c.pts.p, p0, n, c.lo, inv, ctx->keys.p, ctx->vals.p, s) == hipSuccess &&
+         launch_sort_pairs(ctx->scratch.p, sb, ctx->keys.p, ctx->keys_sorted.p, ctx->vals.p, out.p, n, 30,
+                           s) == hipSuccess;
+}
+
+// query order of the shard's 1-NN sweeps and source covariances (once per source cloud and shard)
+const uint32_t* query_perm(mgicp_ctx* ctx) {
+  if (!ctx->query_order) return nullptr;
+  if (ctx->qperm_valid) return ctx->qperm.p;
+  const size_t p0 = ctx->shard_p0(), ns = ctx->shard_p1() - p0;
+  if (ns == 0 || !morton_perm(ctx, ctx->src, p0, ns, ctx->qperm)) return nullptr;
+  ctx->qperm_valid = true;
+  return ctx->qperm.p;
+}
+
 int compute_cov(mgicp_ctx* ctx, Cloud& cl, size_t p0, size_t p1) {
   MGICP_TRACE_AT("cov: begin");
   HIPCK(cl.cov.reserve(3 * cl.n));
   MGICP_TRACE_AT("cov: reserved");
+  // grid order, not Morton order: the k = 20 queries sit on the surface and the row-major order
+  // measured faster (3.97 vs 4.42 ms at 5M, profiles/r01/ab_qorder/)
+  const uint32_t* perm = nullptr;
   {
     ProfScope ps(ctx, kFamCov);
-    HIPCK(launch_knn_cov(cl.view, ctx->prm.k, ctx->prm.gicp_eps, p0, p1, cl.cov3(), ctx->stream));
+    HIPCK(launch_knn_cov(cl.view, ctx->prm.k, ctx->prm.gicp_eps, p0, p1, cl.cov3(), perm, ctx->stream));
   }
   int rc = sync(ctx);
   if (rc) return rc;
@@ -720,31 +751,6 @@ CorrSoA corr_soa(mgicp_ctx* ctx) {
   double* d = ctx->corr_d.p;
   return CorrSoA{f, f + c, f + 2 * c, f + 3 * c, f + 4 * c, f + 5 * c,
                  d, d + c, d + 2 * c, d + 3 * c, d + 4 * c, d + 5 * c};
-}
-
-// Query order of the shard's 1-NN sweeps: a stable sort of 30-bit Morton codes (built once per
-// source cloud and shard; the sweeps' results stay indexed by grid-sorted position)
-const uint32_t* query_perm(mgicp_ctx* ctx) {
-  if (!ctx->query_order) return nullptr;
-  if (ctx->qperm_valid) return ctx->qperm.p;
-  const size_t p0 = ctx->shard_p0(), ns = ctx->shard_p1() - p0;
-  if (ns == 0) return nullptr;
-  hipStream_t s = ctx->stream;
-  const Cloud& c = ctx->src;
-  float ext = 0.f;
-  for (int d = 0; d < 3; ++d) ext = std::max(ext, c.hi[d] - c.lo[d]);
-  const float inv = ext > 0.f ? 1024.0f / (ext * 1.0001f) : 0.f;
-  if (ctx->qperm.reserve(ns) != hipSuccess || ctx->keys.reserve(ns) != hipSuccess ||
-      ctx->keys_sorted.reserve(ns) != hipSuccess || ctx->vals.reserve(ns) != hipSuccess)
-    return nullptr;
-  const size_t sb = sort_scratch_bytes(ns, 30);
-  if (ctx->scratch.reserve(sb) != hipSuccess) return nullptr;
-  if (launch_morton_keys(c.pts.p, p0, ns, c.lo, inv, ctx->keys.p, ctx->vals.p, s) != hipSuccess ||
-      launch_sort_pairs(ctx->scratch.p, sb, ctx->keys.p, ctx->keys_sorted.p, ctx->vals.p, ctx->qperm.p, ns,
-                        30, s) != hipSuccess)
-    return nullptr;
-  ctx->qperm_valid = true;
-  return ctx->qperm.p;
 }
 
 // One correspondence sweep (the loop body of computeTransformation before the BFGS call):

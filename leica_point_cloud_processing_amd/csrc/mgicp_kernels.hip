@@ -437,11 +437,14 @@ __device__ __forceinline__ double sel3(int i, double a, double b, double c) {
   return i == 0 ? a : (i == 1 ? b : c);
 }
 
+// `perm` (optional): query order over [p0, p1) (Morton order: compact 3-D patch per wave)
 template <int K>
 __global__ __launch_bounds__(256) void knn_cov_kernel(GridView g, double eps, size_t p0,
-                                                      size_t p1, Cov3 cov) {
-  const size_t p = p0 + static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (p >= p1) return;
+                                                      size_t p1, Cov3 cov,
+                                                      const uint32_t* __restrict__ perm) {
+  const size_t t = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= p1 - p0) return;
+  const size_t p = p0 + (perm ? perm[t] : t);
   const float4 q = g.pts[p];
   KnnVisitor<K> vis;
   vis.init(q.x, q.y, q.z);
@@ -1194,21 +1197,21 @@ hipError_t launch_iota(uint32_t* v, size_t n, hipStream_t s) {
 
 template <int K>
 static hipError_t knn_cov_k(const GridView& g, double eps, size_t p0, size_t p1, Cov3 cov,
-                            hipStream_t s) {
-  knn_cov_kernel<K><<<nblk(p1 - p0), 256, 0, s>>>(g, eps, p0, p1, cov);
+                            const uint32_t* perm, hipStream_t s) {
+  knn_cov_kernel<K><<<nblk(p1 - p0), 256, 0, s>>>(g, eps, p0, p1, cov, perm);
   return hipGetLastError();
 }
 
 hipError_t launch_knn_cov(const GridView& g, int k, double eps, size_t p0, size_t p1, Cov3 cov,
-                          hipStream_t s) {
+                          const uint32_t* perm, hipStream_t s) {
   if (p1 <= p0) return hipSuccess;
   switch (k) {
-    case 5: return knn_cov_k<5>(g, eps, p0, p1, cov, s);
-    case 10: return knn_cov_k<10>(g, eps, p0, p1, cov, s);
-    case 15: return knn_cov_k<15>(g, eps, p0, p1, cov, s);
-    case 20: return knn_cov_k<20>(g, eps, p0, p1, cov, s);
-    case 25: return knn_cov_k<25>(g, eps, p0, p1, cov, s);
-    case 30: return knn_cov_k<30>(g, eps, p0, p1, cov, s);
+    case 5: return knn_cov_k<5>(g, eps, p0, p1, cov, perm, s);
+    case 10: return knn_cov_k<10>(g, eps, p0, p1, cov, perm, s);
+    case 15: return knn_cov_k<15>(g, eps, p0, p1, cov, perm, s);
+    case 20: return knn_cov_k<20>(g, eps, p0, p1, cov, perm, s);
+    case 25: return knn_cov_k<25>(g, eps, p0, p1, cov, perm, s);
+    case 30: return knn_cov_k<30>(g, eps, p0, p1, cov, perm, s);
     default: return hipErrorInvalidValue;
   }
 }
