@@ -33,7 +33,7 @@ using namespace mgicp;
 
 namespace {
 
-constexpr double kDefaultOccupancy = 12.0;          // mean points per non-empty cell
+constexpr double kDefaultOccupancy = 10.0;          // mean points per non-empty cell (A/B: profiles/r01/ab_tocc)
 constexpr size_t kSmallBytes = size_t(64) << 10;  // pinned readback scratch per context
 constexpr size_t kMaxCells = size_t(1) << 29;       // dense cell table cap (2 GiB of uint32)
 
