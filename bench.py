@@ -311,7 +311,7 @@ def main():
     fod = fod_rows(eng, scan, cad, T_final, args.fod_cpu_sample) if args.fod_cpu_sample > 0 and world == 1 else None
     cpu = None
     frob_sample = None
-    if args.cpu_sample > 0:
+    if args.cpu_sample > 0 and world == 1:  # the CPU baseline is an N=1 figure
         n_cpu = min(args.cpu_sample, args.n_source)
         rate, info, T_cpu, (s_scan, s_cad) = cpu_baseline(n_cpu, args.cpu_threads, args.occlusion)
         scale = n_cpu / args.n_source
