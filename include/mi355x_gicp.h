@@ -183,7 +183,9 @@ int mgicp_debug_trace(mgicp_ctx* ctx, float* out, int max_iters);
 #define MGICP_KERNEL_FAMILIES 6
 int mgicp_debug_kernel_times(mgicp_ctx* ctx, double out_ms[MGICP_KERNEL_FAMILIES],
                              int out_counts[MGICP_KERNEL_FAMILIES]);
-/* enable (1) / disable (0) per-launch HIP event timing (off by default) */
+/* enable (1) / disable (0) per-launch HIP event timing (off by default); objective passes
+ * ([2]) are sampled every 8th launch (env MGICP_PROF_STRIDE), every other family is timed on
+ * every launch */
 int mgicp_set_profiling(mgicp_ctx* ctx, int on);
 
 #ifdef __cplusplus
