@@ -169,4 +169,32 @@ inline hipError_t upload_xyz(HostPool& pool, PinnedRing& ring, const void* host,
   return hipSuccess;
 }
 
+// Copy one 4-byte field (at byte `offset` of each strided host record) of n records into d_out
+// on `s`, through the same pinned ring (the colour word of PointXYZRGB for VoxelGrid).
+inline hipError_t upload_u32_field(HostPool& pool, PinnedRing& ring, const void* host, size_t n,
+                                   size_t stride, size_t offset, uint32_t* d_out, hipStream_t s) {
+  hipError_t e = ring.init();
+  if (e != hipSuccess) return e;
+  const size_t per = PinnedRing::kSlotBytes / 4;
+  const unsigned char* src = static_cast<const unsigned char*>(host) + offset;
+  const size_t parts = static_cast<size_t>(pool.size()) * 4;
+  for (size_t c = 0, k = 0; c < n; c += per, ++k) {
+    const int slot = static_cast<int>(k % PinnedRing::kSlots);
+    e = hipEventSynchronize(ring.ev[slot]);
+    if (e != hipSuccess) return e;
+    const size_t cnt = std::min(per, n - c);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(ring.buf[slot]);
+    const unsigned char* base = src + c * stride;
+    pool.parallel_for(parts, [&](size_t part) {
+      const size_t i0 = cnt * part / parts, i1 = cnt * (part + 1) / parts;
+      for (size_t i = i0; i < i1; ++i) std::memcpy(dst + i, base + i * stride, 4);
+    });
+    e = hipMemcpyAsync(d_out + c, dst, cnt * 4, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return e;
+    e = hipEventRecord(ring.ev[slot], s);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
 }  // namespace mgicp

@@ -1444,13 +1444,16 @@ int mgicp_voxel_grid(mgicp_ctx* ctx, const float* in, size_t n, size_t stride, i
   if (rc) return rc;
   hipStream_t s = ctx->stream;
   const bool rgb = rgb_offset >= 0;
-  if (rgb) {  // the packed colour word of every record (host marshalling of one field)
-    std::vector<uint32_t> h(n);
-    const unsigned char* base = reinterpret_cast<const unsigned char*>(in);
-    for (size_t i = 0; i < n; ++i) std::memcpy(&h[i], base + i * stride + rgb_offset, 4);
+  if (rgb) {  // the packed colour word of every record, through the pinned pipelined upload
     HIPCK(ctx->f_rgba_in.reserve(n));
-    HIPCK(hipMemcpyAsync(ctx->f_rgba_in.p, h.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-    if ((rc = sync(ctx))) return rc;
+    HostUploader& up = HostUploader::instance();
+    HIPCK(up.init(ctx->host_threads));
+    {
+      std::lock_guard<std::mutex> lk(up.mu);
+      HIPCK(upload_u32_field(*up.pool, up.ring, in, n, stride, static_cast<size_t>(rgb_offset),
+                             ctx->f_rgba_in.p, s));
+      if ((rc = sync(ctx))) return rc;
+    }
   }
   // getMinMax3D over the finite points
   const int nb = static_cast<int>(std::min<size_t>((n + 255) / 256, 1024));

@@ -244,7 +244,8 @@ class GICPEngine:
 
         leaf = np.broadcast_to(np.asarray(leaf, np.float64), (3,)).copy()
         _, ptr, n, stride = self._cloud_arg(cloud)
-        out = PointCloudRGB(max(n, 1))
+        out = PointCloudRGB()
+        out.points = np.empty(max(n, 1), dtype=POINT_XYZRGB)  # capacity; the call writes n_out whole records
         nout = ctypes.c_size_t()
         self._check(self._lib.mgicp_voxel_grid(
             self._h, ctypes.c_void_p(ptr), n, stride, int(POINT_XYZRGB.fields["rgb"][1]), _dp(leaf),
