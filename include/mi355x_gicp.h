@@ -162,6 +162,9 @@ int mgicp_debug_covariances(mgicp_ctx* ctx, int which, double* out_c6);
 /* one correspondence sweep at T (col-major); out_tgt[i] = target index or -1;
  * out_M6 (optional) = n x {m00,m01,m02,m11,m12,m22}; returns the count or < 0 */
 int mgicp_debug_correspondences(mgicp_ctx* ctx, const float T_cm[16], int* out_tgt, double* out_M6);
+/* the same sweep SEEDED with the previous sweep's matches, as the outer iterations after the first
+ * run it; same outputs */
+int mgicp_debug_correspondences_seeded(mgicp_ctx* ctx, const float T_cm[16], int* out_tgt, double* out_M6);
 /* OptimizationFunctorWithIndices::fdf at x over the last correspondence sweep */
 int mgicp_debug_fdf(mgicp_ctx* ctx, const double x[6], double* f, double g6[6]);
 /* the raw reduced sums of one objective pass at x: [0] sum r'Mr, [1..3] sum Mr,

@@ -92,6 +92,7 @@ _SIGNATURES = {
     "mgicp_comm_init": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]),
     "mgicp_debug_covariances": (ctypes.c_int, [_P, ctypes.c_int, _DP]),
     "mgicp_debug_correspondences": (ctypes.c_int, [_P, _FP, _IP, _DP]),
+    "mgicp_debug_correspondences_seeded": (ctypes.c_int, [_P, _FP, _IP, _DP]),
     "mgicp_debug_fdf": (ctypes.c_int, [_P, _DP, _DP, _DP]),
     "mgicp_debug_fdf_sums": (ctypes.c_int, [_P, _DP, _DP]),
     "mgicp_debug_moments": (ctypes.c_int, [_P, _FP, _DP]),

@@ -1596,8 +1596,9 @@ int mgicp_debug_covariances(mgicp_ctx* ctx, int which, double* out_c6) {
   return MGICP_OK;
 }
 
-int mgicp_debug_correspondences(mgicp_ctx* ctx, const float T_cm[16], int* out_tgt, double* out_M6) {
+static int debug_corr(mgicp_ctx* ctx, const float T_cm[16], bool seeded, int* out_tgt, double* out_M6) {
   if (!ctx || !T_cm) return MGICP_E_INVALID;
+  if (seeded && !ctx->seed_valid) return fail(ctx, MGICP_E_INVALID, "no previous sweep to seed from");
   HIPCK(hipSetDevice(ctx->device));
   int rc = prepare(ctx, true);
   if (rc) return rc;
@@ -1605,7 +1606,7 @@ int mgicp_debug_correspondences(mgicp_ctx* ctx, const float T_cm[16], int* out_t
   const size_t n = ctx->src.n;
   const Mat4 G = Mat4::identity();
   if ((rc = set_output(ctx, G))) return rc;
-  if ((rc = correspond(ctx, Mat4::from_cm(T_cm), G, false))) return rc;
+  if ((rc = correspond(ctx, Mat4::from_cm(T_cm), G, seeded))) return rc;
   const size_t p0 = ctx->shard_p0(), p1 = ctx->shard_p1(), ns = p1 - p0;
   std::vector<uint32_t> nn(ns), flag(ns), slot(ns), perm(n), tperm(ctx->tgt.n);
   HIPCK(hipMemcpyAsync(nn.data(), ctx->prev_pos.p, ns * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
@@ -1629,6 +1630,14 @@ int mgicp_debug_correspondences(mgicp_ctx* ctx, const float T_cm[16], int* out_t
     }
   }
   return cnt;
+}
+
+int mgicp_debug_correspondences(mgicp_ctx* ctx, const float T_cm[16], int* out_tgt, double* out_M6) {
+  return debug_corr(ctx, T_cm, false, out_tgt, out_M6);
+}
+
+int mgicp_debug_correspondences_seeded(mgicp_ctx* ctx, const float T_cm[16], int* out_tgt, double* out_M6) {
+  return debug_corr(ctx, T_cm, true, out_tgt, out_M6);
 }
 
 int mgicp_debug_fdf(mgicp_ctx* ctx, const double x[6], double* f, double g6[6]) {

@@ -281,6 +281,15 @@ class GICPEngine:
             self._h, _fp(_cm(T)), tgt.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), _dp(M)), "debug_correspondences")
         return m, tgt, M
 
+    def debug_correspondences_seeded(self, T, n: int):
+        """The same sweep seeded with the previous sweep's matches (outer iterations >= 2)."""
+        tgt = np.full(n, -1, np.int32)
+        M = np.zeros((n, 6), np.float64)
+        m = self._check(self._lib.mgicp_debug_correspondences_seeded(
+            self._h, _fp(_cm(T)), tgt.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), _dp(M)),
+            "debug_correspondences_seeded")
+        return m, tgt, M
+
     def debug_fdf(self, x):
         x = np.asarray(x, np.float64)
         f = ctypes.c_double()

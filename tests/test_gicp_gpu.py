@@ -262,3 +262,51 @@ def test_grid_lattice_ties(engine_mod):
     mg, tj_gpu, _ = e.debug_correspondences(T, len(pts))
     assert mr == mg
     np.testing.assert_array_equal(tj_ref, tj_gpu)
+
+
+@pytest.mark.gpu
+def test_seeded_correspondences_exact(engine_mod, part_small):
+    """Outer iterations >= 2 seed the 1-NN search with the previous match.  Sequences of seeded
+    sweeps give the oracle's correspondences exactly, from far (seed useless) to near."""
+    src, tgt, Ttrue = part_small
+    o, e = _pair(engine_mod, src, tgt)
+    Tt = np.linalg.inv(Ttrue).astype(np.float32)
+    near = Tt.copy()
+    near[:3, 3] += np.float32(4e-4)
+    off = np.eye(4, dtype=np.float32)
+    off[:3, 3] = [0.0, 0.0, 0.035]
+    e.debug_correspondences(np.eye(4, dtype=np.float32), len(src))
+    for T in [Tt, near, Tt, off, Tt, np.eye(4, dtype=np.float32)]:
+        m_ref, tj_ref, _, M_ref = o.correspondences(T)
+        m_gpu, tj_gpu, M_gpu = e.debug_correspondences_seeded(T, len(src))
+        assert m_gpu == m_ref
+        np.testing.assert_array_equal(tj_gpu, tj_ref)
+        ok = tj_ref >= 0
+        if ok.any():
+            Mu = _upper(M_ref)[ok]
+            assert np.abs(M_gpu[ok] - Mu).max() / np.abs(Mu).max() <= 1e-12
+
+
+@pytest.mark.gpu
+def test_seeded_correspondences_lattice_ties(engine_mod):
+    """Seeded sweeps on a lattice with exact distance ties: the (d2, index) rule must still pick
+    the oracle's point whatever the seed."""
+    from oracle import ref
+
+    g = np.arange(0.0, 1.0, 0.05, dtype=np.float32)
+    X, Y, Z = np.meshgrid(g, g, g, indexing="ij")
+    pts = np.stack([X.ravel(), Y.ravel(), Z.ravel()], 1).astype(np.float32)
+    e = engine_mod()
+    e.set_source_xyz(pts)
+    e.set_target_xyz(pts)
+    o = ref.RefGICP()
+    o.set_source(pts)
+    o.set_target(pts)
+    e.debug_correspondences(np.eye(4, dtype=np.float32), len(pts))
+    for shift in ([0.025, 0.0, 0.0], [0.013, -0.02, 0.007], [0.0, 0.0, 0.0], [0.0125, 0.0125, 0.0]):
+        T = np.eye(4, dtype=np.float32)
+        T[:3, 3] = shift
+        mr, tj_ref, _, _ = o.correspondences(T)
+        mg, tj_gpu, _ = e.debug_correspondences_seeded(T, len(pts))
+        assert mr == mg
+        np.testing.assert_array_equal(tj_ref, tj_gpu)
