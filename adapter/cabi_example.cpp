@@ -63,6 +63,33 @@ int main() {
   for (int r = 0; r < 4; ++r)
     std::printf("  [% .6f % .6f % .6f % .6f]\n", T[r], T[4 + r], T[8 + r], T[12 + r]);
   const double err = std::fabs(T[0] - c) + std::fabs(T[1] - s) + std::fabs(T[4] + s) + std::fabs(T[12] - 0.01f);
+  bool ok = rc == MGICP_OK && res.converged && err < 1e-3;
+
+  // the opt-in Gauss-Newton mode (one moment pass per outer iteration), same clouds
+  prm.solver = MGICP_SOLVER_GN;
+  rc = mgicp_set_params(ctx, &prm);
+  float Tg[16];
+  rc |= mgicp_align(ctx, nullptr, Tg, &res);
+  const double err_gn = std::fabs(Tg[0] - c) + std::fabs(Tg[1] - s) + std::fabs(Tg[4] + s) + std::fabs(Tg[12] - 0.01f);
+  std::printf("GN: rc=%d converged=%d iterations=%d passes=%d err=%.2e\n", rc, res.converged, res.iterations,
+              res.n_evals, err_gn);
+  ok = ok && rc == MGICP_OK && res.converged && res.n_evals == res.iterations && err_gn < 1e-3;
+
+  // Filter::downsampleCloud (VoxelGrid, 5 cm leaves) and Filter::removeFromCloud
+  // (SegmentDifferences of the aligned source against the target) on PointXYZRGB records
+  std::vector<PointXYZRGB> vox(src.size());
+  size_t n_vox = 0;
+  const double leaf[3] = {0.05, 0.05, 0.05};
+  rc = mgicp_voxel_grid(ctx, &src[0].x, src.size(), sizeof(PointXYZRGB), 16, leaf, 0, &vox[0].x,
+                        sizeof(PointXYZRGB), &n_vox);
+  std::vector<unsigned char> keep(src.size());
+  size_t n_keep = 0;
+  rc |= mgicp_segment_differences(ctx, Tg, &src[0].x, src.size(), sizeof(PointXYZRGB), &tgt[0].x, tgt.size(),
+                                  sizeof(PointXYZRGB), 1e-4, keep.data(), &n_keep);
+  std::printf("VoxelGrid: %zu -> %zu leaves; SegmentDifferences(aligned, 1 cm): %zu of %zu kept; rc=%d\n",
+              src.size(), n_vox, n_keep, src.size(), rc);
+  ok = ok && rc == MGICP_OK && n_vox > 0 && n_vox < src.size() && n_keep < src.size() / 100;
   mgicp_destroy(ctx);
-  return (rc == MGICP_OK && res.converged && err < 1e-3) ? 0 : 1;
+  std::printf("%s\n", ok ? "cabi_example: OK" : "cabi_example: FAILED");
+  return ok ? 0 : 1;
 }

@@ -92,3 +92,16 @@ def test_product_never_imports_oracle():
                 assert not re.search(r"\bref_[a-z_]+\s*\(", text), f
                 assert not re.search(r"^\s*(from oracle|import oracle)", text, re.M), f
                 assert "libgicp_ref" not in text, f
+
+
+@pytest.mark.gpu
+def test_cabi_example_plain_cpp_host():
+    """adapter/cabi_example (g++, no HIP headers, no torch) drives the C-ABI as the catkin adapter
+    does: PCL-mode and GN aligns, VoxelGrid and SegmentDifferences on PointXYZRGB records."""
+    import subprocess
+
+    exe = os.path.join(ROOT, "adapter", "cabi_example")
+    assert os.path.exists(exe), "build it with `make adapter-example`"
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "cabi_example: OK" in out.stdout
