@@ -19,7 +19,7 @@
 #define MGICP_NN_UNROLL 4  // candidate gathers in flight per lane in the 1-NN scans
 #endif
 #ifndef MGICP_CORR_WAVES
-#define MGICP_CORR_WAVES 1  // minimum resident waves per SIMD requested for the 1-NN kernel
+#define MGICP_CORR_WAVES 8  // resident waves per SIMD requested for the 1-NN kernel (64 VGPRs; A/B profiles/r01/ab_w8)
 #endif
 #ifndef MGICP_CORR_STATS
 #define MGICP_CORR_STATS 0  // 1: count 1-NN work per sweep (diagnostic builds only)
