@@ -21,6 +21,9 @@
 #ifndef MGICP_CORR_WAVES
 #define MGICP_CORR_WAVES 8  // resident waves per SIMD requested for the 1-NN kernel (64 VGPRs; A/B profiles/r01/ab_w8)
 #endif
+#ifndef MGICP_COV_WAVES
+#define MGICP_COV_WAVES 1  // resident waves per SIMD requested for the k-NN covariance kernel
+#endif
 #ifndef MGICP_CORR_STATS
 #define MGICP_CORR_STATS 0  // 1: count 1-NN work per sweep (diagnostic builds only)
 #endif
@@ -459,7 +462,7 @@ __device__ __forceinline__ double sel3(int i, double a, double b, double c) {
 
 // `perm` (optional): query order over [p0, p1) (Morton order: compact 3-D patch per wave)
 template <int K>
-__global__ __launch_bounds__(256) void knn_cov_kernel(GridView g, double eps, size_t p0,
+__global__ __launch_bounds__(256, MGICP_COV_WAVES) void knn_cov_kernel(GridView g, double eps, size_t p0,
                                                       size_t p1, Cov3 cov,
                                                       const uint32_t* __restrict__ perm) {
   const size_t t = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
