@@ -81,6 +81,7 @@ void        mgicp_destroy(mgicp_ctx* ctx);
 int         mgicp_device_count(int* n);
 
 /* ---- inputs (Registration::setInputTarget / setInputSource) ----
+ * At most 2^31 - 2 points per cloud (32-bit point indices); larger clouds return MGICP_E_INVALID.
  * Host buffers are copied at call time; the cloud is marked dirty so the next align()
  * rebuilds its grid and covariances (PCL resets its trees/covariances the same way).
  * The *_device variants take a device pointer already resident in HBM on this context's

@@ -383,6 +383,8 @@ int upload_cloud(mgicp_ctx* ctx, Cloud& cl, const float* xyz, size_t n, size_t s
                  bool device_ptr) {
   if (n == 0 || !xyz || stride < 12 || (stride % 4) != 0)
     return fail(ctx, MGICP_E_INVALID, "invalid cloud (null, empty or stride not a multiple of 4 >= 12)");
+  if (n >= (size_t(1) << 31) - 1)  // 32-bit point indices / hipcub item counts
+    return fail(ctx, MGICP_E_INVALID, "cloud too large: at most 2^31 - 2 points per cloud");
   const double t0 = now_ms();
   MGICP_TRACE_AT("upload: begin");
   HIPCK(cl.orig.reserve(n));
