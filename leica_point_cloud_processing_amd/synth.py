@@ -269,6 +269,17 @@ def axis_angle_matrix(axis, angle: float, center=(0.0, 0.0, 0.0), t=(0.0, 0.0, 0
 # ---------------------------------------------------------------------------------------
 # reference unit-test fixture (test_gicp_alignment.cpp)
 # ---------------------------------------------------------------------------------------
+def filter_test_cube(rng: "GlibcRand", dim: float = 5.0, nsamples: int = 5000, x: float = 0.0) -> np.ndarray:
+    """TestFilter::cubePointCloud (/root/reference/test/test_filter.cpp:36-49): nsamples points
+    x + dim * (double)rand() / (double)RAND_MAX per coordinate (double arithmetic, stored as float),
+    drawing x, y, z in that order from the glibc rand() stream `rng`."""
+    out = np.empty((nsamples, 3), np.float32)
+    for i in range(nsamples):
+        for d in range(3):
+            out[i, d] = np.float32(x + dim * float(rng.rand()) / 2147483647.0)
+    return out
+
+
 def cube_fixture(ply_path: str, n: int = 5000, yaw: float = 0.175):
     """(source_xyz, target_xyz, T_rot): source = CADToPointCloud(cube.ply, n) with glibc rand()
     from its default seed, target = Utils::rotateCloud(source, 0, 0, yaw)."""

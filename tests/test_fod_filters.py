@@ -205,3 +205,114 @@ def test_voxel_grid_gpu_overflow_and_filter_class(eng):
     sub = PointCloudRGB()
     Filter.removeFromCloud(c, d, 1e-4, sub)
     assert 0 < len(sub) < len(c)
+
+
+# ---------------------------------------------------------------------------------------
+# The reference's own Filter tests (test/test_filter.cpp), same data, same assertions
+# ---------------------------------------------------------------------------------------
+def _filter_fixture_clouds():
+    """gtest runs TestFilter's cases in file order, each constructing the fixture (one
+    5000-point cube, 15000 rand() calls) from the shared glibc rand() stream (default seed):
+    testDownsample sees calls 0..14999, testBox 15000..29999, testDifference 30000..44999 plus
+    its own target cube (x = 2) from 45000..59999."""
+    from leica_point_cloud_processing_amd import synth
+
+    rng = synth.GlibcRand(1)
+    down = synth.filter_test_cube(rng)
+    synth.filter_test_cube(rng)  # testBox's fixture
+    diff_src = synth.filter_test_cube(rng)
+    diff_tgt = synth.filter_test_cube(rng, x=2.0)
+    return down, diff_src, diff_tgt
+
+
+def _white(xyz):
+    c = PointCloudRGB.from_xyz(xyz)
+    c.points["rgb"] = 0xFFFFFFFF  # r = g = b = 255 (alpha 255)
+    return c
+
+
+def test_filter_fixture_reproduction():
+    down, diff_src, diff_tgt = _filter_fixture_clouds()
+    assert down.shape == (5000, 3) and (down >= 0).all() and (down <= 5).all()
+    assert (diff_tgt >= 2).all() and (diff_tgt <= 7).all()
+    # the first glibc rand() after srand(1) is 1804289383
+    assert down[0, 0] == np.float32(5.0 * 1804289383 / 2147483647.0)
+
+
+@pytest.mark.gpu
+def test_reference_testDownsample(eng):
+    """test_filter.cpp:63-77: leaf = 2 * computeCloudResolution; the downsampled cloud's
+    resolution is larger.  Also bit-exact against the VoxelGrid restatement."""
+    from leica_point_cloud_processing_amd.filter import Filter
+    from oracle import ref
+
+    down, _, _ = _filter_fixture_clouds()
+    cloud = _white(down)
+    res = eng.cloud_resolution(cloud)
+    leaf = float(np.float32(2 * res))
+    out = PointCloudRGB()
+    Filter(leaf).downsampleCloud(cloud, out)
+    assert eng.cloud_resolution(out) > res
+    xyz_ref, rgba_ref, _ = ref.voxel_grid(cloud.points, leaf)
+    np.testing.assert_array_equal(out.xyz(), xyz_ref)
+    np.testing.assert_array_equal(out.points["rgb"], rgba_ref)
+
+
+@pytest.mark.gpu
+def test_reference_testDifference(eng):
+    """test_filter.cpp:95-106: removeFromCloud(target, source, res, diff) leaves a valid
+    (size > 1) cloud.  Also bit-exact against the SegmentDifferences restatement."""
+    from leica_point_cloud_processing_amd.filter import Filter
+    from oracle import ref
+
+    _, src, tgt = _filter_fixture_clouds()
+    source, target = _white(src), _white(tgt)
+    res = eng.cloud_resolution(source)
+    diff = PointCloudRGB()
+    Filter.removeFromCloud(target, source, res, diff)
+    assert len(diff) > 1  # Utils::isValidCloud
+    keep_ref, cnt_ref = ref.segment_differences(tgt, src, res)
+    assert len(diff) == cnt_ref
+    np.testing.assert_array_equal(diff.xyz(), tgt[keep_ref])
+
+
+def _utils_lattice(dim=3.0, step=0.1):
+    """TestUtils::cubeXYZ / cubeRGB (test_utils.cpp:31-60): float loop counters i += step."""
+    vals = []
+    v = np.float32(0.0)
+    while v < np.float32(dim):
+        vals.append(v)
+        v = np.float32(v + np.float32(step))
+    g = np.array(vals, np.float32)
+    X, Y, Z = np.meshgrid(g, g, g, indexing="ij")
+    return np.stack([X.ravel(), Y.ravel(), Z.ravel()], 1).astype(np.float32)
+
+
+@pytest.mark.gpu
+def test_reference_testCloudResolution(eng):
+    """test_utils.cpp:77-91: the resolution of a 0.1-step lattice is within
+    0.05 of 0.1, for PointXYZ (16-byte records) and PointXYZRGB (32-byte records) alike; the GPU
+    2-NN mean equals a brute-force numpy evaluation."""
+    from leica_point_cloud_processing_amd.cloud import PointCloudRGB as RGB
+
+    import ctypes
+
+    xyz = _utils_lattice()
+    rec16 = np.zeros((len(xyz), 4), np.float32)  # pcl::PointXYZ records (x, y, z, pad)
+    rec16[:, :3] = xyz
+    rec16[:, 3] = 1.0
+    out = ctypes.c_double()
+    rc = eng._lib.mgicp_cloud_resolution(eng._h, ctypes.c_void_p(rec16.ctypes.data), len(rec16), 16,
+                                         ctypes.byref(out))
+    assert rc == 0
+    res_xyz = out.value
+    res_rgb = eng.cloud_resolution(RGB.from_xyz(xyz, rgb=0xFFFFFFFF))
+    assert 0.05 <= res_xyz <= 0.15 and 0.05 <= res_rgb <= 0.15
+    assert res_xyz == res_rgb
+    # brute force on a sub-lattice corner (same float arithmetic: fp32 d2, sqrt in fp32, fp64 mean)
+    sub = xyz[(xyz < np.float32(0.55)).all(1)]
+    d = sub[:, None, :] - sub[None, :, :]
+    d2 = ((d[..., 0] * d[..., 0] + d[..., 1] * d[..., 1]).astype(np.float32) + d[..., 2] * d[..., 2]).astype(np.float32)
+    np.fill_diagonal(d2, np.inf)
+    expect = float(np.mean(np.sqrt(d2.min(1)).astype(np.float64)))
+    assert abs(eng.cloud_resolution(sub) - expect) <= 1e-12
