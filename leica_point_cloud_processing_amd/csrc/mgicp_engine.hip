@@ -210,6 +210,7 @@ struct Cloud {
   bool want_empty_map = false;
   bool drop_nonfinite = false; // build the grid over the finite points only (KdTreeFLANN semantics)
   double occupancy = 0;        // grid sizing target (points per non-empty cell); 0 = context default
+  size_t n_built = 0;          // points of the last grid built in this slot (cell-size hint)
   DevBuf<double2> cov;        // 3 * n
   float lo[3] = {0.f, 0.f, 0.f}, hi[3] = {0.f, 0.f, 0.f};  // bounding box (original coordinates)
   GridView view{};
@@ -485,10 +486,20 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
     return nc;
   };
   double h = maxext > 0.f ? static_cast<double>(maxext) / std::cbrt(static_cast<double>(n)) : 1.0;
+  // a cell size that already fitted a cloud of the same scene is a better start than the 3-D
+  // guess: this cloud's previous grid, else (source) the target's, scaled as a surface (sqrt n)
+  if (cl.view.h > 0.f && cl.n_built > 0)
+    h = static_cast<double>(cl.view.h) * std::sqrt(static_cast<double>(cl.n_built) / n);
+  else if (&cl == &ctx->src && ctx->tgt.view.h > 0.f && ctx->tgt.n_built > 0)
+    h = static_cast<double>(ctx->tgt.view.h) * std::sqrt(static_cast<double>(ctx->tgt.n_built) / n);
   h = std::max(h, 1e-6);
   int nd[3];
   double h_prev = 0, occ_prev = 0;
   HIPCK(ctx->u64.reserve(1));
+  HIPCK(ctx->keys.reserve(n));
+  // the sizing histogram also writes the cell keys: when its cell size is accepted as is, the
+  // final keyed histogram pass is skipped
+  double h_keys = -1.0;
   for (int it = 0; it < 6 && maxext > 0.f; ++it) {
     size_t nc = dims(h, nd);
     int guard = 0;
@@ -501,7 +512,7 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
     HIPCK(hipMemsetAsync(ctx->counts.p, 0, (nc + 1) * sizeof(uint32_t), s));
     HIPCK(hipMemsetAsync(ctx->u64.p, 0, sizeof(unsigned long long), s));
     HIPCK(launch_cell_hist(cl.orig.p, n, mn[0], mn[1], mn[2], static_cast<float>(1.0 / h), nd[0],
-                           nd[1], nd[2], ctx->counts.p, nullptr, s));
+                           nd[1], nd[2], ctx->counts.p, ctx->keys.p, s));
     HIPCK(launch_count_nonzero(ctx->counts.p, nc, ctx->u64.p, s));
     HIPCK(hipMemcpyAsync(ctx->h_small, ctx->u64.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     rc = sync(ctx);
@@ -510,8 +521,10 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
     std::memcpy(&nonempty, ctx->h_small, sizeof(nonempty));
     MGICP_TRACE_AT("grid: sizing histogram synced");
     const double occ = static_cast<double>(n) / std::max<unsigned long long>(nonempty, 1);
-    if ((occ > 0.6 * target_occ && occ < 1.6 * target_occ) || nc >= kMaxCells / 2)
+    if ((occ > 0.6 * target_occ && occ < 1.6 * target_occ) || nc >= kMaxCells / 2) {
+      h_keys = h;  // counts and keys of this pass are the final ones
       break;
+    }
     if (nonempty <= 1 && occ < target_occ) break;  // everything in one cell already
     double dim = 2.0;
     if (h_prev > 0 && occ_prev > 0 && std::fabs(std::log(h / h_prev)) > 1e-3) {
@@ -529,7 +542,9 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
     nc = dims(h, nd);
   }
   const float inv_h = static_cast<float>(1.0 / h);
-  // 3. final histogram with keys, scan -> cell_start, stable radix sort -> permutation
+  const bool have_keys = h_keys == h;
+  // 3. final histogram with keys (unless the accepted sizing pass made them), scan ->
+  // cell_start, stable radix sort -> permutation
   HIPCK(ctx->counts.reserve(nc + 1));
   HIPCK(ctx->keys.reserve(n));
   HIPCK(ctx->keys_sorted.reserve(n));
@@ -538,9 +553,11 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
   HIPCK(cl.cell_start.reserve(nc + 1));
   HIPCK(cl.pts.reserve(n));
   MGICP_TRACE_AT("grid: final buffers reserved");
-  HIPCK(hipMemsetAsync(ctx->counts.p, 0, (nc + 1) * sizeof(uint32_t), s));
-  HIPCK(launch_cell_hist(cl.orig.p, n, mn[0], mn[1], mn[2], inv_h, nd[0], nd[1], nd[2],
-                         ctx->counts.p, ctx->keys.p, s));
+  if (!have_keys) {
+    HIPCK(hipMemsetAsync(ctx->counts.p, 0, (nc + 1) * sizeof(uint32_t), s));
+    HIPCK(launch_cell_hist(cl.orig.p, n, mn[0], mn[1], mn[2], inv_h, nd[0], nd[1], nd[2],
+                           ctx->counts.p, ctx->keys.p, s));
+  }
   int bits = 1;
   while ((size_t(1) << bits) < nc && bits < 32) ++bits;
   const size_t sb = std::max(sort_scratch_bytes(n, bits), scan_scratch_bytes(nc + 1));
@@ -579,6 +596,7 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
     g.empty_dist = cl.empty_dist.p;
   }
   cl.ncells = nc;
+  cl.n_built = n;
   cl.dirty = false;
   cl.have_cov = false;
   return MGICP_OK;
