@@ -29,7 +29,10 @@ struct GridView {
   const uint8_t* empty_dist;
 };
 
-constexpr int kEmptyCap = 15;
+#ifndef MGICP_EMPTY_CAP
+#define MGICP_EMPTY_CAP 15
+#endif
+constexpr int kEmptyCap = MGICP_EMPTY_CAP;
 
 struct Cov3 {  // SoA triple of double2 arrays
   double2* a;  // {m00, m01}
