@@ -21,6 +21,9 @@
 #ifndef MGICP_CORR_WAVES
 #define MGICP_CORR_WAVES 8  // resident waves per SIMD requested for the 1-NN kernel (64 VGPRs; A/B profiles/r01/ab_w8)
 #endif
+#ifndef MGICP_KNN_INSERT_EARLY
+#define MGICP_KNN_INSERT_EARLY 0  // k-NN top-K insert: 1 = early-exit tail shift, 0 = branchless
+#endif
 #ifndef MGICP_COV_WAVES
 #define MGICP_COV_WAVES 1  // resident waves per SIMD requested for the k-NN covariance kernel
 #endif
@@ -197,6 +200,19 @@ struct KnnVisitor {
     return key[K - 1] == ~0ull ? INFINITY : __uint_as_float(static_cast<uint32_t>(key[K - 1] >> 32));
   }
   __device__ __forceinline__ void insert(unsigned long long c, uint32_t cp) {
+#if MGICP_KNN_INSERT_EARLY
+    // shift from the tail and stop at the insertion slot (accepted candidates of the
+    // nearest-rows-first order usually land near the tail)
+#pragma unroll
+    for (int k = K - 1; k > 0; --k) {
+      if (!(c < key[k - 1])) { key[k] = c; pos[k] = cp; return; }
+      key[k] = key[k - 1];
+      pos[k] = pos[k - 1];
+    }
+    key[0] = c;
+    pos[0] = cp;
+    return;
+#endif
 #pragma unroll
     for (int k = K - 1; k > 0; --k) {
       const bool sh = c < key[k - 1];
