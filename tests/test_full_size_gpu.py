@@ -1,0 +1,81 @@
+"""Full-size (BASELINE.json C4: 5M <-> 5M) GPU checks through size-independent properties.
+
+The oracle finishes the 5M case in minutes, so at this size the engine is checked by what holds
+at any size (DESIGN.md "Parity"; bench.py's `frob_vs_oracle_sample` covers the 500k sample):
+  * determinism: align() twice (cached grids / covariances) gives bit-identical transforms;
+  * correspondences: a seeded sample of queries against a brute-force float64 1-NN over the
+    whole 5M target (the reference's kd-tree nearestKSearch(k=1) + maxCorrDist gate,
+    gicp_alignment.cpp -> pcl::GeneralizedIterativeClosestPoint::computeTransformation);
+  * covariances: PCL's plane-regularised form U diag(1, 1, eps) U^T (gicp.hpp
+    computeCovariances), i.e. symmetric with eigenvalues {eps, 1, 1}, for every point.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+N = 5_000_000
+MAX_CORR = 0.04  # BASELINE.json C4 maxCorrDist
+EPS = 1e-3  # PCL gicp_epsilon_ default
+
+
+@pytest.fixture(scope="module")
+def c4():
+    from leica_point_cloud_processing_amd import synth
+    from leica_point_cloud_processing_amd.engine import GICPEngine
+
+    scan, cad, T_true = synth.scan_vs_cad(N, N)
+    e = GICPEngine()
+    e.set_source_xyz(scan)
+    e.set_target_xyz(cad)
+    return e, scan, cad, T_true
+
+
+def test_full_size_align_deterministic(c4):
+    e, _, _, T_true = c4
+    T1 = e.align()
+    assert e.hasConverged()
+    T2 = e.align()
+    assert np.array_equal(T1, T2)
+    # moved towards the synthetic ground truth (PCL's loose delta rule stops early)
+    assert np.abs(T1.astype(np.float64) @ T_true - np.eye(4)).max() < 0.05
+
+
+def test_full_size_correspondences_brute_force(c4):
+    e, scan, cad, _ = c4
+    T = np.eye(4, dtype=np.float32)
+    T[:3, 3] = [0.0, 0.0, 0.01]  # 1 cm off: a mix of near matches and gate rejections
+    m, tj, _ = e.debug_correspondences(T, len(scan))
+    assert 0 < m <= len(scan) and m == int((tj >= 0).sum())
+    tgt = cad.astype(np.float64)
+    q_all = scan.astype(np.float32) + T[:3, 3]  # identity rotation: exact fp32 transform
+    rng = np.random.default_rng(11)
+    gate = MAX_CORR * MAX_CORR
+    for i in rng.choice(len(scan), 96, replace=False):
+        q = q_all[i].astype(np.float64)
+        d2 = ((tgt - q) ** 2).sum(axis=1)
+        dmin = float(d2.min())
+        if abs(dmin - gate) <= 1e-5 * gate:
+            continue  # float32 vs float64 rounding at the gate itself: either answer is exact
+        if dmin > gate:
+            assert tj[i] == -1, (i, dmin)
+        else:
+            assert tj[i] >= 0, (i, dmin)
+            assert d2[tj[i]] <= dmin * (1 + 1e-5) + 1e-12, (i, d2[tj[i]], dmin)
+
+
+@pytest.mark.parametrize("which", ["source", "target"])
+def test_full_size_covariance_structure(c4, which):
+    e, scan, cad, _ = c4
+    c = e.debug_covariances(which, len(scan) if which == "source" else len(cad))
+    assert np.isfinite(c).all()
+    M = np.empty((len(c), 3, 3))
+    M[:, 0, 0], M[:, 0, 1], M[:, 0, 2] = c[:, 0], c[:, 1], c[:, 2]
+    M[:, 1, 1], M[:, 1, 2], M[:, 2, 2] = c[:, 3], c[:, 4], c[:, 5]
+    M[:, 1, 0], M[:, 2, 0], M[:, 2, 1] = c[:, 1], c[:, 2], c[:, 4]
+    idx = np.random.default_rng(5).choice(len(c), 200_000, replace=False)
+    w = np.linalg.eigvalsh(M[idx])
+    np.testing.assert_allclose(w[:, 0], EPS, rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(w[:, 1:], 1.0, rtol=0, atol=1e-9)
+    # trace is a per-point invariant: check it for every point
+    np.testing.assert_allclose(c[:, 0] + c[:, 3] + c[:, 5], 2.0 + EPS, rtol=0, atol=1e-9)
