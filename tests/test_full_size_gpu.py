@@ -79,3 +79,34 @@ def test_full_size_covariance_structure(c4, which):
     np.testing.assert_allclose(w[:, 1:], 1.0, rtol=0, atol=1e-9)
     # trace is a per-point invariant: check it for every point
     np.testing.assert_allclose(c[:, 0] + c[:, 3] + c[:, 5], 2.0 + EPS, rtol=0, atol=1e-9)
+
+
+def test_full_size_gn_mode_deterministic(c4):
+    """The opt-in Gauss-Newton mode (MGICP_SOLVER_GN) at C4: repeatable and converging."""
+    from leica_point_cloud_processing_amd.engine import GICPEngine
+
+    _, scan, cad, T_true = c4
+    g = GICPEngine(solver=1)
+    g.set_source_xyz(scan)
+    g.set_target_xyz(cad)
+    T1 = g.align()
+    assert g.hasConverged()
+    T2 = g.align()
+    assert np.array_equal(T1, T2)
+    assert np.abs(T1.astype(np.float64) @ T_true - np.eye(4)).max() < 1e-3
+
+
+def test_c5_occluded_scan_deterministic():
+    """BASELINE.json C5 (20M-point scan with 25 % occlusion vs 5M CAD): repeatable align."""
+    from leica_point_cloud_processing_amd import synth
+    from leica_point_cloud_processing_amd.engine import GICPEngine
+
+    scan, cad, T_true = synth.scan_vs_cad(20_000_000, N, occlusion=0.25)
+    e = GICPEngine()
+    e.set_source_xyz(scan)
+    e.set_target_xyz(cad)
+    T1 = e.align()
+    assert e.hasConverged()
+    T2 = e.align()
+    assert np.array_equal(T1, T2)
+    assert np.abs(T1.astype(np.float64) @ T_true - np.eye(4)).max() < 0.05
