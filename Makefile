@@ -8,7 +8,7 @@ HDRS  := $(wildcard $(PKG)/csrc/*.hpp) include/mi355x_gicp.h
 # -ffp-contract=off: no FMA contraction, so fp32/fp64 expressions round like PCL's SSE2 Eigen
 HIPFLAGS := -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -ffp-contract=off -Wall -Wno-unused-result
 
-all: $(LIB) oracle adapter-example
+all: $(LIB) oracle adapter-example adapter-replay
 
 $(LIB): $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS) -lrccl
@@ -23,6 +23,21 @@ adapter/cabi_example: adapter/cabi_example.cpp include/mi355x_gicp.h $(LIB)
 
 adapter-example: adapter/cabi_example
 
+# the drop-in adapter itself (adapter/GICPAlignment.cpp + adapter/Filter_mi355x.cpp), compiled as the
+# catkin package would compile it (-std=c++14, the reference's CMakeLists.txt:6) against the
+# layout-exact PCL / Eigen / ROS stand-ins of tests/adapter_standins (PCL and ROS are absent here),
+# linked with a replay of test/test_gicp_alignment.cpp:50-131 (test infrastructure)
+STANDIN := tests/adapter_standins
+REPLAY  := adapter/build/replay_test_gicp_alignment
+$(REPLAY): adapter/GICPAlignment.cpp adapter/GICPAlignment.h adapter/Filter_mi355x.cpp include/mi355x_gicp.h \
+           $(wildcard $(STANDIN)/*.h) $(STANDIN)/Utils_standin.cpp $(STANDIN)/replay_test_gicp_alignment.cpp $(LIB)
+	mkdir -p adapter/build
+	g++ -O2 -std=c++14 -Wall -Wextra -Werror -I$(STANDIN) -Iadapter -Iinclude -o $@ \
+	    adapter/GICPAlignment.cpp adapter/Filter_mi355x.cpp $(STANDIN)/Utils_standin.cpp \
+	    $(STANDIN)/replay_test_gicp_alignment.cpp -L$(PKG) -lmgicp -Wl,-rpath,'$$ORIGIN/../../$(PKG)'
+
+adapter-replay: $(REPLAY)
+
 oracle:
 	$(MAKE) -C oracle
 
@@ -30,4 +45,4 @@ clean:
 	rm -f $(LIB) $(PKG)/libmgicp_*.so
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean adapter-example variant
+.PHONY: all oracle clean adapter-example adapter-replay variant

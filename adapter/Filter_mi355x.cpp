@@ -14,6 +14,7 @@
 #include <mi355x_gicp.h>
 
 #include <cstddef>
+#include <mutex>
 #include <vector>
 
 namespace
@@ -21,7 +22,16 @@ namespace
 static_assert(sizeof(pcl::PointXYZRGB) == 32, "PointXYZRGB record must be 32 bytes (x,y,z,pad,rgb,pad)");
 constexpr int kRgbOffset = offsetof(pcl::PointXYZRGB, rgba);
 
-// one engine context per process for the stateless helpers (mgicp_create resolves every kernel)
+// one engine context per process for the stateless helpers (mgicp_create resolves every kernel).
+// A context holds mutable scratch and one stream and serves one caller at a time
+// (include/mi355x_gicp.h "Threading"): every use takes helperMutex(), so concurrent ROS
+// callbacks (a multi-threaded spinner) serialise on it instead of racing.
+std::mutex& helperMutex()
+{
+    static std::mutex m;
+    return m;
+}
+
 mgicp_ctx* helperContext()
 {
     static mgicp_ctx* ctx = []() {
@@ -43,6 +53,7 @@ void Filter::downsampleCloud(PointCloudRGB::Ptr cloud, PointCloudRGB::Ptr cloud_
     double res = Utils::computeCloudResolution(cloud);
     ROS_INFO("Pointcloud resolution before downsampling: %f", res);
 
+    std::lock_guard<std::mutex> lock(helperMutex());
     mgicp_ctx* ctx = helperContext();
     if (!ctx)
         return;
@@ -76,6 +87,7 @@ void Filter::removeFromCloud(PointCloudRGB::Ptr input_cloud, PointCloudRGB::Ptr 
                              PointCloudRGB::Ptr cloud_filtered)
 {
     ROS_INFO("Difference from segment with threshold: %f", threshold);
+    std::lock_guard<std::mutex> lock(helperMutex());
     mgicp_ctx* ctx = helperContext();
     if (!ctx)
         return;

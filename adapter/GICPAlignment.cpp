@@ -19,11 +19,6 @@ namespace
 {
 static_assert(sizeof(pcl::PointXYZRGB) == 32, "PointXYZRGB record must be 32 bytes (x,y,z,pad,rgb,pad)");
 
-const float* xyzOf(const pcl::PointCloud<pcl::PointXYZRGB>& c)
-{
-    return c.points.empty() ? nullptr : &c.points[0].x;
-}
-
 float* xyzOf(pcl::PointCloud<pcl::PointXYZRGB>& c)
 {
     return c.points.empty() ? nullptr : &c.points[0].x;
@@ -83,13 +78,22 @@ void GICPAlignment::getCovariances(PointCloudRGB::Ptr cloud)
     if (!engine_ || cloud->points.empty())
         return;
     double res_t = 0.0, res_s = 0.0;
-    mgicp_cloud_resolution(engine_, xyzOf(*target_cloud_), target_cloud_->points.size(), sizeof(pcl::PointXYZRGB), &res_t);
-    mgicp_cloud_resolution(engine_, xyzOf(*source_cloud_), source_cloud_->points.size(), sizeof(pcl::PointXYZRGB), &res_s);
+    int rc = mgicp_cloud_resolution(engine_, xyzOf(*target_cloud_), target_cloud_->points.size(),
+                                    sizeof(pcl::PointXYZRGB), &res_t);
+    if (rc == MGICP_OK)
+        rc = mgicp_cloud_resolution(engine_, xyzOf(*source_cloud_), source_cloud_->points.size(),
+                                    sizeof(pcl::PointXYZRGB), &res_s);
+    if (rc != MGICP_OK)
+    {
+        // no radius, no filtering: leave the cloud as it is rather than filter with radius 0
+        reportEngineError(engine_, rc, "cloud resolution");
+        return;
+    }
     const double radius = (res_t + res_s) * 2.0;
     ROS_INFO("Computing normals with radius: %f", radius);
     std::vector<unsigned char> keep(cloud->points.size(), 0);
-    int rc = mgicp_radius_filter(engine_, xyzOf(*cloud), cloud->points.size(), sizeof(pcl::PointXYZRGB),
-                                 radius, 3, keep.data());
+    rc = mgicp_radius_filter(engine_, xyzOf(*cloud), cloud->points.size(), sizeof(pcl::PointXYZRGB), radius, 3,
+                             keep.data());
     if (rc != MGICP_OK)
     {
         reportEngineError(engine_, rc, "radius filter");

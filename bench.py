@@ -28,11 +28,16 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
-# algorithmic bytes of one objective pass (DESIGN.md "Kernels"): per accepted correspondence
-# source xyz fp32 (12) + matched target xyz fp32 (12) + Mahalanobis upper triangle fp64 (48);
-# rejected source points are compacted away once per outer iteration and cost nothing per pass
-FDF_BYTES_ACCEPTED = 72
-FDF_BYTES_REJECTED = 0
+# Algorithmic bytes per unit, SURVEY.md 8(d) / BASELINE.md section 2 (DESIGN.md "Kernels"):
+#   BFGS objective pass, per accepted correspondence: s 12 + q 12 + M (6 x fp32) 24 + idx 4 = 52 B
+#     (the engine stores M as 6 fp64 for bit parity with PCL's Matrix3d: 72 B actually read per
+#      correspondence, reported as a labelled second figure)
+#   correspondence + Mahalanobis, per source point per outer iteration: s 12 + Cs 24 + NN 12 + Ct 24 = 72 B
+#   k-NN(20) covariance, per point: (k + 1) x 12 + 24 = 276 B
+FDF_BYTES_SURVEY = 52
+FDF_BYTES_STORED = 72
+CORR_BYTES = 72
+COV_BYTES = lambda k: (k + 1) * 12 + 24  # noqa: E731
 
 
 # BASELINE.json configs (C1, the cube plumbing case, is the unit-test fixture, not a bench line)
@@ -60,7 +65,10 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=500_000,
                     help="points per cloud of the bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=1)
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01_pmc_fdf.json"))
+    ap.add_argument("--oracle-full", type=int, default=1,
+                    help="1 = run the oracle on the full workload with all usable host cores "
+                         "(all-core CPU baseline + full-size frob_vs_oracle; rank 0, N = 1 only)")
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r02", "pmc_summary.json"))
     ap.add_argument("--gn-steps", type=int, default=5,
                     help="timed aligns of the opt-in Gauss-Newton mode (MGICP_SOLVER_GN; 0 = skip)")
     ap.add_argument("--fod-cpu-sample", type=int, default=500_000,
@@ -104,6 +112,41 @@ def cpu_baseline(n, threads, occlusion=0.0):
     T, info = g.align()
     rate = info["iterations"] / info["t_loop_s"]
     return rate, info, T, (scan, cad)
+
+
+def host_info():
+    """The GPU box's host CPU as the CPU baseline states it."""
+    model = None
+    try:
+        import subprocess
+
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except Exception:  # noqa: BLE001 -- lscpu absent: report what python sees
+        pass
+    share = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    # the box grants a CPU share (OMP_NUM_THREADS) smaller than the machine (nproc)
+    usable = min(share, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else share
+    return {"lscpu_model": model, "nproc": os.cpu_count(), "sched_affinity": share,
+            "OMP_NUM_THREADS": omp, "threads_used_all_core": usable}
+
+
+def oracle_full(scan, cad, threads, max_iter, fixed, guess=None):
+    """The oracle on the FULL workload with every usable host core (OpenMP): the all-core CPU
+    baseline at the config's own size (no scaling) and the full-size final-transform parity."""
+    from oracle import ref
+
+    g = ref.RefGICP(threads=threads, max_iterations=max_iter, fixed_iterations=fixed)
+    g.set_source(scan)
+    g.set_target(cad)
+    t = time.perf_counter()
+    T, info = g.align(want_trace=True)
+    info["wall_s"] = time.perf_counter() - t
+    return T, info
 
 
 def fod_rows(eng, scan, cad, T_final, n_cpu):
@@ -204,6 +247,7 @@ def main():
     eng.set_profiling(False)
     dt = pg.allreduce_max(dt)
     T_final = eng.getFinalTransformation()
+    trace_final = eng.debug_trace(args.max_iter + 1)  # per-iteration transforms of the last timed align
     result = dict(eng.last_result)
 
     # opt-in Gauss-Newton mode on the same cached grids / covariances (every rank takes part:
@@ -270,43 +314,58 @@ def main():
     value = total_iters / dt
     n_shard = args.n_source // world
     m_shard = result["n_corr"] / world
-    fdf_bytes = m_shard * FDF_BYTES_ACCEPTED + (n_shard - m_shard) * FDF_BYTES_REJECTED
     fdf_ms = kt["fdf"]["avg_ms"]
-    achieved = fdf_bytes / (fdf_ms * 1e-3) / 1e9 if fdf_ms > 0 else None
-    traffic = None
+    pmc = {}
     if os.path.exists(args.pmc_json):
         with open(args.pmc_json) as f:
             pmc = json.load(f)
-        if pmc.get("n_source") == args.n_source and pmc.get("world") == world:
-            traffic = pmc.get("fdf_hbm_bytes_per_launch")
-    roofline = {
-        "kernel": "fdf (BFGS objective pass)",
-        "bound": "hbm",
-        "achieved": round(achieved, 1) if achieved else None,
-        "peak": HBM_PEAK_GBS,
-        "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-        "traffic": traffic,
-        "algorithmic_bytes_per_launch": int(fdf_bytes),
-        "avg_launch_ms": fdf_ms,
-        "launches_timed": kt["fdf"]["count"],
-        "launches": n_evals,
-        "timing": "HIP events on the engine stream around every 8th objective pass of the timed region "
-                  "(identical work per pass; sampling keeps the events' own cost out of value)",
-    }
+        if not (pmc.get("n_source") == args.n_source and pmc.get("world") == world):
+            pmc = {}
+    pmc_k = pmc.get("kernels", {})
+
+    def roof(name, unit_bytes, units, avg_ms, launches_timed, pmc_key, note):
+        """one roofline record: algorithmic bytes (SURVEY 8d per-unit figure x units per launch) /
+        average launch time (HIP events on the engine's stream during the timed region)"""
+        alg = unit_bytes * units
+        ach = alg / (avg_ms * 1e-3) / 1e9 if avg_ms and avg_ms > 0 else None
+        tr = pmc_k.get(pmc_key, {})
+        return {"kernel": name, "bound": "hbm", "achieved": round(ach, 1) if ach else None,
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None,
+                "traffic": tr.get("hbm_bytes_per_launch"), "traffic_note": tr.get("correction"),
+                "bytes_per_unit": unit_bytes, "units_per_launch": int(units),
+                "algorithmic_bytes_per_launch": int(alg), "avg_launch_ms": avg_ms,
+                "launches_timed": launches_timed, "numerator": note}
+
+    roofline = roof("fdf_soa_kernel (BFGS objective pass, dominant: ~48 launches per outer iteration)",
+                    FDF_BYTES_SURVEY, m_shard, fdf_ms, kt["fdf"]["count"], "fdf_soa_kernel",
+                    "SURVEY 8d / BASELINE.md: 52 B per accepted correspondence per pass (M as 6 fp32)")
+    roofline["launches"] = n_evals
+    roofline["timing"] = ("HIP events on the engine stream around every 8th objective pass of the timed region "
+                          "(identical work per pass; sampling keeps the events' own cost out of value)")
+    stored = roof("fdf_soa_kernel", FDF_BYTES_STORED, m_shard, fdf_ms, kt["fdf"]["count"], "fdf_soa_kernel",
+                  "72 B per accepted correspondence: the bytes the pass actually reads (M stored as 6 fp64 "
+                  "for bit parity with PCL's Matrix3d)")
+    roofline["frac_72B_stored"] = stored["frac"]
+    roofline["achieved_72B_stored"] = stored["achieved"]
+    corr_ms = kt["correspond"]["avg_ms"] + kt["compact"]["avg_ms"]
     cov_ms = kt_cov["knn_cov"]["avg_ms"]
+    k = 20
+    rooflines = {
+        "fdf_52B": roofline,
+        "fdf_72B_stored": stored,
+        "correspondence_plus_mahalanobis": roof(
+            "correspond_kernel + compact_kernel (1-NN sweep, Mahalanobis, compaction; once per outer iteration)",
+            CORR_BYTES, n_shard, corr_ms, kt["correspond"]["count"], "correspond_plus_compact",
+            "SURVEY 8d: 72 B per source point (s 12 + Cs 24 + NN 12 + Ct 24)"),
+        "knn_cov": roof(
+            "knn_cov_kernel<20> (k-NN covariances, once per cloud per set_*)", COV_BYTES(k), args.n_target,
+            cov_ms, kt_cov["knn_cov"]["count"], "knn_cov_kernel",
+            "SURVEY 8d: (k+1) x 12 + 24 = 276 B per point"),
+    }
     kernels = {
-        "knn_cov": {"avg_ms": cov_ms, "points": args.n_target,
-                    "algorithmic_GBps": (args.n_target * (21 * 16 + 48)) / (cov_ms * 1e-3) / 1e9 if cov_ms else None},
+        "knn_cov": kt_cov["knn_cov"],
         "correspond": kt["correspond"],
         "compact_mahalanobis": kt["compact"],
-        # correspondence + Mahalanobis = 72 B per source point (s 12, Cs 24, NN 12, Ct 24)
-        "correspond_plus_mahalanobis": {
-            "avg_ms": kt["correspond"]["avg_ms"] + kt["compact"]["avg_ms"],
-            "algorithmic_bytes": 72 * n_shard,
-            "achieved_GBps": (72 * n_shard / ((kt["correspond"]["avg_ms"] + kt["compact"]["avg_ms"]) * 1e-3) / 1e9
-                              if kt["correspond"]["avg_ms"] else None),
-        },
         "fdf": kt["fdf"],
         "reduce_finish": kt["reduce_finish"],
     }
@@ -314,11 +373,12 @@ def main():
     fod = fod_rows(eng, scan, cad, T_final, args.fod_cpu_sample) if args.fod_cpu_sample > 0 and world == 1 else None
     cpu = None
     frob_sample = None
+    full = None
     if args.cpu_sample > 0 and world == 1:  # the CPU baseline is an N=1 figure
         n_cpu = min(args.cpu_sample, args.n_source)
         rate, info, T_cpu, (s_scan, s_cad) = cpu_baseline(n_cpu, args.cpu_threads, args.occlusion)
         scale = n_cpu / args.n_source
-        cpu = {
+        single = {
             "value": rate * scale,
             "unit": "iterations/s",
             "cores": args.cpu_threads,
@@ -331,7 +391,8 @@ def main():
             "sample_rate": rate,
             "sample_frac_scale": scale,
         }
-        # final-transform parity on the sample (the 5M oracle run is not bounded)
+        cpu = dict(single)
+        # final-transform parity on the sample
         e3 = GICPEngine(device=local)
         e3.set_source_xyz(s_scan)
         e3.set_target_xyz(s_cad)
@@ -350,6 +411,39 @@ def main():
             T_egn = e3.align()
             gn["frob_vs_oracle_gn_sample"] = float(np.linalg.norm(T_egn.astype(np.float64) - T_ogn.astype(np.float64)))
         e3.close()
+        host = host_info()
+        cpu["host"] = host
+        if args.oracle_full:
+            # all usable host cores, the FULL workload: the stronger baseline (no scaling) and the
+            # full-size final-transform parity of BASELINE.json's metric
+            nt = host["threads_used_all_core"]
+            T_o, oinfo = oracle_full(scan, cad, nt, args.max_iter, args.fixed)
+            trace_err = (max(float(np.linalg.norm(a.astype(np.float64) - b.astype(np.float64)))
+                             for a, b in zip(trace_final, oinfo["trace"]))
+                         if len(trace_final) == len(oinfo["trace"]) else None)
+            all_rate = oinfo["iterations"] / oinfo["t_loop_s"]
+            full = {
+                "frob_vs_oracle": float(np.linalg.norm(T_final.astype(np.float64) - T_o.astype(np.float64))),
+                "iterations_gpu": iters_per_align, "iterations_oracle": oinfo["iterations"],
+                "converged_oracle": bool(oinfo["converged"]),
+                "max_trace_frob_vs_oracle": trace_err,
+                "oracle_threads": nt,
+            }
+            cpu = {
+                "value": all_rate,
+                "unit": "iterations/s",
+                "cores": nt,
+                "kind": "port",
+                "sample": (f"oracle/gicp_ref.c with OpenMP on {nt} threads over the FULL {args.n_source}<->"
+                           f"{args.n_target} workload (no scaling): {oinfo['iterations']} iterations in "
+                           f"{oinfo['t_loop_s']:.2f} s loop, covariances + kd-trees {oinfo['t_cov_s']:.2f} s, "
+                           f"ms-to-converge {1e3 * oinfo['t_total_s']:.0f} ms"),
+                "ms_to_converge": 1e3 * oinfo["t_total_s"],
+                "host": host,
+                "single_thread": single,
+                "gpu_over_all_core": value / all_rate,
+                "gpu_over_single_thread": value / single["value"],
+            }
 
     line = {
         "metric": ("GICP iterations/sec, 5M<->5M scan-vs-CAD (PCL-1.8.1-faithful BFGS GICP)" if args.config == "C4"
@@ -380,8 +474,11 @@ def main():
         "ms_to_converge_new_clouds_warm_process": new_clouds,
         "ms_to_converge_first_detail": {k: round(first[k], 3) for k in ("ms_upload", "ms_prep", "ms_loop")},
         "ms_to_converge_cached": round(1e3 * dt / args.steps, 3),
+        "frob_vs_oracle": full["frob_vs_oracle"] if full else None,
+        "parity_full_size": full,
         "frob_vs_oracle_sample": frob_sample,
         "roofline": roofline,
+        "rooflines": rooflines,
         "kernels": kernels,
         "cpu_baseline": cpu,
         "gn_mode": gn,

@@ -51,7 +51,7 @@ typedef struct {
     double rot_eps;         /* GICP rotation_epsilon_                (PCL default 2e-3) */
     double max_corr_dist;   /* setMaxCorrespondenceDistance          (GICPAlignment.cpp:51; default 0.04) */
     double gicp_eps;        /* GICP gicp_epsilon_                    (PCL default 1e-3) */
-    int    k;               /* GICP k_correspondences_               (PCL default 20; max 32) */
+    int    k;               /* GICP k_correspondences_               (PCL default 20; any k in [1, 32]) */
     int    max_inner_iter;  /* GICP max_inner_iterations_            (PCL default 20) */
     int    solver;          /* MGICP_SOLVER_* */
     int    device;          /* HIP device ordinal; -1 = current device */
@@ -114,13 +114,15 @@ int mgicp_transform_cloud(mgicp_ctx* ctx, const float T_cm[16], const float* in,
 
 /* ---- helpers of GICPAlignment(use_covariances = true) ----
  * Utils::computeCloudResolution (src/Utils.cpp:145-174): mean distance from each point to its
- * nearest other point (the 2nd of a 2-NN query), fp64 sum of float sqrt. */
+ * nearest other point (the 2nd of a 2-NN query), fp64 sum of float sqrt.  Non-finite records are
+ * skipped as queries and as neighbours (0 when fewer than 2 finite points remain). */
 int mgicp_cloud_resolution(mgicp_ctx* ctx, const float* xyz, size_t n, size_t stride_bytes,
                            double* out);
 /* The NaN-normal removal of GICPAlignment::getCovariances (src/GICPAlignment.cpp:56-71):
  * pcl::NormalEstimation yields a NaN normal when fewer than 3 points (self included) lie
  * within the search radius (KdTreeFLANN::radiusSearch: float d^2 < float(radius^2)).
- * keep[i] = 1 iff at least min_neighbors such points exist. */
+ * keep[i] = 1 iff record i is finite and at least min_neighbors finite points (itself included)
+ * lie within the radius; non-finite records always get keep[i] = 0 (NaN normal). */
 int mgicp_radius_filter(mgicp_ctx* ctx, const float* xyz, size_t n, size_t stride_bytes,
                         double radius, int min_neighbors, unsigned char* keep);
 

@@ -111,8 +111,42 @@ def header_symbols(path: str = HEADER_PATH) -> list[str]:
     return sorted(set(re.findall(r"\b(mgicp_[a-z_0-9]+)\s*\(", text)))
 
 
+def _mapped_hip_runtimes() -> set[str]:
+    """Real paths of every HIP runtime (libamdhip64*) mapped into this process."""
+    out = set()
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                parts = line.split(None, 5)
+                if len(parts) == 6 and "libamdhip64" in os.path.basename(parts[5].strip()):
+                    out.add(os.path.realpath(parts[5].strip()))
+    except OSError:  # no procfs: nothing to check against
+        pass
+    return out
+
+
+def _rocm_lib_dir() -> str:
+    return os.path.realpath(os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "lib"))
+
+
+def check_single_hip_runtime(when: str) -> None:
+    """libmgicp.so links ROCm's HIP runtime (/opt/rocm/lib/libamdhip64.so.7).  A second HIP runtime
+    in the same process -- torch bundles its own (torch/lib/libamdhip64.so, a different ROCm
+    release) and maps it at `import torch` -- was observed to corrupt the heap on MI355X ("double
+    free or corruption" at teardown, round 1, parallel.py).  Refuse that combination loudly."""
+    libs = _mapped_hip_runtimes()
+    foreign = sorted(p for p in libs if os.path.dirname(p) != _rocm_lib_dir())
+    if foreign or len(libs) > 1:
+        raise MgicpError(
+            MGICP_E_HIP,
+            f"{when}: another HIP runtime is mapped in this process ({', '.join(sorted(libs))}); libmgicp.so "
+            f"uses {_rocm_lib_dir()}/libamdhip64.so and two HIP runtimes in one process corrupt the heap. "
+            "Do not import torch (or anything bundling its own HIP runtime) in a process that uses libmgicp.so.")
+
+
 def load() -> ctypes.CDLL:
-    """Load the in-tree libmgicp.so; raise loudly when it is absent (no fallback path)."""
+    """Load the in-tree libmgicp.so; raise loudly when it is absent (no fallback path) or when a
+    second HIP runtime is (or would become) mapped next to it."""
     global _lib
     if _lib is not None:
         return _lib
@@ -120,7 +154,9 @@ def load() -> ctypes.CDLL:
         raise ImportError(
             f"{LIB_PATH} not found: build the HIP engine first (python -c 'import __graft_entry__ as g; g.build()' "
             "or `make`). There is no CPU fallback.")
+    check_single_hip_runtime("before loading libmgicp.so")
     lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    check_single_hip_runtime("after loading libmgicp.so")
     for name, (res, args) in _SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = res

@@ -413,7 +413,9 @@ int upload_cloud(mgicp_ctx* ctx, Cloud& cl, const float* xyz, size_t n, size_t s
   cl.have_cov = false;
   if (&cl == &ctx->src) ctx->qperm_valid = false;
   if (&cl == &ctx->src || &cl == &ctx->tgt) {
+    // the previous sweep's matches index the old clouds: never seed from / reuse them
     ctx->have_corr = false;
+    ctx->seed_valid = false;
     ctx->ms_upload_pending += now_ms() - t0;
   }
   return MGICP_OK;
@@ -599,6 +601,10 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
   cl.n_built = n;
   cl.dirty = false;
   cl.have_cov = false;
+  if (&cl == &ctx->src || &cl == &ctx->tgt) {  // sorted positions changed
+    ctx->have_corr = false;
+    ctx->seed_valid = false;
+  }
   return MGICP_OK;
 }
 
@@ -1036,9 +1042,8 @@ int estimate_gn(mgicp_ctx* ctx, Mat4& T, int* n_corr) {
 }
 
 int check_params(mgicp_ctx* ctx, const mgicp_params& p) {
-  const int k = p.k;
-  if (!(k == 5 || k == 10 || k == 15 || k == 20 || k == 25 || k == 30))
-    return fail(ctx, MGICP_E_INVALID, "k must be one of 5, 10, 15, 20, 25, 30");
+  if (p.k < 1 || p.k > kMaxK)
+    return fail(ctx, MGICP_E_INVALID, "k (k_correspondences) must be in [1, 32]");
   if (p.max_iter < 1 || p.max_inner_iter < 1 || !(p.max_corr_dist >= 0) || !(p.rot_eps > 0) ||
       !(p.tf_eps >= 0) ||
       (p.solver != MGICP_SOLVER_PCL_BFGS && p.solver != MGICP_SOLVER_GN))
@@ -1377,12 +1382,20 @@ int mgicp_cloud_resolution(mgicp_ctx* ctx, const float* xyz, size_t n, size_t st
   *out = 0.0;
   if (n < 2) return MGICP_OK;  // no point has a 2nd neighbour: res stays 0
   int rc = upload_cloud(ctx, ctx->aux, xyz, n, stride, false);
-  if (rc || (rc = build_grid(ctx, ctx->aux))) return rc;
-  const int nb = static_cast<int>((n + 255) / 256);
+  if (rc) return rc;
+  // Utils::computeCloudResolution skips non-finite points and its KdTree holds only finite ones
+  // (src/Utils.cpp:152-160): grid and queries over the finite points
+  ctx->aux.drop_nonfinite = true;
+  rc = build_grid(ctx, ctx->aux);
+  ctx->aux.drop_nonfinite = false;
+  if (rc) return rc;
+  const size_t nf = ctx->aux.n;
+  if (nf < 2) return MGICP_OK;  // nearestKSearch never returns 2: n_points = 0, res = 0
+  const int nb = static_cast<int>((nf + 255) / 256);
   HIPCK(ctx->partial.reserve(static_cast<size_t>(nb) * kRedVals));
   HIPCK(ctx->red.reserve(kRedVals));
   if ((rc = ensure_host_red(ctx))) return rc;
-  HIPCK(launch_resolution(ctx->aux.view, n, ctx->partial.p, nb, ctx->stream));
+  HIPCK(launch_resolution(ctx->aux.view, nf, ctx->partial.p, nb, ctx->stream));
   HIPCK(launch_reduce_finish(ctx->partial.p, nb, ctx->red.p, ctx->stream));
   HIPCK(hipMemcpyAsync(ctx->h_red, ctx->red.p, kRedVals * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
   if ((rc = sync(ctx))) return rc;
@@ -1397,11 +1410,19 @@ int mgicp_radius_filter(mgicp_ctx* ctx, const float* xyz, size_t n, size_t strid
   HIPCK(hipSetDevice(ctx->device));
   if (n == 0) return MGICP_OK;
   int rc = upload_cloud(ctx, ctx->aux, xyz, n, stride, false);
-  if (rc || (rc = build_grid(ctx, ctx->aux))) return rc;
+  if (rc) return rc;
+  // NormalEstimation gives non-finite points NaN normals and searches a tree of the finite points
+  // only: grid over the finite points, keep = 0 for every other record
+  ctx->aux.drop_nonfinite = true;
+  rc = build_grid(ctx, ctx->aux);
+  ctx->aux.drop_nonfinite = false;
+  if (rc) return rc;
   DevBuf<unsigned char> d_keep;
   HIPCK(d_keep.reserve(n));
+  HIPCK(hipMemsetAsync(d_keep.p, 0, n, ctx->stream));
   const float r2 = static_cast<float>(radius * radius);
-  HIPCK(launch_radius_keep(ctx->aux.view, n, r2, min_neighbors, d_keep.p, ctx->stream));
+  // one query per finite point; the kernel scatters keep[] through the original index in w
+  HIPCK(launch_radius_keep(ctx->aux.view, ctx->aux.n, r2, min_neighbors, d_keep.p, ctx->stream));
   HIPCK(hipMemcpyAsync(keep, d_keep.p, n, hipMemcpyDeviceToHost, ctx->stream));
   rc = sync(ctx);
   d_keep.release();
@@ -1586,6 +1607,7 @@ int mgicp_comm_init(mgicp_ctx* ctx, int nranks, int rank, const unsigned char id
   ctx->qperm_valid = false;
   ctx->src.have_cov = false;
   ctx->have_corr = false;
+  ctx->seed_valid = false;  // the shard (and its per-point match buffers) changes
   // id == NULL: detached shard (debug entry points only).  nranks == 1 with an id builds a real
   // one-rank communicator, so the collective code path can be exercised on a single device.
   if (!id) return MGICP_OK;

@@ -51,6 +51,7 @@ struct CorrSoA {
 // Number of values reduced per objective pass:
 //   [0] f-sum  [1..3] g_t sum  [4..12] Rsum (row-major)  [13] count  [14..15] pad
 constexpr int kRedVals = 16;
+constexpr int kMaxK = 32;  // largest k_correspondences_ the covariance kernel serves
 constexpr int kRedThreads = 256;
 // Number of values reduced per Gauss-Newton moment pass (MGICP_SOLVER_GN):
 //   [0] sum r0'M r0  [1..12] sum (M r0) w'  [13..72] sum M_p (w w')_q  [73] count  [74..79] pad

@@ -178,7 +178,10 @@ __device__ __forceinline__ void ring_search(const GridView& g, float qx, float q
   }
 }
 
-// exact k-NN visitor: register-resident sorted list of (d2, index) keys
+// exact k-NN visitor: register-resident sorted list of (d2, index) keys.  A runtime k < K is
+// served by the K-slot list with its first K - k slots pre-filled with the sentinel key 0: every
+// real key is >= 0 and an insert never moves in front of an equal key, so the sentinels stay in
+// front and slots [K - k, K) hold the k nearest in (d2, index) order.
 template <int K>
 struct KnnVisitor {
   static constexpr bool kNearFirst = true;
@@ -186,10 +189,10 @@ struct KnnVisitor {
   unsigned long long key[K];
   uint32_t pos[K];
 
-  __device__ __forceinline__ void init(float x, float y, float z) {
+  __device__ __forceinline__ void init(float x, float y, float z, int nsent = 0) {
     qx = x; qy = y; qz = z;
 #pragma unroll
-    for (int k = 0; k < K; ++k) { key[k] = ~0ull; pos[k] = 0u; }
+    for (int k = 0; k < K; ++k) { key[k] = k < nsent ? 0ull : ~0ull; pos[k] = 0u; }
   }
   __device__ __forceinline__ bool done(float Ls) const {
     if (key[K - 1] == ~0ull || !(Ls > 0.f)) return false;
@@ -477,22 +480,24 @@ __device__ __forceinline__ double sel3(int i, double a, double b, double c) {
 }
 
 // `perm` (optional): query order over [p0, p1) (Morton order: compact 3-D patch per wave)
+// k = K - nsent neighbours (nsent > 0 only on the generic rounded-up instantiations)
 template <int K>
 __global__ __launch_bounds__(256, MGICP_COV_WAVES) void knn_cov_kernel(GridView g, double eps, size_t p0,
                                                       size_t p1, Cov3 cov,
-                                                      const uint32_t* __restrict__ perm) {
+                                                      const uint32_t* __restrict__ perm, int nsent) {
   const size_t t = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (t >= p1 - p0) return;
   const size_t p = p0 + (perm ? perm[t] : t);
   const float4 q = g.pts[p];
   KnnVisitor<K> vis;
-  vis.init(q.x, q.y, q.z);
+  vis.init(q.x, q.y, q.z, nsent);
   ring_search(g, q.x, q.y, q.z, vis);
 
   double m0 = 0.0, m1 = 0.0, m2 = 0.0;
   double a[3][3] = {{0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}};
 #pragma unroll
   for (int k = 0; k < K; ++k) {
+    if (k < nsent) continue;
     const float4 pt = g.pts[vis.pos[k]];
     m0 += pt.x;
     m1 += pt.y;
@@ -504,7 +509,7 @@ __global__ __launch_bounds__(256, MGICP_COV_WAVES) void knn_cov_kernel(GridView 
     a[2][1] += static_cast<double>(pt.z * pt.y);
     a[2][2] += static_cast<double>(pt.z * pt.z);
   }
-  const double kd = static_cast<double>(K);
+  const double kd = static_cast<double>(K - nsent);
   double mean[3] = {m0 / kd, m1 / kd, m2 / kd};
 #pragma unroll
   for (int i = 0; i < 3; ++i)
@@ -1237,23 +1242,30 @@ hipError_t launch_iota(uint32_t* v, size_t n, hipStream_t s) {
 
 template <int K>
 static hipError_t knn_cov_k(const GridView& g, double eps, size_t p0, size_t p1, Cov3 cov,
-                            const uint32_t* perm, hipStream_t s) {
-  knn_cov_kernel<K><<<nblk(p1 - p0), 256, 0, s>>>(g, eps, p0, p1, cov, perm);
+                            const uint32_t* perm, int k, hipStream_t s) {
+  knn_cov_kernel<K><<<nblk(p1 - p0), 256, 0, s>>>(g, eps, p0, p1, cov, perm, K - k);
   return hipGetLastError();
 }
 
+// exact instantiations for PCL's default (20) and its round neighbours; any other k in
+// [1, kMaxK] runs on the next multiple of 8 with K - k sentinel slots
 hipError_t launch_knn_cov(const GridView& g, int k, double eps, size_t p0, size_t p1, Cov3 cov,
                           const uint32_t* perm, hipStream_t s) {
   if (p1 <= p0) return hipSuccess;
   switch (k) {
-    case 5: return knn_cov_k<5>(g, eps, p0, p1, cov, perm, s);
-    case 10: return knn_cov_k<10>(g, eps, p0, p1, cov, perm, s);
-    case 15: return knn_cov_k<15>(g, eps, p0, p1, cov, perm, s);
-    case 20: return knn_cov_k<20>(g, eps, p0, p1, cov, perm, s);
-    case 25: return knn_cov_k<25>(g, eps, p0, p1, cov, perm, s);
-    case 30: return knn_cov_k<30>(g, eps, p0, p1, cov, perm, s);
-    default: return hipErrorInvalidValue;
+    case 5: return knn_cov_k<5>(g, eps, p0, p1, cov, perm, k, s);
+    case 10: return knn_cov_k<10>(g, eps, p0, p1, cov, perm, k, s);
+    case 15: return knn_cov_k<15>(g, eps, p0, p1, cov, perm, k, s);
+    case 20: return knn_cov_k<20>(g, eps, p0, p1, cov, perm, k, s);
+    case 25: return knn_cov_k<25>(g, eps, p0, p1, cov, perm, k, s);
+    case 30: return knn_cov_k<30>(g, eps, p0, p1, cov, perm, k, s);
+    default: break;
   }
+  if (k < 1 || k > kMaxK) return hipErrorInvalidValue;
+  if (k <= 8) return knn_cov_k<8>(g, eps, p0, p1, cov, perm, k, s);
+  if (k <= 16) return knn_cov_k<16>(g, eps, p0, p1, cov, perm, k, s);
+  if (k <= 24) return knn_cov_k<24>(g, eps, p0, p1, cov, perm, k, s);
+  return knn_cov_k<32>(g, eps, p0, p1, cov, perm, k, s);
 }
 
 hipError_t launch_correspond(const GridView& tgt, const float4* src, size_t p0, size_t p1, Xf34 T,
@@ -1440,6 +1452,10 @@ hipError_t preload_kernels(void* pinned, size_t pinned_bytes, hipStream_t s) {
       reinterpret_cast<const void*>(&knn_cov_kernel<20>),
       reinterpret_cast<const void*>(&knn_cov_kernel<25>),
       reinterpret_cast<const void*>(&knn_cov_kernel<30>),
+      reinterpret_cast<const void*>(&knn_cov_kernel<8>),
+      reinterpret_cast<const void*>(&knn_cov_kernel<16>),
+      reinterpret_cast<const void*>(&knn_cov_kernel<24>),
+      reinterpret_cast<const void*>(&knn_cov_kernel<32>),
       reinterpret_cast<const void*>(&correspond_kernel),
       reinterpret_cast<const void*>(&morton_key_kernel),
       reinterpret_cast<const void*>(&compact_kernel),

@@ -7,16 +7,26 @@ Control path (this module): a tiny TCP rendezvous for the id broadcast, barriers
 max-over-ranks timer.  It deliberately does not use torch.distributed: importing torch loads
 torch's own bundled HIP/HSA runtime (torch/lib/libamdhip64.so, ROCm 7.0) next to the ROCm 7.2
 runtime libmgicp.so links, and two HIP runtimes in one process corrupt the heap at teardown
-(observed on MI355X: "double free or corruption").  Processes are still launched by
-`python -m torch.distributed.run`, which only sets RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT.
+(observed on MI355X: "double free or corruption"; _lib.load() now refuses that combination).
+Processes are still launched by `python -m torch.distributed.run`, which only sets RANK /
+WORLD_SIZE / MASTER_ADDR / MASTER_PORT.
+
+Wire format: nothing is unpickled.  Every message is a typed frame (1-byte tag, 4-byte length,
+payload): raw bytes, one little-endian float64, or "none".  A connecting peer first sends a
+fixed hello (magic, rank as int32, and the SHA-256 of MGICP_CTRL_SECRET when that variable is
+set); rank 0 accepts only ranks 1..world-1, each once, and drops any other connection.
 """
 from __future__ import annotations
 
+import hashlib
 import os
-import pickle
 import socket
 import struct
 import time
+
+_MAGIC = b"MGICPRV1"
+_T_NONE, _T_BYTES, _T_F64 = 0, 1, 2
+_MAX_FRAME = 1 << 20  # control messages are tiny (the unique id is 128 bytes)
 
 
 def shard_range(n: int, world: int, rank: int) -> tuple[int, int]:
@@ -25,9 +35,27 @@ def shard_range(n: int, world: int, rank: int) -> tuple[int, int]:
     return n * rank // world, n * (rank + 1) // world
 
 
+def _secret_digest() -> bytes:
+    s = os.environ.get("MGICP_CTRL_SECRET", "")
+    return hashlib.sha256(s.encode()).digest() if s else bytes(32)
+
+
+def _encode(obj) -> bytes:
+    if obj is None:
+        tag, payload = _T_NONE, b""
+    elif isinstance(obj, (bytes, bytearray)):
+        tag, payload = _T_BYTES, bytes(obj)
+    elif isinstance(obj, (int, float)):
+        tag, payload = _T_F64, struct.pack("<d", float(obj))
+    else:
+        raise TypeError(f"rendezvous carries bytes, float or None, not {type(obj).__name__}")
+    if len(payload) > _MAX_FRAME:
+        raise ValueError("rendezvous frame too large")
+    return struct.pack("<BI", tag, len(payload)) + payload
+
+
 def _send(sock: socket.socket, obj) -> None:
-    data = pickle.dumps(obj)
-    sock.sendall(struct.pack("<Q", len(data)) + data)
+    sock.sendall(_encode(obj))
 
 
 def _recv_exact(sock: socket.socket, n: int) -> bytes:
@@ -41,8 +69,36 @@ def _recv_exact(sock: socket.socket, n: int) -> bytes:
 
 
 def _recv(sock: socket.socket):
-    (n,) = struct.unpack("<Q", _recv_exact(sock, 8))
-    return pickle.loads(_recv_exact(sock, n))
+    tag, n = struct.unpack("<BI", _recv_exact(sock, 5))
+    if n > _MAX_FRAME:
+        raise ConnectionError("rendezvous frame too large")
+    payload = _recv_exact(sock, n)
+    if tag == _T_NONE and n == 0:
+        return None
+    if tag == _T_BYTES:
+        return payload
+    if tag == _T_F64 and n == 8:
+        return struct.unpack("<d", payload)[0]
+    raise ConnectionError(f"malformed rendezvous frame (tag {tag}, {n} bytes)")
+
+
+def _hello(rank: int) -> bytes:
+    return _MAGIC + struct.pack("<i", rank) + _secret_digest()
+
+
+_HELLO_LEN = len(_MAGIC) + 4 + 32
+
+
+def _check_hello(data: bytes, world: int, seen: dict) -> int | None:
+    """The peer's rank when its hello is well-formed, authorised and new; else None."""
+    if len(data) != _HELLO_LEN or data[:len(_MAGIC)] != _MAGIC:
+        return None
+    (r,) = struct.unpack("<i", data[len(_MAGIC):len(_MAGIC) + 4])
+    if data[len(_MAGIC) + 4:] != _secret_digest():
+        return None
+    if not (1 <= r < world) or r in seen:
+        return None
+    return r
 
 
 class Rendezvous:
@@ -65,13 +121,27 @@ class Rendezvous:
             srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
             srv.bind((addr, port))
             srv.listen(world)
-            srv.settimeout(timeout)
-            peers = {}
-            while len(peers) < world - 1:
-                conn, _ = srv.accept()
-                conn.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-                peers[_recv(conn)] = conn
-            srv.close()
+            peers: dict[int, socket.socket] = {}
+            try:
+                while len(peers) < world - 1:
+                    left = deadline - time.time()
+                    if left <= 0:
+                        raise TimeoutError(f"rendezvous: {len(peers)} of {world - 1} peers joined")
+                    srv.settimeout(left)
+                    conn, _ = srv.accept()
+                    conn.settimeout(min(10.0, max(0.1, left)))
+                    try:
+                        r = _check_hello(_recv_exact(conn, _HELLO_LEN), world, peers)
+                    except (OSError, ConnectionError):
+                        r = None
+                    if r is None:  # bogus, unauthorised or duplicate peer: drop it, keep waiting
+                        conn.close()
+                        continue
+                    conn.settimeout(timeout)
+                    conn.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+                    peers[r] = conn
+            finally:
+                srv.close()
             self.peers = [peers[r] for r in range(1, world)]
         else:
             while True:
@@ -84,11 +154,11 @@ class Rendezvous:
                     time.sleep(0.05)
             s.settimeout(timeout)
             s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-            _send(s, rank)
+            s.sendall(_hello(rank))
             self.sock = s
 
     def broadcast(self, obj=None):
-        """Rank 0's `obj` to every rank."""
+        """Rank 0's `obj` (bytes, float or None) to every rank."""
         if self.world == 1:
             return obj
         if self.rank == 0:
@@ -107,7 +177,7 @@ class Rendezvous:
         return None
 
     def allreduce_max(self, x: float) -> float:
-        vals = self.gather(x)
+        vals = self.gather(float(x))
         return self.broadcast(max(vals) if self.rank == 0 else None)
 
     def barrier(self) -> None:

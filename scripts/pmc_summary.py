@@ -1,19 +1,27 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 --pmc counter CSVs into per-launch HBM bytes of one kernel.
+"""Summarise rocprofv3 --pmc counter CSVs into per-launch HBM bytes of the path's kernels.
 
-Corrections follow /opt/skills/guides/MI355X_MICROARCH.md "HBM" (and cdna_hip_programming.md
-section 7): FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports exactly half of
-the bytes of a wide (16 B/lane) coalesced streaming read, so it is doubled here -- the objective
-pass reads only 16-byte-per-lane vectors (float4, double2).  WRITE_SIZE is taken as is.
-FETCH_SIZE and WRITE_SIZE were collected in separate --pmc passes (slot limits).
+Corrections follow /opt/skills/guides/MI355X_MICROARCH.md "HBM": FETCH_SIZE / WRITE_SIZE are in
+KiB; on gfx950 FETCH_SIZE reports exactly HALF of the bytes of a wide (16 B/lane) coalesced
+STREAMING read, and "other access widths are uncalibrated".  So the x2 correction is applied per
+kernel only where the kernel's reads are all 16-byte-per-lane coalesced streams:
+  * fdf_soa_kernel -- every load is a float4 / double2 stream at consecutive addresses: x2;
+  * correspond_kernel, knn_cov_kernel, fitness / segdiff (grid gathers), compact_kernel and
+    gn_moments_kernel (coalesced 4 B index loads mixed with 16 B gathers): raw FETCH_SIZE,
+    labelled uncalibrated -- the true HBM bytes lie between 1x and 2x the raw figure.
+WRITE_SIZE is taken as is.  FETCH_SIZE and WRITE_SIZE come from separate --pmc passes.
 
-usage: pmc_summary.py FETCH_DIR WRITE_DIR KERNEL_SUBSTR N_SOURCE WORLD OUT_JSON
+usage: pmc_summary.py FETCH_DIR WRITE_DIR N_SOURCE WORLD OUT_JSON
 """
 import csv
 import glob
 import json
 import os
 import sys
+
+STREAMING = {"fdf_soa_kernel"}
+KERNELS = ("fdf_soa_kernel", "correspond_kernel", "compact_kernel", "knn_cov_kernel", "fitness_kernel",
+           "gn_moments_kernel", "segdiff_kernel", "voxel_key_kernel", "voxel_centroid_kernel")
 
 
 def per_dispatch(directory, counter, kernel):
@@ -26,35 +34,39 @@ def per_dispatch(directory, counter, kernel):
     return vals
 
 
-def main():
-    fdir, wdir, kernel, n_source, world, out = sys.argv[1:7]
-    fetch = per_dispatch(fdir, "FETCH_SIZE", kernel)
-    write = per_dispatch(wdir, "WRITE_SIZE", kernel)
-    if not fetch or not write:
-        raise SystemExit(f"no counters found for {kernel}: fetch={len(fetch)} write={len(write)}")
-    f_kib = sum(fetch) / len(fetch)
-    w_kib = sum(write) / len(write)
-    hbm = 2.0 * f_kib * 1024 + w_kib * 1024
-    res = {
-        "kernel": kernel,
-        "n_source": int(n_source),
-        "world": int(world),
-        "dispatches_fetch": len(fetch),
-        "dispatches_write": len(write),
+def entry(fk, wk, streaming):
+    f_kib = sum(fk) / len(fk)
+    w_kib = sum(wk) / len(wk)
+    mult = 2.0 if streaming else 1.0
+    return {
+        "dispatches": len(fk),
         "fetch_size_kib_raw_avg": f_kib,
         "write_size_kib_raw_avg": w_kib,
-        "fdf_hbm_bytes_per_launch": hbm,
-        "correction": "bytes = 2*FETCH_SIZE*1024 (gfx950 wide-read halving) + WRITE_SIZE*1024",
+        "hbm_bytes_per_launch": mult * f_kib * 1024 + w_kib * 1024,
+        "correction": ("2 x FETCH_SIZE x 1024 (gfx950 wide streaming read halving) + WRITE_SIZE x 1024"
+                       if streaming else
+                       "raw FETCH_SIZE x 1024 + WRITE_SIZE x 1024; gather / mixed access widths are "
+                       "uncalibrated on gfx950: true HBM bytes between 1x and 2x the raw fetch"),
     }
-    # the other kernels of the path, for DESIGN.md (same correction; gathers use 16 B/lane loads)
-    others = {}
-    for k in ("correspond_kernel", "compact_kernel", "knn_cov_kernel", "xform_points", "fitness_kernel",
-              "gn_moments_kernel", "segdiff_kernel", "voxel_key_kernel", "voxel_centroid_kernel"):
+
+
+def main():
+    fdir, wdir, n_source, world, out = sys.argv[1:6]
+    kernels = {}
+    for k in KERNELS:
         fk, wk = per_dispatch(fdir, "FETCH_SIZE", k), per_dispatch(wdir, "WRITE_SIZE", k)
         if fk and wk:
-            others[k] = {"dispatches": len(fk),
-                         "hbm_bytes_per_launch": 2.0 * sum(fk) / len(fk) * 1024 + sum(wk) / len(wk) * 1024}
-    res["other_kernels"] = others
+            kernels[k] = entry(fk, wk, k in STREAMING)
+    if "correspond_kernel" in kernels and "compact_kernel" in kernels:
+        a, b = kernels["correspond_kernel"], kernels["compact_kernel"]
+        kernels["correspond_plus_compact"] = {
+            "hbm_bytes_per_launch": a["hbm_bytes_per_launch"] + b["hbm_bytes_per_launch"],
+            "correction": a["correction"],
+        }
+    if "fdf_soa_kernel" not in kernels:
+        raise SystemExit("no counters found for fdf_soa_kernel")
+    res = {"n_source": int(n_source), "world": int(world), "kernels": kernels,
+           "fdf_hbm_bytes_per_launch": kernels["fdf_soa_kernel"]["hbm_bytes_per_launch"]}
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res))

@@ -105,3 +105,35 @@ def test_cabi_example_plain_cpp_host():
     out = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "cabi_example: OK" in out.stdout
+
+
+def test_second_hip_runtime_is_refused():
+    """the observed "double free or corruption" with torch's bundled HIP runtime next
+    to ROCm's (parallel.py) is now a guard: _lib.load() raises MgicpError when another libamdhip64
+    is mapped.  Run in a child process (import torch maps torch/lib/libamdhip64.so)."""
+    import subprocess
+    import sys
+
+    code = ("import torch, sys; sys.path.insert(0, %r)\n"
+            "from leica_point_cloud_processing_amd import _lib\n"
+            "try:\n    _lib.load()\nexcept _lib.MgicpError as e:\n    print('REFUSED', e.code)\n"
+            "else:\n    print('LOADED')\n") % ROOT
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert "REFUSED -5" in r.stdout, r.stdout + r.stderr
+    # and the plain process (no torch) loads it
+    code2 = ("import sys; sys.path.insert(0, %r)\nfrom leica_point_cloud_processing_amd import _lib\n"
+             "_lib.load(); print('LOADED', sorted(_lib._mapped_hip_runtimes()))\n") % ROOT
+    r2 = subprocess.run([sys.executable, "-c", code2], capture_output=True, text=True, timeout=300)
+    assert "LOADED" in r2.stdout and "torch" not in r2.stdout, r2.stdout + r2.stderr
+
+
+@pytest.mark.parametrize("k", [0, 33, -1])
+def test_k_out_of_range_is_invalid(k):
+    """k_correspondences outside [1, 32] is refused before any device work (include/mi355x_gicp.h)."""
+    from leica_point_cloud_processing_amd import _lib
+
+    lib = _lib.load()
+    p = _lib.default_params()
+    p.k = k
+    h = ctypes.c_void_p()
+    assert lib.mgicp_create(ctypes.byref(h), ctypes.byref(p)) == _lib.MGICP_E_INVALID

@@ -107,6 +107,64 @@ def test_rendezvous_control_plane(world):
     assert all(mx == world - 0.5 for _, _, mx in res)
 
 
+def _bogus_then_real(port, q):
+    """A pickle payload and an out-of-range rank arrive before the real rank 1: rank 0 must drop
+    them (nothing is unpickled) and finish the rendezvous."""
+    import pickle
+    import struct
+    import time as _t
+
+    from leica_point_cloud_processing_amd import parallel
+
+    def connect():
+        for _ in range(200):
+            try:
+                return socket.create_connection(("127.0.0.1", port), timeout=5.0)
+            except OSError:
+                _t.sleep(0.05)
+        raise RuntimeError("no server")
+
+    class Boom:
+        def __reduce__(self):
+            return (os._exit, (3,))
+
+    s1 = connect()
+    s1.sendall(struct.pack("<Q", 64) + pickle.dumps(Boom()).ljust(64, b"\0"))
+    s2 = connect()
+    s2.sendall(parallel._hello(7))  # rank outside 1..world-1
+    real = parallel.Rendezvous(1, 2, addr="127.0.0.1", port=port, timeout=60)
+    uid = real.broadcast(None)
+    real.barrier()
+    q.put(uid)
+    real.close()
+    for s in (s1, s2):
+        s.close()
+
+
+def test_rendezvous_rejects_bogus_peers():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    peer = ctx.Process(target=_bogus_then_real, args=(port, q))
+    peer.start()
+    from leica_point_cloud_processing_amd.parallel import Rendezvous
+
+    r = Rendezvous(0, 2, addr="127.0.0.1", port=port, timeout=60)
+    r.broadcast(bytes(range(128)))
+    r.barrier()
+    assert q.get(timeout=60) == bytes(range(128))
+    peer.join(timeout=30)
+    assert peer.exitcode == 0
+    r.close()
+    from leica_point_cloud_processing_amd.parallel import _check_hello, _encode, _hello
+
+    with pytest.raises(TypeError):
+        _encode({"not": "allowed"})
+    assert _check_hello(_hello(1), 3, {}) == 1
+    assert _check_hello(_hello(1), 3, {1: None}) is None  # duplicate rank
+    assert _check_hello(_hello(0), 3, {}) is None and _check_hello(_hello(3), 3, {}) is None
+
+
 def test_shard_ranges_partition():
     from leica_point_cloud_processing_amd.parallel import shard_range
 

@@ -165,3 +165,65 @@ def test_covariance_path_filter(part_small):
         exp[i] = int((d2 < r2).sum()) >= 3
     np.testing.assert_array_equal(keep, exp)
     assert 0 < exp.sum() < len(pts)
+
+
+@pytest.mark.gpu
+def test_covariance_path_nonfinite_records(part_small):
+    """ADVICE r01: non-finite records on the use_covariances path.  Utils::computeCloudResolution
+    skips them as queries and its KdTree never holds them (src/Utils.cpp:152-160);
+    NormalEstimation gives them NaN normals, so getCovariances drops them (GICPAlignment.cpp:62-67).
+    The GICP that follows then runs on finite clouds (PCL: same as the oracle on the kept points)."""
+    from leica_point_cloud_processing_amd.engine import GICPEngine
+    from leica_point_cloud_processing_amd.gicp_alignment import GICPAlignment
+    from oracle import ref
+
+    scan, cad, _ = part_small
+    bad = scan.copy()
+    rng = np.random.default_rng(3)
+    idx = rng.choice(len(bad), 50, replace=False)
+    bad[idx[:20], 0] = np.nan
+    bad[idx[20:35], 1] = np.inf
+    bad[idx[35:], 2] = -np.nan
+    finite = np.isfinite(bad).all(axis=1)
+    e = GICPEngine()
+    res = e.cloud_resolution(bad)
+    assert abs(res - _resolution_np(bad[finite])) <= 1e-9 * res
+    radius = 2.0 * (res + e.cloud_resolution(cad)) * 0.25  # small: some finite points lose the test
+    keep = e.radius_filter(bad, radius, 3)
+    assert not keep[~finite].any()
+    keep_f = e.radius_filter(bad[finite], radius, 3)
+    np.testing.assert_array_equal(keep[finite], keep_f)
+    assert e.cloud_resolution(np.full((5, 3), np.nan, np.float32)) == 0.0
+    # the class path: both clouds filtered in place, then GICP on the finite remainder
+    a = GICPAlignment(_rgb(cad), _rgb(bad), True)
+    a.run()
+    assert a.transform_exists_
+    kept_src = a.source_cloud_.xyz()
+    assert np.isfinite(kept_src).all() and len(kept_src) <= finite.sum()
+    o = ref.RefGICP()
+    o.set_source(kept_src)
+    o.set_target(a.target_cloud_.xyz())
+    T_ref, _ = o.align()
+    assert frob(a.getFineTransform(), T_ref) <= 1e-4
+
+
+@pytest.mark.gpu
+def test_seeded_debug_after_new_target_is_refused(part_small):
+    """a seeded sweep must never seed from the previous target's sorted positions."""
+    from leica_point_cloud_processing_amd import _lib
+    from leica_point_cloud_processing_amd.engine import GICPEngine
+
+    scan, cad, _ = part_small
+    e = GICPEngine()
+    e.set_source_xyz(scan)
+    e.set_target_xyz(cad)
+    e.debug_correspondences(np.eye(4, dtype=np.float32), len(scan))
+    e.set_target_xyz(cad[:1000])
+    with pytest.raises(_lib.MgicpError) as ei:
+        e.debug_correspondences_seeded(np.eye(4, dtype=np.float32), len(scan))
+    assert ei.value.code == _lib.MGICP_E_INVALID
+    with pytest.raises(_lib.MgicpError):
+        e.debug_moments(np.eye(4, dtype=np.float32))
+    m, tj, _ = e.debug_correspondences(np.eye(4, dtype=np.float32), len(scan))  # unseeded: fine
+    assert tj.max() < 1000
+    e.close()

@@ -310,3 +310,20 @@ def test_seeded_correspondences_lattice_ties(engine_mod):
         mg, tj_gpu, _ = e.debug_correspondences_seeded(T, len(pts))
         assert mr == mg
         np.testing.assert_array_equal(tj_ref, tj_gpu)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [1, 2, 7, 12, 20, 32])
+def test_covariances_any_k(engine_mod, part_small, k):
+    """PCL's setCorrespondenceRandomness accepts any k: exact instantiations (5..30 step 5) and the
+    rounded-up sentinel path (others, up to 32) both match the oracle."""
+    from oracle import ref
+
+    src, tgt, _ = part_small
+    e = engine_mod(k=k)
+    e.set_source_xyz(src[:6000])
+    e.set_target_xyz(tgt[:6000])
+    c_gpu = e.debug_covariances("source", 6000)
+    c_ref = ref.covariances(src[:6000], k=k)
+    assert np.abs(c_gpu - c_ref).max() <= 1e-12 * max(1.0, np.abs(c_ref).max())
+    assert float(np.mean(np.all(c_gpu == c_ref, axis=1))) > 0.99
