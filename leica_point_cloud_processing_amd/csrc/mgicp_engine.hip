@@ -36,6 +36,7 @@ namespace {
 constexpr double kDefaultOccupancy = 10.0;          // mean points per non-empty cell (A/B: profiles/r01/ab_tocc)
 constexpr size_t kSmallBytes = size_t(64) << 10;  // pinned readback scratch per context
 constexpr size_t kMaxCells = size_t(1) << 29;       // dense cell table cap (2 GiB of uint32)
+constexpr size_t kMaxBoxCells = size_t(1) << 27;    // per-cell point boxes up to 4 GiB (32 B per cell)
 
 double now_ms() {
   return std::chrono::duration<double, std::milli>(
@@ -208,6 +209,8 @@ struct Cloud {
   DevBuf<uint32_t> cell_start;
   DevBuf<uint8_t> empty_dist; // empty-space map (target only: 1-NN queries leave the surface)
   bool want_empty_map = false;
+  DevBuf<float4> boxes;       // per-cell point boxes (target only: the 1-NN sweeps prune by them)
+  bool want_boxes = false;
   bool drop_nonfinite = false; // build the grid over the finite points only (KdTreeFLANN semantics)
   double occupancy = 0;        // grid sizing target (points per non-empty cell); 0 = context default
   size_t n_built = 0;          // points of the last grid built in this slot (cell-size hint)
@@ -596,6 +599,12 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
     if ((rc = sync(ctx))) return rc;
     MGICP_TRACE_AT("grid: empty map done");
     g.empty_dist = cl.empty_dist.p;
+  }
+  g.boxes = nullptr;
+  if (cl.want_boxes && nc <= kMaxBoxCells) {
+    HIPCK(cl.boxes.reserve(2 * nc));
+    HIPCK(launch_cell_boxes(cl.pts.p, cl.cell_start.p, nc, cl.boxes.p, s));
+    g.boxes = cl.boxes.p;
   }
   cl.ncells = nc;
   cl.n_built = n;
@@ -1130,6 +1139,11 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
   }
   ctx->tgt.want_empty_map = true;  // correspondence / fitness queries start off the surface
   if (const char* em = std::getenv("MGICP_EMPTY_MAP")) ctx->tgt.want_empty_map = std::atoi(em) != 0;
+  // per-cell point boxes in the 1-NN sweeps: exact and 1.75x fewer candidates in sweep 1, but the
+  // per-cell box loads and tests cost more than they save (C4 correspondence 1.39 vs 1.11 ms,
+  // profiles/r02/ab_boxes): off by default, knob MGICP_CELL_BOXES=1
+  ctx->tgt.want_boxes = false;
+  if (const char* cb = std::getenv("MGICP_CELL_BOXES")) ctx->tgt.want_boxes = std::atoi(cb) != 0;
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
     return MGICP_E_HIP;
@@ -1174,7 +1188,7 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   ctx->f_count.release();
   for (Cloud* c : {&ctx->src, &ctx->tgt, &ctx->aux, &ctx->qry}) {
     c->raw.release(); c->orig.release(); c->pts.release(); c->perm.release();
-    c->cell_start.release(); c->cov.release(); c->empty_dist.release();
+    c->cell_start.release(); c->cov.release(); c->empty_dist.release(); c->boxes.release();
   }
   ctx->src_out.release();
   ctx->qperm.release();

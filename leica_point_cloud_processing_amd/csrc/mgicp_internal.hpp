@@ -27,6 +27,9 @@ struct GridView {
   // optional empty-space map: per cell, the Chebyshev distance (in cells) to the nearest
   // non-empty cell, capped at kEmptyCap + 1; rings closer than it hold no point
   const uint8_t* empty_dist;
+  // optional per-cell point boxes (2 float4 per cell: min xyz | bits(start), max xyz | bits(end));
+  // 1-NN searches skip cells whose point box lies beyond their bound
+  const float4* boxes;
 };
 
 #ifndef MGICP_EMPTY_CAP
@@ -152,6 +155,9 @@ hipError_t launch_iota(uint32_t* v, size_t n, hipStream_t s);
 // resolve all kernels once (moves the code-object loading cost into mgicp_create)
 // and exercise both copy directions once, small and large (pinned: pinned host scratch)
 hipError_t preload_kernels(void* pinned, size_t pinned_bytes, hipStream_t s);
+// per-cell point boxes of a built grid (GridView::boxes), 2 * nc float4
+hipError_t launch_cell_boxes(const float4* pts, const uint32_t* cell_start, size_t nc, float4* boxes,
+                             hipStream_t s);
 // empty-space distance map of a grid (3 separable capped min-max passes); scratch: nc bytes
 hipError_t launch_empty_map(const uint32_t* cell_start, int nx, int ny, int nz, uint8_t* out,
                             uint8_t* scratch, hipStream_t s);

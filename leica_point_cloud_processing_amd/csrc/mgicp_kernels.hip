@@ -178,6 +178,82 @@ __device__ __forceinline__ void ring_search(const GridView& g, float qx, float q
   }
 }
 
+// lower bound of the distance from q to a point box [lo, hi] (component-wise, each gap shrunk by
+// the rounding slop); an empty cell's sentinel box (lo = +INF, hi = -INF) gives +INF
+__device__ __forceinline__ float box_gap2(float qx, float qy, float qz, const float4& lo, const float4& hi,
+                                          float slop) {
+  const float gx = fmaxf(fmaxf(lo.x - qx, qx - hi.x) - slop, 0.f);
+  const float gy = fmaxf(fmaxf(lo.y - qy, qy - hi.y) - slop, 0.f);
+  const float gz = fmaxf(fmaxf(lo.z - qz, qz - hi.z) - slop, 0.f);
+  return gx * gx + gy * gy + gz * gz;
+}
+
+// Cells [xa, xb] of one grid row with their TIGHT point boxes (GridView::boxes): only the span
+// from the first to the last cell whose box can still hold a winner is scanned.  A query off a
+// surface (the 1-NN sweeps: 2-35 mm above the target) sees a whole slab of surface cells inside
+// its ball when cells are bounded by their grid boxes; by their point boxes only the cells next
+// to the foot of the query survive.  Exact: a skipped cell's every point lies beyond the bound.
+template <class V>
+__device__ __forceinline__ void visit_row_boxed(const GridView& g, size_t row, int xa, int xb, float w,
+                                                V& vis) {
+  uint32_t s = 0xffffffffu, e = 0u;
+  for (int x = xa; x <= xb; ++x) {
+    const float4 lo = g.boxes[2 * (row + x)], hi = g.boxes[2 * (row + x) + 1];
+    if (box_gap2(vis.qx, vis.qy, vis.qz, lo, hi, g.slop) <= w) {
+      s = min(s, __float_as_uint(lo.w));
+      e = max(e, __float_as_uint(hi.w));
+    }
+  }
+  if (s < e) vis.range(g, s, e);
+}
+
+// ring_search with per-cell point boxes (targets of the 1-NN sweeps): identical ring order,
+// termination and row pruning; inside a row the cell boxes decide which points are scanned
+template <class V>
+__device__ __forceinline__ void ring_search_boxed(const GridView& g, float qx, float qy, float qz,
+                                                  V& vis) {
+  const int cx = qcell(qx, g.ox, g.inv_h), cy = qcell(qy, g.oy, g.inv_h),
+            cz = qcell(qz, g.oz, g.inv_h);
+  int rmin = max(max(dist_out(cx, g.nx), dist_out(cy, g.ny)), dist_out(cz, g.nz));
+  if (rmin == 0 && g.empty_dist)
+    rmin = g.empty_dist[static_cast<size_t>(cx) +
+                        static_cast<size_t>(g.nx) * (static_cast<size_t>(cy) + static_cast<size_t>(g.ny) * cz)];
+  for (int r = rmin; r < (1 << 22); ++r) {
+    if (r > 0) {
+      const float L = fminf(fminf(axis_bound(qx, g.ox, g.h, cx, r - 1, g.nx),
+                                  axis_bound(qy, g.oy, g.h, cy, r - 1, g.ny)),
+                            axis_bound(qz, g.oz, g.h, cz, r - 1, g.nz));
+      if (L == INFINITY) return;
+      const float Ls = L * 0.99999f - g.slop;
+      if (vis.done(Ls)) return;
+    }
+    const int x0 = cx - r, x1 = cx + r, y0 = cy - r, y1 = cy + r, z0 = cz - r, z1 = cz + r;
+    const int xlo = max(x0, 0), xhi = min(x1, g.nx - 1);
+    const int ylo = max(y0, 0), yhi = min(y1, g.ny - 1);
+    const int zlo = max(z0, 0), zhi = min(z1, g.nz - 1);
+    for (int z = zlo; z <= zhi; ++z) {
+      const bool zf = (z == z0) || (z == z1);
+      const float gz = cell_gap(qz, g.oz, g.h, z, g.slop);
+      for (int y = ylo; y <= yhi; ++y) {
+        const float w = vis.prune2() * 1.00001f;
+        const float gy = cell_gap(qy, g.oy, g.h, y, g.slop);
+        const float gyz = gy * gy + gz * gz;
+        if (gyz > w) continue;
+        const size_t row = (static_cast<size_t>(z) * g.ny + y) * g.nx;
+        if (zf || y == y0 || y == y1) {
+          const float rx = sqrtf(w - gyz) + g.slop;
+          const int xa = max(xlo, qcell(qx - rx, g.ox, g.inv_h));
+          const int xb = min(xhi, qcell(qx + rx, g.ox, g.inv_h));
+          if (xa <= xb) visit_row_boxed(g, row, xa, xb, w, vis);
+        } else {
+          if (x0 >= 0) visit_row_boxed(g, row, x0, x0, w, vis);
+          if (x1 < g.nx) visit_row_boxed(g, row, x1, x1, vis.prune2() * 1.00001f, vis);
+        }
+      }
+    }
+  }
+}
+
 // exact k-NN visitor: register-resident sorted list of (d2, index) keys.  A runtime k < K is
 // served by the K-slot list with its first K - k slots pre-filled with the sentinel key 0: every
 // real key is >= 0 and an insert never moves in front of an equal key, so the sentinels stay in
@@ -427,6 +503,23 @@ __global__ void empty_pass_kernel(const uint8_t* __restrict__ in, uint8_t* __res
   out[c] = static_cast<uint8_t>(min(best, cap + 1));
 }
 
+// per-cell point boxes: boxes[2c] = (min x, min y, min z, bits(start)), boxes[2c + 1] =
+// (max x, max y, max z, bits(end)); an empty cell gets the sentinel (+INF / -INF) box
+__global__ void cell_box_kernel(const float4* __restrict__ pts, const uint32_t* __restrict__ cs, size_t nc,
+                                float4* __restrict__ boxes) {
+  const size_t c = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (c >= nc) return;
+  const uint32_t a = cs[c], b = cs[c + 1];
+  float lx = INFINITY, ly = INFINITY, lz = INFINITY, hx = -INFINITY, hy = -INFINITY, hz = -INFINITY;
+  for (uint32_t j = a; j < b; ++j) {
+    const float4 p = pts[j];
+    lx = fminf(lx, p.x); ly = fminf(ly, p.y); lz = fminf(lz, p.z);
+    hx = fmaxf(hx, p.x); hy = fmaxf(hy, p.y); hz = fmaxf(hz, p.z);
+  }
+  boxes[2 * c] = make_float4(lx, ly, lz, __uint_as_float(a));
+  boxes[2 * c + 1] = make_float4(hx, hy, hz, __uint_as_float(b));
+}
+
 __global__ void iota_kernel(uint32_t* v, size_t n) {
   const size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i < n) v[i] = static_cast<uint32_t>(i);
@@ -586,7 +679,8 @@ __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_kernel(GridV
     const uint32_t pp = nn_pos[p - p0];
     if (pp != 0xffffffffu) vis.range(tg, pp, pp + 1);
   }
-  ring_search(tg, qx, qy, qz, vis);
+  if (tg.boxes) ring_search_boxed(tg, qx, qy, qz, vis);
+  else ring_search(tg, qx, qy, qz, vis);
   const bool ok = vis.best != ~0ull &&
                   static_cast<double>(__uint_as_float(static_cast<uint32_t>(vis.best >> 32))) < thr;
   nn_pos[p - p0] = ok ? vis.pos : 0xffffffffu;
@@ -979,7 +1073,8 @@ __global__ __launch_bounds__(256) void fitness_kernel(GridView tg, const float4*
     xform(T, s.x, s.y, s.z, qx, qy, qz);
     NnVisitor vis;
     vis.init(qx, qy, qz, INFINITY);
-    ring_search(tg, qx, qy, qz, vis);
+    if (tg.boxes) ring_search_boxed(tg, qx, qy, qz, vis);
+    else ring_search(tg, qx, qy, qz, vis);
     if (vis.best != ~0ull) {
       const float d2 = __uint_as_float(static_cast<uint32_t>(vis.best >> 32));
       if (static_cast<double>(d2) <= max_range) {
@@ -1234,6 +1329,13 @@ hipError_t launch_empty_map(const uint32_t* cell_start, int nx, int ny, int nz, 
   return hipMemcpyAsync(out, scratch, nc, hipMemcpyDeviceToDevice, s);
 }
 
+hipError_t launch_cell_boxes(const float4* pts, const uint32_t* cell_start, size_t nc, float4* boxes,
+                             hipStream_t s) {
+  if (!nc) return hipSuccess;
+  cell_box_kernel<<<nblk(nc), 256, 0, s>>>(pts, cell_start, nc, boxes);
+  return hipGetLastError();
+}
+
 hipError_t launch_iota(uint32_t* v, size_t n, hipStream_t s) {
   if (!n) return hipSuccess;
   iota_kernel<<<nblk(n), 256, 0, s>>>(v, n);
@@ -1446,6 +1548,7 @@ hipError_t preload_kernels(void* pinned, size_t pinned_bytes, hipStream_t s) {
       reinterpret_cast<const void*>(&empty_init_kernel),
       reinterpret_cast<const void*>(&empty_pass_kernel),
       reinterpret_cast<const void*>(&iota_kernel),
+      reinterpret_cast<const void*>(&cell_box_kernel),
       reinterpret_cast<const void*>(&knn_cov_kernel<5>),
       reinterpret_cast<const void*>(&knn_cov_kernel<10>),
       reinterpret_cast<const void*>(&knn_cov_kernel<15>),
