@@ -62,6 +62,19 @@ constexpr int kMomVals = 80;
 
 // Xform as 3x4 row-major float (the top three rows of an Eigen::Matrix4f).
 struct Xf34 { float m[12]; };
+
+// Command block of a pre-launched (gated) objective pass, in pinned mapped host memory (and its
+// device-memory forward).  Self-validating without fences: every 8-byte half carries one payload
+// word (low 32 bits) and the low 32 bits of the pass's sequence number (high 32 bits); aligned
+// 8-byte stores and loads are single-copy atomic on both sides, so a reader that finds the stamp
+// in all kCmdWords halves holds a complete command of that pass -- in the same PCIe round trip
+// that detects it.  Words: [0..11] A (Xf34 bit patterns), [12] op, [13] sweep direction.
+constexpr unsigned int kPassRun = 1;
+constexpr unsigned int kPassCancel = 2;
+constexpr int kCmdWords = 14;
+struct alignas(128) PassCmd {
+  unsigned long long h[16];
+};
 struct Rot33d { double m[9]; };
 
 // ---- launchers (mgicp_kernels.hip); all asynchronous on `s` ----
@@ -100,6 +113,14 @@ hipError_t launch_compact(const float4* src, const float4* tpts, const Cov3& cov
 hipError_t launch_fdf_soa(const CorrSoA& c, size_t m, Xf34 A, double* partial, int nb,
                           unsigned int* ticket, double* out, int reverse,
                           unsigned long long* done_flag, unsigned long long seq, hipStream_t s);
+// the same pass pre-launched before its state is known: block 0 waits for cmd->seq == seq (or for
+// `timeout_ticks` of wall_clock64) and forwards the command to `mail` (device memory) for the other
+// blocks; then every block runs with its A / reverse, or exits on a cancel
+hipError_t launch_fdf_soa_gated(const CorrSoA& c, size_t m, double* partial, int nb, unsigned int* ticket,
+                                double* out, unsigned long long* done_flag, unsigned long long seq,
+                                const PassCmd* cmd, PassCmd* mail, unsigned long long timeout_ticks,
+                                unsigned long long* gtrace /*nullable: diagnostics*/,
+                                int host_pollers /*blocks [0, host_pollers) poll the host copy*/, hipStream_t s);
 int        fdf_grid_blocks(size_t n, int max_blocks = 2048);
 // Gauss-Newton moments of the accepted correspondences of [p0, p1) at T0 (R = rot(T0 * guess),
 // ctr = expansion centre): nb block partials of kMomVals doubles, then a one-block finish

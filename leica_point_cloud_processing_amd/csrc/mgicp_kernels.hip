@@ -884,6 +884,38 @@ __device__ __forceinline__ void finish_in_last_block(const double* partial, unsi
   }
 }
 
+// the 8 x 16 bytes of a command block: system-coherent loads of the host's pinned copy
+// (sc0 sc1: no GPU cache holds them) or agent-coherent loads of the device mailbox (sc1)
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+template <bool kHost>
+__device__ __forceinline__ void read_cmd(const PassCmd* c, unsigned long long (&v)[16]) {
+  u32x4 r[8];
+  const u32x4* p = reinterpret_cast<const u32x4*>(c);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (kHost) asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1" : "=v"(r[i]) : "v"(p + i) : "memory");
+    else asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(r[i]) : "v"(p + i) : "memory");
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    v[2 * i] = (static_cast<unsigned long long>(r[i].y) << 32) | r[i].x;
+    v[2 * i + 1] = (static_cast<unsigned long long>(r[i].w) << 32) | r[i].z;
+  }
+}
+
+// block 0's forward of a validated command to the device mailbox (agent-coherent vector stores)
+__device__ __forceinline__ void write_mail(PassCmd* c, const unsigned long long (&v)[16]) {
+  u32x4* p = reinterpret_cast<u32x4*>(c);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    u32x4 w;
+    w.x = static_cast<unsigned int>(v[2 * i]); w.y = static_cast<unsigned int>(v[2 * i] >> 32);
+    w.z = static_cast<unsigned int>(v[2 * i + 1]); w.w = static_cast<unsigned int>(v[2 * i + 1] >> 32);
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(p + i), "v"(w) : "memory");
+  }
+}
+
 // one correspondence of OptimizationFunctorWithIndices::fdf: pp = A s (fp32, Eigen order),
 // r = fp32(pp - q) widened to fp64, t = M r, accumulate r't, t and s t'
 __device__ __forceinline__ void fdf_point(const Xf34& A, float sx, float sy, float sz, float qx,
@@ -910,12 +942,62 @@ __device__ __forceinline__ void fdf_point(const Xf34& A, float sx, float sy, flo
 
 // Objective pass over the compacted streams: 4 correspondences per thread-iteration, every load
 // 16 bytes per lane (float4 of 4 coordinates, double2 of 2 matrix entries).
-__global__ __launch_bounds__(256) void fdf_soa_kernel(CorrSoA c, size_t m, Xf34 A,
-                                                      double* __restrict__ partial,
-                                                      unsigned int* __restrict__ ticket,
-                                                      double* __restrict__ out, int reverse,
-                                                      unsigned long long* done_flag,
-                                                      unsigned long long seq) {
+// kGated (fdf_soa_gated_kernel): the pass is launched BEFORE the host knows its state.  Every
+// block's thread 0 polls the host-written command block (pinned, mapped, system-scope acquire)
+// until it carries this pass's sequence number, then the block takes A / direction from it -- or
+// returns at once on a cancel command (or after `timeout` wall-clock ticks: every wave reaches
+// an exit).  The host pre-launches pass k + 1 while pass k runs, so the next pass is resident
+// when the host's BFGS step publishes x_{k+1}: no launch latency between consecutive passes.
+template <bool kGated>
+__device__ __forceinline__ void fdf_soa_body(CorrSoA c, size_t m, Xf34 A, double* __restrict__ partial,
+                                             unsigned int* __restrict__ ticket, double* __restrict__ out,
+                                             int reverse, unsigned long long* done_flag,
+                                             unsigned long long seq, const PassCmd* cmd, PassCmd* mail,
+                                             unsigned long long timeout, unsigned long long* gtrace,
+                                             int host_pollers) {
+  if constexpr (kGated) {
+    __shared__ unsigned int sw[kCmdWords];
+    __shared__ int sok;
+    if (threadIdx.x == 0) {
+      // block 0 alone polls the host's command block over PCIe (256 pollers of host memory were
+      // measured to delay the command by ~320 us) and forwards it to the device mailbox the
+      // other blocks poll; both blocks are read whole (8 x 16 B per poll) and validated by stamp
+      const bool host_poller = blockIdx.x < host_pollers;
+      const unsigned int stamp = static_cast<unsigned int>(seq);
+      const unsigned long long t0 = wall_clock64();
+      unsigned long long v[16];
+      bool got = false;
+      for (;;) {
+        if (host_poller) read_cmd<true>(cmd, v);
+        else read_cmd<false>(mail, v);
+        bool all = true;
+#pragma unroll
+        for (int i = 0; i < kCmdWords; ++i) all = all && static_cast<unsigned int>(v[i] >> 32) == stamp;
+        if (all) { got = true; break; }
+        if (wall_clock64() - t0 > timeout) break;  // no command: give up as if cancelled
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (gtrace && host_poller) {  // diagnostics: kernel start and command seen (wall clock)
+        gtrace[4 * (seq & 1023)] = t0;
+        gtrace[4 * (seq & 1023) + 1] = wall_clock64();
+      }
+      if (!got) {  // a timeout forwards a cancel, so every block exits promptly
+#pragma unroll
+        for (int i = 0; i < kCmdWords; ++i) v[i] = (static_cast<unsigned long long>(stamp) << 32) | (i == 12 ? kPassCancel : 0u);
+      }
+#pragma unroll
+      for (int i = 0; i < kCmdWords; ++i) sw[i] = static_cast<unsigned int>(v[i]);
+      if (blockIdx.x == 0 && host_pollers < static_cast<int>(gridDim.x)) write_mail(mail, v);
+      sok = got ? 1 : 0;
+    }
+    __syncthreads();
+    if (gtrace && threadIdx.x == 0)  // diagnostics: the latest block to pass the gate
+      atomicMax(&gtrace[4 * (seq & 1023) + 2], wall_clock64());
+    if (!sok || sw[12] != kPassRun) return;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) A.m[i] = __uint_as_float(sw[i]);
+    reverse = static_cast<int>(sw[13]);
+  }
   double acc[kRedVals];
 #pragma unroll
   for (int v = 0; v < kRedVals; ++v) acc[v] = 0.0;
@@ -957,6 +1039,23 @@ __global__ __launch_bounds__(256) void fdf_soa_kernel(CorrSoA c, size_t m, Xf34 
   } else {
     block_reduce_store(acc, partial + static_cast<size_t>(blockIdx.x) * kRedVals);
   }
+}
+
+__global__ __launch_bounds__(256) void fdf_soa_kernel(CorrSoA c, size_t m, Xf34 A, double* __restrict__ partial,
+                                                      unsigned int* __restrict__ ticket, double* __restrict__ out,
+                                                      int reverse, unsigned long long* done_flag,
+                                                      unsigned long long seq) {
+  fdf_soa_body<false>(c, m, A, partial, ticket, out, reverse, done_flag, seq, nullptr, nullptr, 0, nullptr, 0);
+}
+
+__global__ __launch_bounds__(256) void fdf_soa_gated_kernel(CorrSoA c, size_t m, double* __restrict__ partial,
+                                                            unsigned int* __restrict__ ticket,
+                                                            double* __restrict__ out, unsigned long long* done_flag,
+                                                            unsigned long long seq, const PassCmd* cmd,
+                                                            PassCmd* mail, unsigned long long timeout,
+                                                            unsigned long long* gtrace, int host_pollers) {
+  fdf_soa_body<true>(c, m, Xf34{}, partial, ticket, out, 0, done_flag, seq, cmd, mail, timeout, gtrace,
+                     host_pollers);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1402,6 +1501,15 @@ hipError_t launch_fdf_soa(const CorrSoA& c, size_t m, Xf34 A, double* partial, i
   return hipGetLastError();
 }
 
+hipError_t launch_fdf_soa_gated(const CorrSoA& c, size_t m, double* partial, int nb, unsigned int* ticket,
+                                double* out, unsigned long long* done_flag, unsigned long long seq,
+                                const PassCmd* cmd, PassCmd* mail, unsigned long long timeout_ticks,
+                                unsigned long long* gtrace, int host_pollers, hipStream_t s) {
+  fdf_soa_gated_kernel<<<nb, 256, 0, s>>>(c, m, partial, ticket, out, done_flag, seq, cmd, mail, timeout_ticks,
+                                          gtrace, host_pollers);
+  return hipGetLastError();
+}
+
 hipError_t launch_publish(const double* in, int n, double* host_out, unsigned long long* flag,
                           unsigned long long seq, hipStream_t s) {
   publish_kernel<<<1, 64, 0, s>>>(in, n, host_out, flag, seq);
@@ -1563,6 +1671,7 @@ hipError_t preload_kernels(void* pinned, size_t pinned_bytes, hipStream_t s) {
       reinterpret_cast<const void*>(&morton_key_kernel),
       reinterpret_cast<const void*>(&compact_kernel),
       reinterpret_cast<const void*>(&fdf_soa_kernel),
+      reinterpret_cast<const void*>(&fdf_soa_gated_kernel),
       reinterpret_cast<const void*>(&fitness_kernel),
       reinterpret_cast<const void*>(&resolution_kernel),
       reinterpret_cast<const void*>(&radius_keep_kernel),
