@@ -1398,678 +1398,6 @@ int mgicp_align(mgicp_ctx* ctx, const float guess_cm[16], float out_T_cm[16], mg
       std::fprintf(stderr, "[gate-trace] passes %d | device: block-0 wait %.2f us, last block through the gate +%.2f us | host: sums seen -> command published %.2f us\n",
                    cnt, w / cnt, sp / cnt, hd / cnt);
     std::memset(ctx->h_gtrace, 0, 4 * 1024 * sizeof(unsigned long long));
-      ctx->host_gt.assign(2 * 1024, 0.0);
-    }
-  }
-  if (ctx->h_red) return MGICP_OK;
-  // kRedVals sums followed by the pass-completion word (see launch_fdf_soa's done_flag)
-  HIPCK(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_red), 2 * kRedVals * sizeof(double),
-                      hipHostMallocMapped | hipHostMallocCoherent));
-  HIPCK(hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->d_h_red), ctx->h_red, 0));
-  std::memset(ctx->h_red, 0, 2 * kRedVals * sizeof(double));
-  ctx->h_flag = reinterpret_cast<unsigned long long*>(ctx->h_red + kRedVals);
-  ctx->d_flag = reinterpret_cast<unsigned long long*>(ctx->d_h_red + kRedVals);
-  return MGICP_OK;
-}
-
-// Wait for pass `seq` to publish its sums: spin on the mapped completion word; after ~0.5 s fall
-// back to a stream synchronisation so a failed launch surfaces as an error instead of a hang.
-int wait_pass(mgicp_ctx* ctx, unsigned long long seq) {
-  const auto t0 = std::chrono::steady_clock::now();
-  for (unsigned spins = 0;; ++spins) {
-    if (__atomic_load_n(ctx->h_flag, __ATOMIC_ACQUIRE) == seq) return MGICP_OK;
-    if ((spins & 1023u) == 1023u &&
-        std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(500))
-      break;
-  }
-  int rc = sync(ctx);
-  if (rc) return rc;
-  if (__atomic_load_n(ctx->h_flag, __ATOMIC_ACQUIRE) != seq)
-    return fail(ctx, MGICP_E_HIP, "objective pass finished without publishing its sums");
-  return MGICP_OK;
-}
-
-int ensure_iter_buffers(mgicp_ctx* ctx) {
-  const size_t n = ctx->src.n;
-  const int nb = std::max(fdf_grid_blocks(n), static_cast<int>((n + 255) / 256));
-  HIPCK(ctx->partial.reserve(static_cast<size_t>(nb) * kRedVals));
-  HIPCK(ctx->red.reserve(kRedVals));
-  int rc = ensure_host_red(ctx);
-  if (rc) return rc;
-  const size_t ns = ctx->shard_p1() - ctx->shard_p0();
-  const size_t cap = (ns + 3) / 4 * 4 + 4;
-  HIPCK(ctx->prev_pos.reserve(ns + 1));
-  HIPCK(ctx->flags.reserve(ns + 1));
-  HIPCK(ctx->cpos.reserve(ns + 1));
-  if (ctx->corr_cap < cap) {
-    HIPCK(ctx->corr_f.reserve(6 * cap));
-    HIPCK(ctx->corr_d.reserve(6 * cap));
-    ctx->corr_cap = cap;
-  }
-  HIPCK(ctx->cscratch.reserve(scan_scratch_bytes(ns + 1)));
-  if (!ctx->ticket.p) {
-    HIPCK(ctx->ticket.reserve(1));
-    HIPCK(hipMemsetAsync(ctx->ticket.p, 0, sizeof(unsigned int), ctx->stream));
-  }
-  return MGICP_OK;
-}
-
-// guess-applied source cloud ("output" after transformPointCloud(output, output, guess))
-int set_output(mgicp_ctx* ctx, const Mat4& G) {
-  float lo[3], hi[3];
-  if (G.is_identity()) {
-    ctx->d_out = ctx->src.pts.p;  // x*1 + y*0 + z*0 + 0 == x: identity leaves points intact
-    for (int d = 0; d < 3; ++d) {
-      lo[d] = ctx->src.lo[d];
-      hi[d] = ctx->src.hi[d];
-    }
-  } else {
-    HIPCK(ctx->src_out.reserve(ctx->src.n));
-    HIPCK(launch_xform_points(ctx->src.pts.p, ctx->src.n, G.xf(), ctx->src_out.p, ctx->stream));
-    ctx->d_out = ctx->src_out.p;
-    // bbox of the transformed cloud (the Gauss-Newton expansion centre)
-    const size_t n = ctx->src.n;
-    const int nb = static_cast<int>(std::min<size_t>((n + 255) / 256, 1024));
-    HIPCK(launch_bbox(ctx->src_out.p, n, reinterpret_cast<float*>(ctx->d_small), nb, ctx->stream));
-    int rc = sync(ctx);
-    if (rc) return rc;
-    const float* hp = reinterpret_cast<const float*>(ctx->h_small);
-    for (int d = 0; d < 3; ++d) {
-      lo[d] = INFINITY;
-      hi[d] = -INFINITY;
-    }
-    for (int b = 0; b < nb; ++b)
-      for (int d = 0; d < 3; ++d) {
-        lo[d] = std::min(lo[d], hp[b * 8 + d]);
-        hi[d] = std::max(hi[d], hp[b * 8 + 3 + d]);
-      }
-  }
-  for (int d = 0; d < 3; ++d) ctx->out_ctr[d] = static_cast<double>(0.5f * (lo[d] + hi[d]));
-  ctx->last_guess = G;
-  return MGICP_OK;
-}
-
-// transform_R(i,j) = sum_k double(T(i,k)) * double(G(k,j)), top-left 3x3
-Rot33d rot_of(const Mat4& T, const Mat4& G) {
-  Rot33d R;
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j) {
-      double a = 0.0;
-      for (int k = 0; k < 4; ++k) a += static_cast<double>(T.m[i][k]) * static_cast<double>(G.m[k][j]);
-      R.m[3 * i + j] = a;
-    }
-  return R;
-}
-
-CorrSoA corr_soa(mgicp_ctx* ctx) {
-  const size_t c = ctx->corr_cap;
-  float* f = ctx->corr_f.p;
-  double* d = ctx->corr_d.p;
-  return CorrSoA{f, f + c, f + 2 * c, f + 3 * c, f + 4 * c, f + 5 * c,
-                 d, d + c, d + 2 * c, d + 3 * c, d + 4 * c, d + 5 * c};
-}
-
-// One correspondence sweep (the loop body of computeTransformation before the BFGS call):
-// exact 1-NN per source point, then a deterministic compaction of the accepted ones (exclusive
-// scan of the flags, scatter in grid-sorted order) that computes their Mahalanobis matrices
-// straight into the SoA streams.  `seed` uses the previous sweep's matches as 1-NN starting
-// candidates (exact either way).
-int correspond(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
-  const double thr = ctx->prm.max_corr_dist * ctx->prm.max_corr_dist;
-  const size_t p0 = ctx->shard_p0(), p1 = ctx->shard_p1(), ns = p1 - p0;
-  hipStream_t s = ctx->stream;
-  const bool seeded = seed && ctx->seed_valid;
-  HIPCK(hipMemsetAsync(ctx->flags.p + ns, 0, sizeof(uint32_t), s));
-  const uint32_t* qp = query_perm(ctx);
-  {
-    ProfScope ps(ctx, kFamCorr);
-    HIPCK(launch_correspond(ctx->tgt.view, ctx->d_out, p0, p1, T.xf(), thr, seeded ? 1 : 0,
-                            ctx->prev_pos.p, ctx->flags.p, qp, s));
-  }
-  ctx->seed_valid = true;
-#if MGICP_CORR_STATS
-  {
-    unsigned long long st[8];
-    HIPCK(hipStreamSynchronize(s));
-    HIPCK(corr_stats_take(st));
-    std::fprintf(stderr, "[corr-stats] queries %llu accepted %llu rejected %llu | tests/query acc %.1f rej %.1f | ranges/query acc %.1f rej %.1f\n",
-                 st[0], st[1], st[2], st[1] ? double(st[3]) / st[1] : 0.0, st[2] ? double(st[4]) / st[2] : 0.0,
-                 st[1] ? double(st[5]) / st[1] : 0.0, st[2] ? double(st[6]) / st[2] : 0.0);
-  }
-#endif
-  const size_t sb = scan_scratch_bytes(ns + 1);
-  HIPCK(launch_exclusive_scan(ctx->cscratch.p, sb, ctx->flags.p, ctx->cpos.p, ns + 1, s));
-  {
-    ProfScope ps(ctx, kFamCompact);
-    HIPCK(launch_compact(ctx->d_out, ctx->tgt.view.pts, ctx->src.cov3(), ctx->tgt.cov3(),
-                         rot_of(T, G), ctx->prev_pos.p, ctx->flags.p, ctx->cpos.p, p0, p1,
-                         corr_soa(ctx), s));
-  }
-  HIPCK(hipMemcpyAsync(ctx->h_small, ctx->cpos.p + ns, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-  int rc = sync(ctx);
-  if (rc) return rc;
-  uint32_t m = 0;
-  std::memcpy(&m, ctx->h_small, sizeof(m));
-  ctx->m_local = m;
-  ctx->have_corr = true;
-  return MGICP_OK;
-}
-
-// finish the block partials (fixed order), all-reduce across ranks, copy to host
-int reduce_to_host(mgicp_ctx* ctx, int nb) {
-  {
-    ProfScope ps(ctx, kFamRed);
-    HIPCK(launch_reduce_finish(ctx->partial.p, nb, ctx->red.p, ctx->stream));
-  }
-  if (ctx->comm)
-    NCCLCK(ncclAllReduce(ctx->red.p, ctx->red.p, kRedVals, ncclDouble, ncclSum, ctx->comm,
-                         ctx->stream));
-  HIPCK(hipMemcpyAsync(ctx->h_red, ctx->red.p, kRedVals * sizeof(double), hipMemcpyDeviceToHost,
-                       ctx->stream));
-  return sync(ctx);
-}
-
-// OptimizationFunctorWithIndices::fdf on the device; memoises the last state
-struct DeviceFunctor {
-  mgicp_ctx* ctx;
-  bool have_memo = false;
-  Vec6 memo_x{};
-  double memo_f = 0;
-  Vec6 memo_g{};
-  double m = 0;  // correspondences of this sweep (all ranks)
-
-  int pass(const Vec6& x, double sums[kRedVals]) {
-    const Mat4 A = apply_state(x);
-    const int nb = fdf_grid_blocks(ctx->m_local, ctx->fdf_max_blocks);
-    int rc;
-    // alternate the sweep direction so each pass starts on the Infinity-Cache-resident tail
-    // of the previous one (deterministic: the direction follows the pass index)
-    const int reverse = ctx->alt_sweep ? (ctx->n_evals & 1) : 0;
-    if (ctx->fused_finish) {
-      // the last block writes the sums straight into mapped pinned host memory (single GPU)
-      // or device memory (multi-GPU: then one 16-double RCCL all-reduce, and a one-wave kernel
-      // publishes the reduced sums plus the completion word into mapped host memory)
-      double* out = ctx->comm ? ctx->red.p : ctx->d_h_red;
-      const bool poll = ctx->poll;
-      const unsigned long long seq = ++ctx->pass_seq;
-      const bool gate = ctx->gated && poll && !ctx->comm && !ctx->profiling;
-      const Xf34 Ax = A.xf();
-      if (ctx->gated_seq == seq) {
-        // pass `seq` is already resident, waiting: hand it its state
-        publish_cmd(ctx, seq, kPassRun, reverse, &Ax);
-        if (ctx->h_gtrace) ctx->host_gt[2 * (seq & 1023) + 1] = now_ms() * 1e3;
-        ctx->gated_seq = 0;
-      } else {
-        cancel_gated(ctx);
-        ProfScope ps(ctx, kFamFdf);
-        HIPCK(launch_fdf_soa(corr_soa(ctx), ctx->m_local, Ax, ctx->partial.p, nb,
-                             ctx->ticket.p, out, reverse,
-                             (poll && !ctx->comm) ? ctx->d_flag : nullptr, seq, ctx->stream));
-      }
-      if (gate) {
-        // queue pass seq + 1 now (its launch overlaps this pass); it runs once the BFGS step has
-        // published x_{k+1}, or exits on cancel when the BFGS run ends
-        HIPCK(launch_fdf_soa_gated(corr_soa(ctx), ctx->m_local, ctx->partial.p, nb, ctx->ticket.p, out,
-                                   ctx->d_flag, seq + 1, ctx->d_cmd, ctx->mail, ctx->gate_timeout,
-                                   ctx->d_gtrace, ctx->gate_pollers, ctx->stream));
-        ctx->gated_seq = seq + 1;
-      }
-      if (ctx->comm) {
-        NCCLCK(ncclAllReduce(ctx->red.p, ctx->red.p, kRedVals, ncclDouble, ncclSum, ctx->comm,
-                             ctx->stream));
-        if (poll) {
-          HIPCK(launch_publish(ctx->red.p, kRedVals, ctx->d_h_red, ctx->d_flag, seq, ctx->stream));
-        } else {
-          HIPCK(hipMemcpyAsync(ctx->h_red, ctx->red.p, kRedVals * sizeof(double),
-                               hipMemcpyDeviceToHost, ctx->stream));
-        }
-      }
-      rc = poll ? wait_pass(ctx, seq) : sync(ctx);
-      if (ctx->h_gtrace) ctx->host_gt[2 * ((seq + 1) & 1023)] = now_ms() * 1e3;  // sums of seq seen
-    } else {
-      {
-        ProfScope ps(ctx, kFamFdf);
-        HIPCK(launch_fdf_soa(corr_soa(ctx), ctx->m_local, A.xf(), ctx->partial.p, nb, nullptr,
-                             nullptr, reverse, nullptr, 0, ctx->stream));
-      }
-      rc = reduce_to_host(ctx, nb);
-    }
-    if (rc) return rc;
-    std::memcpy(sums, ctx->h_red, kRedVals * sizeof(double));
-    ctx->n_evals++;
-    return MGICP_OK;
-  }
-
-  int eval(const Vec6& x, double& f, Vec6& g) {
-    if (have_memo && std::memcmp(x.v, memo_x.v, sizeof(x.v)) == 0) {
-      f = memo_f;
-      g = memo_g;
-      return 0;
-    }
-    double s[kRedVals];
-    int rc = pass(x, s);
-    if (rc) return rc;
-    m = s[13];
-    f = s[0] / m;
-    const double sc = 2.0 / m;
-    g[0] = s[1] * sc;
-    g[1] = s[2] * sc;
-    g[2] = s[3] * sc;
-    double R[3][3];
-    for (int a = 0; a < 3; ++a)
-      for (int b = 0; b < 3; ++b) R[a][b] = s[4 + 3 * a + b] * sc;
-    r_derivative(x, R, g);
-    have_memo = true;
-    memo_x = x;
-    memo_f = f;
-    memo_g = g;
-    return 0;
-  }
-};
-
-// GICP::estimateRigidTransformationBFGS: 0 = accepted, MGICP_E_SOLVER = PCL would throw
-struct GateGuard {  // a BFGS run leaves no gated pass queued behind it
-  mgicp_ctx* ctx;
-  ~GateGuard() { cancel_gated(ctx); }
-};
-
-int estimate_bfgs(mgicp_ctx* ctx, Mat4& T, int* n_corr) {
-  GateGuard guard{ctx};
-  Vec6 x;
-  x[0] = T.m[0][3];
-  x[1] = T.m[1][3];
-  x[2] = T.m[2][3];
-  x[3] = std::atan2(static_cast<double>(T.m[2][1]), static_cast<double>(T.m[2][2]));
-  x[4] = std::asin(-static_cast<double>(T.m[2][0]));
-  x[5] = std::atan2(static_cast<double>(T.m[1][0]), static_cast<double>(T.m[0][0]));
-  DeviceFunctor fn{ctx};
-  // the correspondence count arrives with the first objective pass (its count lane)
-  double s[kRedVals];
-  int rc = fn.pass(x, s);
-  if (rc) return rc;
-  *n_corr = static_cast<int>(s[13]);
-  if (s[13] < 4) return MGICP_E_SOLVER;  // NotEnoughPointsException
-  {
-    // seed the memo with this pass so minimizeInit reuses it
-    fn.m = s[13];
-    fn.memo_x = x;
-    fn.memo_f = s[0] / fn.m;
-    const double sc = 2.0 / fn.m;
-    fn.memo_g[0] = s[1] * sc;
-    fn.memo_g[1] = s[2] * sc;
-    fn.memo_g[2] = s[3] * sc;
-    double R[3][3];
-    for (int a = 0; a < 3; ++a)
-      for (int b = 0; b < 3; ++b) R[a][b] = s[4 + 3 * a + b] * sc;
-    r_derivative(x, R, fn.memo_g);
-    fn.have_memo = true;
-  }
-  PclBfgs<DeviceFunctor> bfgs(fn);
-  const double gradient_tol = 1e-2;
-  int inner = 0;
-  int result = bfgs.init(x);
-  result = kRunning;
-  do {
-    inner++;
-    result = bfgs.step(x);
-    if (bfgs.error) return bfgs.error;
-    if (result) break;
-    result = bfgs.test_gradient(gradient_tol);
-  } while (result == kRunning && inner < ctx->prm.max_inner_iter);
-  if (bfgs.error) return bfgs.error;
-  if (result == kNoProgress || result == kSuccess || inner == ctx->prm.max_inner_iter) {
-    T = apply_state(x);
-    return MGICP_OK;
-  }
-  return MGICP_E_SOLVER;  // SolverDidntConvergeException
-}
-
-// Gauss-Newton mode, one device pass per outer iteration: the 74 moments of the objective over
-// the accepted correspondences of the last sweep at T (Mahalanobis computed on the fly), finished
-// in a fixed block order, all-reduced across ranks (one 80-double RCCL call), copied to the host.
-int moments_pass(mgicp_ctx* ctx, const Mat4& T, const Mat4& G) {
-  const size_t p0 = ctx->shard_p0(), p1 = ctx->shard_p1();
-  hipStream_t s = ctx->stream;
-  const int nb = gn_grid_blocks(p1 - p0);
-  HIPCK(ctx->mpartial.reserve(static_cast<size_t>(nb) * kMomVals));
-  HIPCK(ctx->mred.reserve(kMomVals));
-  {
-    ProfScope ps(ctx, kFamMoments);
-    HIPCK(launch_gn_moments(ctx->d_out, ctx->tgt.view.pts, ctx->src.cov3(), ctx->tgt.cov3(),
-                            rot_of(T, G), T.xf(), ctx->out_ctr, ctx->prev_pos.p, ctx->flags.p, p0,
-                            p1, ctx->mpartial.p, nb, s));
-    HIPCK(launch_reduce_finish_moments(ctx->mpartial.p, nb, ctx->mred.p, s));
-  }
-  if (ctx->comm)
-    NCCLCK(ncclAllReduce(ctx->mred.p, ctx->mred.p, kMomVals, ncclDouble, ncclSum, ctx->comm, s));
-  HIPCK(hipMemcpyAsync(ctx->h_small, ctx->mred.p, kMomVals * sizeof(double), hipMemcpyDeviceToHost, s));
-  int rc = sync(ctx);
-  if (rc) return rc;
-  std::memcpy(ctx->mom, ctx->h_small, kMomVals * sizeof(double));
-  ctx->n_evals++;
-  return MGICP_OK;
-}
-
-// the correspondence sweep of the Gauss-Newton mode: exact 1-NN (same kernel as the BFGS mode),
-// then the moment pass; no scan / compaction (the moment pass reads the flags directly)
-int correspond_gn(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
-  const double thr = ctx->prm.max_corr_dist * ctx->prm.max_corr_dist;
-  const size_t p0 = ctx->shard_p0(), p1 = ctx->shard_p1();
-  const bool seeded = seed && ctx->seed_valid;
-  const uint32_t* qp = query_perm(ctx);
-  {
-    ProfScope ps(ctx, kFamCorr);
-    HIPCK(launch_correspond(ctx->tgt.view, ctx->d_out, p0, p1, T.xf(), thr, seeded ? 1 : 0,
-                            ctx->prev_pos.p, ctx->flags.p, qp, ctx->stream));
-  }
-  ctx->seed_valid = true;
-  ctx->have_corr = false;  // the SoA streams of the BFGS mode are not refreshed
-  return moments_pass(ctx, T, G);
-}
-
-// Gauss-Newton estimate on the moments of the last sweep (taken at T); T <- solution.
-// 0 = accepted, MGICP_E_SOLVER = fewer than 4 correspondences or a singular normal matrix.
-int estimate_gn(mgicp_ctx* ctx, Mat4& T, int* n_corr) {
-  *n_corr = static_cast<int>(ctx->mom[73]);
-  if (ctx->mom[73] < 4) return MGICP_E_SOLVER;
-  gn::Problem pb;
-  pb.mom = ctx->mom;
-  gn::Pose P;
-  for (int a = 0; a < 3; ++a) {
-    pb.c[a] = ctx->out_ctr[a];
-    for (int k = 0; k < 4; ++k) pb.T0[a][k] = static_cast<double>(T.m[a][k]);
-    for (int k = 0; k < 3; ++k) P.R[a][k] = pb.T0[a][k];
-    P.t[a] = pb.T0[a][3];
-  }
-  int host_evals = 0;
-  if (!gn::solve(pb, P, ctx->prm.max_inner_iter, &host_evals)) return MGICP_E_SOLVER;
-  for (int a = 0; a < 3; ++a) {
-    for (int k = 0; k < 3; ++k) T.m[a][k] = static_cast<float>(P.R[a][k]);
-    T.m[a][3] = static_cast<float>(P.t[a]);
-  }
-  return MGICP_OK;
-}
-
-int check_params(mgicp_ctx* ctx, const mgicp_params& p) {
-  if (p.k < 1 || p.k > kMaxK)
-    return fail(ctx, MGICP_E_INVALID, "k (k_correspondences) must be in [1, 32]");
-  if (p.max_iter < 1 || p.max_inner_iter < 1 || !(p.max_corr_dist >= 0) || !(p.rot_eps > 0) ||
-      !(p.tf_eps >= 0) ||
-      (p.solver != MGICP_SOLVER_PCL_BFGS && p.solver != MGICP_SOLVER_GN))
-    return fail(ctx, MGICP_E_INVALID, "invalid GICP parameters");
-  return MGICP_OK;
-}
-
-}  // namespace
-
-// =====================================================================================
-// C-ABI
-// =====================================================================================
-extern "C" {
-
-void mgicp_default_params(mgicp_params* p) {
-  if (!p) return;
-  p->max_iter = 100;        // GICPAlignment.cpp:30
-  p->tf_eps = 4e-3;         // GICPAlignment.cpp:29
-  p->rot_eps = 2e-3;        // PCL GICP rotation_epsilon_
-  p->max_corr_dist = 4e-2;  // GICPAlignment.cpp:31
-  p->gicp_eps = 1e-3;       // PCL GICP gicp_epsilon_
-  p->k = 20;                // PCL GICP k_correspondences_
-  p->max_inner_iter = 20;   // PCL GICP max_inner_iterations_
-  p->solver = MGICP_SOLVER_PCL_BFGS;
-  p->device = -1;
-  p->fixed_iterations = 0;
-}
-
-int mgicp_device_count(int* n) {
-  if (!n) return MGICP_E_INVALID;
-  return hipGetDeviceCount(n) == hipSuccess ? MGICP_OK : MGICP_E_HIP;
-}
-
-int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
-  if (!out) return MGICP_E_INVALID;
-  *out = nullptr;
-  mgicp_ctx* ctx = new mgicp_ctx();
-  if (const char* occ = std::getenv("MGICP_GRID_OCC")) {
-    const double v = std::atof(occ);
-    if (v >= 1.0 && v <= 256.0) ctx->occupancy = v;
-  }
-  if (const char* ff = std::getenv("MGICP_FUSED_FINISH")) ctx->fused_finish = std::atoi(ff) != 0;
-  if (const char* fa = std::getenv("MGICP_FDF_ALT")) ctx->alt_sweep = std::atoi(fa) != 0;
-  if (const char* po = std::getenv("MGICP_POLL")) ctx->poll = std::atoi(po) != 0;
-  if (const char* ga = std::getenv("MGICP_GATED")) ctx->gated = std::atoi(ga) != 0;
-  if (const char* ps = std::getenv("MGICP_PROF_STRIDE")) ctx->prof_stride = std::max(1, std::atoi(ps));
-  if (const char* qo = std::getenv("MGICP_QUERY_ORDER")) ctx->query_order = std::atoi(qo) != 0;
-  if (const char* so = std::getenv("MGICP_SRC_GRID_OCC")) {
-    const double v = std::atof(so);
-    if (v >= 1.0 && v <= 256.0) ctx->src.occupancy = v;
-  }
-  {
-    const unsigned hc = std::thread::hardware_concurrency();
-    ctx->host_threads = static_cast<int>(std::max(1u, std::min(8u, hc ? hc : 1u)));
-    if (const char* ht = std::getenv("MGICP_HOST_THREADS")) {
-      const int v = std::atoi(ht);
-      if (v >= 1 && v <= 64) ctx->host_threads = v;
-    }
-  }
-  if (const char* fb = std::getenv("MGICP_FDF_BLOCKS")) {
-    const int v = std::atoi(fb);
-    if (v >= 1 && v <= 65536) ctx->fdf_max_blocks = v;
-  }
-  if (p) ctx->prm = *p;
-  else mgicp_default_params(&ctx->prm);
-  int rc = check_params(ctx, ctx->prm);
-  if (rc) {
-    delete ctx;
-    return rc;
-  }
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
-    delete ctx;
-    return MGICP_E_HIP;
-  }
-  if (ctx->prm.device >= 0) {
-    if (ctx->prm.device >= ndev || hipSetDevice(ctx->prm.device) != hipSuccess) {
-      delete ctx;
-      return MGICP_E_INVALID;
-    }
-    ctx->device = ctx->prm.device;
-  } else if (hipGetDevice(&ctx->device) != hipSuccess) {
-    delete ctx;
-    return MGICP_E_HIP;
-  }
-  ctx->tgt.want_empty_map = true;  // correspondence / fitness queries start off the surface
-  if (const char* em = std::getenv("MGICP_EMPTY_MAP")) ctx->tgt.want_empty_map = std::atoi(em) != 0;
-  // per-cell point boxes in the 1-NN sweeps: exact and 1.75x fewer candidates in sweep 1, but the
-  // per-cell box loads and tests cost more than they save (C4 correspondence 1.39 vs 1.11 ms,
-  // profiles/r02/ab_boxes): off by default, knob MGICP_CELL_BOXES=1
-  ctx->tgt.want_boxes = false;
-  if (const char* cb = std::getenv("MGICP_CELL_BOXES")) ctx->tgt.want_boxes = std::atoi(cb) != 0;
-  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
-    delete ctx;
-    return MGICP_E_HIP;
-  }
-  if (hipHostMalloc(reinterpret_cast<void**>(&ctx->h_small), kSmallBytes,
-                    hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
-      hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->d_small), ctx->h_small, 0) != hipSuccess ||
-      preload_kernels(ctx->h_small, kSmallBytes, ctx->stream) != hipSuccess ||
-      HostUploader::instance().init(ctx->host_threads) != hipSuccess) {
-    if (ctx->h_small) (void)hipHostFree(ctx->h_small);
-    (void)hipStreamDestroy(ctx->stream);
-    delete ctx;
-    return MGICP_E_HIP;
-  }
-  *out = ctx;
-  return MGICP_OK;
-}
-
-int mgicp_set_params(mgicp_ctx* ctx, const mgicp_params* p) {
-  if (!ctx || !p) return MGICP_E_INVALID;
-  int rc = check_params(ctx, *p);
-  if (rc) return rc;
-  const bool cov_change = p->k != ctx->prm.k || p->gicp_eps != ctx->prm.gicp_eps;
-  const int dev = ctx->device;
-  ctx->prm = *p;
-  ctx->prm.device = dev;
-  if (cov_change) {
-    ctx->src.have_cov = false;
-    ctx->tgt.have_cov = false;
-  }
-  return MGICP_OK;
-}
-
-const char* mgicp_last_error(const mgicp_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
-
-void mgicp_destroy(mgicp_ctx* ctx) {
-  if (!ctx) return;
-  (void)hipSetDevice(ctx->device);
-  cancel_gated(ctx);
-  (void)hipStreamSynchronize(ctx->stream);
-  ctx->f_flags.release(); ctx->f_pos.release(); ctx->f_rgba_in.release(); ctx->f_rgba.release();
-  ctx->f_rgba2.release(); ctx->f_vox.release(); ctx->f_vox2.release(); ctx->f_keep.release();
-  ctx->f_count.release();
-  for (Cloud* c : {&ctx->src, &ctx->tgt, &ctx->aux, &ctx->qry}) {
-    c->raw.release(); c->orig.release(); c->pts.release(); c->perm.release();
-    c->cell_start.release(); c->cov.release(); c->empty_dist.release(); c->boxes.release();
-  }
-  ctx->src_out.release();
-  ctx->qperm.release();
-  ctx->partial.release(); ctx->red.release(); ctx->mpartial.release(); ctx->mred.release(); ctx->counts.release(); ctx->keys.release();
-  ctx->keys_sorted.release(); ctx->vals.release(); ctx->scratch.release(); ctx->u64.release();
-  ctx->fpartial.release();
-  ctx->ticket.release();
-  ctx->prev_pos.release(); ctx->flags.release(); ctx->cpos.release();
-  ctx->corr_f.release(); ctx->corr_d.release(); ctx->cscratch.release();
-  ctx->xyz_dev.release();
-  if (ctx->mail) (void)hipFree(ctx->mail);
-  if (ctx->h_red) (void)hipHostFree(ctx->h_red);
-  if (ctx->h_cmd) (void)hipHostFree(ctx->h_cmd);
-  if (ctx->h_gtrace) (void)hipHostFree(ctx->h_gtrace);
-  if (ctx->h_small) (void)hipHostFree(ctx->h_small);
-  prof_resolve(ctx);
-  for (hipEvent_t e : ctx->pool) (void)hipEventDestroy(e);
-  if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
-  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
-  delete ctx;
-}
-
-int mgicp_set_target(mgicp_ctx* ctx, const float* xyz, size_t n, size_t stride) {
-  if (!ctx) return MGICP_E_INVALID;
-  HIPCK(hipSetDevice(ctx->device));
-  return upload_cloud(ctx, ctx->tgt, xyz, n, stride, false);
-}
-int mgicp_set_source(mgicp_ctx* ctx, const float* xyz, size_t n, size_t stride) {
-  if (!ctx) return MGICP_E_INVALID;
-  HIPCK(hipSetDevice(ctx->device));
-  return upload_cloud(ctx, ctx->src, xyz, n, stride, false);
-}
-int mgicp_set_target_device(mgicp_ctx* ctx, const float* d_xyz, size_t n, size_t stride) {
-  if (!ctx) return MGICP_E_INVALID;
-  HIPCK(hipSetDevice(ctx->device));
-  return upload_cloud(ctx, ctx->tgt, d_xyz, n, stride, true);
-}
-int mgicp_set_source_device(mgicp_ctx* ctx, const float* d_xyz, size_t n, size_t stride) {
-  if (!ctx) return MGICP_E_INVALID;
-  HIPCK(hipSetDevice(ctx->device));
-  return upload_cloud(ctx, ctx->src, d_xyz, n, stride, true);
-}
-
-int mgicp_align(mgicp_ctx* ctx, const float guess_cm[16], float out_T_cm[16], mgicp_result* res) {
-  if (!ctx || !out_T_cm) return MGICP_E_INVALID;
-  if (ctx->nranks > 1 && !ctx->comm)
-    return fail(ctx, MGICP_E_INVALID, "detached shard context: only the debug entry points are available");
-  HIPCK(hipSetDevice(ctx->device));
-  mgicp_result r;
-  std::memset(&r, 0, sizeof(r));
-  const double t0 = now_ms();
-  MGICP_TRACE_AT("align: begin");
-  int rc = prepare(ctx, true);
-  if (rc) return rc;
-  MGICP_TRACE_AT("align: prepared");
-  rc = ensure_iter_buffers(ctx);
-  if (rc) return rc;
-  MGICP_TRACE_AT("align: iteration buffers ready");
-  const double t1 = now_ms();
-  const Mat4 G = guess_cm ? Mat4::from_cm(guess_cm) : Mat4::identity();
-  if ((rc = set_output(ctx, G))) return rc;
-
-  Mat4 T = Mat4::identity(), prev = Mat4::identity();
-  ctx->trace.clear();
-  ctx->n_evals = 0;
-  int nr_iterations = 0;
-  bool converged = false;
-  int solver_rc = MGICP_OK;
-  while (!converged) {
-    const bool gn_mode = ctx->prm.solver == MGICP_SOLVER_GN;
-    rc = gn_mode ? correspond_gn(ctx, T, G, nr_iterations > 0)
-                 : correspond(ctx, T, G, nr_iterations > 0);
-    if (rc) return rc;
-    prev = T;
-    int ncorr = 0;
-    rc = gn_mode ? estimate_gn(ctx, T, &ncorr) : estimate_bfgs(ctx, T, &ncorr);
-    r.n_corr = ncorr;
-    if (rc == MGICP_E_SOLVER) {  // PCLException caught: converged_ stays false
-      T = prev;
-      solver_rc = rc;
-      break;
-    }
-    if (rc) return rc;
-    double delta = 0.;
-    for (int k = 0; k < 4; ++k)
-      for (int l = 0; l < 4; ++l) {
-        const double ratio = (k < 3 && l < 3) ? 1. / ctx->prm.rot_eps : 1. / ctx->prm.tf_eps;
-        const double c_delta = ratio * static_cast<double>(std::fabs(prev.m[k][l] - T.m[k][l]));
-        if (c_delta > delta) delta = c_delta;
-      }
-    float tcm[16];
-    T.to_cm(tcm);
-    ctx->trace.insert(ctx->trace.end(), tcm, tcm + 16);
-    nr_iterations++;
-    const bool stop = ctx->prm.fixed_iterations
-                          ? nr_iterations >= ctx->prm.max_iter
-                          : (nr_iterations >= ctx->prm.max_iter || delta < 1);
-    if (stop) {
-      converged = true;
-      prev = T;
-    }
-  }
-  // polled passes leave their kernels' completion unobserved: drain the stream once
-  if ((rc = sync(ctx))) return rc;
-  if (ctx->h_gtrace) {
-    // diagnostics of the gated passes of this align: device-side gate wait and spread, host-side
-    // decision time (sums seen -> command published); device wall clock in 10 ns ticks (100 MHz)
-    double w = 0, sp = 0, hd = 0;
-    int cnt = 0;
-    for (int i = 0; i < 1024; ++i) {
-      const unsigned long long* t = ctx->h_gtrace + 4 * i;
-      if (!t[0] || !t[1] || !t[2] || ctx->host_gt[2 * i + 1] <= 0 || ctx->host_gt[2 * i] <= 0) continue;
-      w += (t[1] - t[0]) * 0.01;
-      sp += (static_cast<double>(t[2]) - static_cast<double>(t[1])) * 0.01;
-      hd += ctx->host_gt[2 * i + 1] - ctx->host_gt[2 * i];
-      ++cnt;
-    }
-    if (cnt)
-      std::fprintf(stderr, "[gate-trace] passes %d | device: block-0 wait %.2f us, last block through the gate +%.2f us | host: sums seen -> command published %.2f us\n",
-                   cnt, w / cnt, sp / cnt, hd / cnt);
-    {
-      std::vector<std::pair<double, int>> bt;
-      unsigned long long mn = ~0ull;
-      for (int b = 0; b < 512; ++b)
-        if (ctx->h_gtrace[4096 + b]) mn = std::min(mn, ctx->h_gtrace[4096 + 512 + b]);
-      for (int b = 0; b < 512; ++b)
-        if (ctx->h_gtrace[4096 + b]) bt.push_back({(ctx->h_gtrace[4096 + b] - mn) * 0.01, b});
-      std::sort(bt.begin(), bt.end());
-      std::fprintf(stderr, "[gate-trace] last pass, per block through-gate (us after first block start):");
-      for (size_t i = 0; i < bt.size(); i += 16) std::fprintf(stderr, " %.2f(b%d)", bt[i].first, bt[i].second);
-      if (!bt.empty()) std::fprintf(stderr, " last %.2f(b%d)", bt.back().first, bt.back().second);
-      std::vector<double> st;
-      for (int b = 0; b < 512; ++b)
-        if (ctx->h_gtrace[4096 + b]) st.push_back((ctx->h_gtrace[4096 + 512 + b] - mn) * 0.01);
-      std::sort(st.begin(), st.end());
-      if (!st.empty()) std::fprintf(stderr, " | block starts: median %.2f max %.2f", st[st.size() / 2], st.back());
-      std::fprintf(stderr, "\n");
-    }
-    std::memset(ctx->h_gtrace, 0, 4 * 1024 * sizeof(unsigned long long));
     std::fill(ctx->host_gt.begin(), ctx->host_gt.end(), 0.0);
   }
   // final_transformation_ = previous_transformation_ (3x3) * guess (3x3); t = prev t + guess t
