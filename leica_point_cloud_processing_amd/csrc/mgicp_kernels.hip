@@ -30,6 +30,10 @@
 #ifndef MGICP_CORR_STATS
 #define MGICP_CORR_STATS 0  // 1: count 1-NN work per sweep (diagnostic builds only)
 #endif
+#ifndef MGICP_SEED_BOX
+#define MGICP_SEED_BOX 1  // seeded 1-NN queries search the cube of their seed's ball (box_search)
+#endif
+constexpr bool kSeedBox = MGICP_SEED_BOX != 0;
 
 #include "mgicp_internal.hpp"
 
@@ -362,25 +366,58 @@ struct NnVisitor {
     ntest += b - a;
     nrange += 1;
 #endif
-#if MGICP_NN_UNROLL >= 8
-    for (; j + 8 <= b; j += 8) {  // eight gathers in flight per lane (latency-bound loop)
-      float4 p[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) p[u] = g.pts[j + u];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) test(p[u], j + u);
-    }
-#endif
-    for (; j + 4 <= b; j += 4) {  // four gathers in flight per lane (latency-bound loop)
-      const float4 p0 = g.pts[j], p1 = g.pts[j + 1], p2 = g.pts[j + 2], p3 = g.pts[j + 3];
+    // a moving pointer: the four loads of a step share one 64-bit address (immediate offsets);
+    // indexing g.pts[j + u] with a 32-bit j recomputed a 64-bit address per candidate (the
+    // sweep is VALU-bound: SQ_INSTS_VALU x 4 cycles = the kernel time)
+    const float4* q = g.pts + a;
+    const uint32_t n4 = (b - a) >> 2;
+    for (uint32_t i = 0; i < n4; ++i, q += 4, j += 4) {
+      const float4 p0 = q[0], p1 = q[1], p2 = q[2], p3 = q[3];
       test(p0, j);
       test(p1, j + 1);
       test(p2, j + 2);
       test(p3, j + 3);
     }
-    for (; j < b; ++j) test(g.pts[j], j);
+    for (; j < b; ++j, ++q) test(*q, j);
   }
 };
+
+// Exact search of the cube [q - R, q + R] of cells, R = the visitor's current bound (a real seed
+// candidate, so the nearest point lies inside): rows nearest to q first, each row's x-range and
+// each row itself pruned by the shrinking bound exactly as in ring_search.  For a seeded query
+// it visits the rows of the seed's ball once, without ring_search's per-ring face bounds and the
+// rows of whole Chebyshev shells (sweeps >= 2 of the correspondence loop).
+template <class V>
+__device__ __forceinline__ void box_search(const GridView& g, float qx, float qy, float qz, V& vis) {
+  const float R = sqrtf(vis.prune2() * 1.00001f) + g.slop;
+  const int za = max(qcell(qz - R, g.oz, g.inv_h), 0), zb = min(qcell(qz + R, g.oz, g.inv_h), g.nz - 1);
+  const int ya = max(qcell(qy - R, g.oy, g.inv_h), 0), yb = min(qcell(qy + R, g.oy, g.inv_h), g.ny - 1);
+  const int zc = min(max(qcell(qz, g.oz, g.inv_h), za), zb), yc = min(max(qcell(qy, g.oy, g.inv_h), ya), yb);
+  const int zdn = near_side(qz, g.oz, g.h, zc), ydn = near_side(qy, g.oy, g.h, yc);
+  const int zspan = 2 * max(zc - za, zb - zc), yspan = 2 * max(yc - ya, yb - yc);
+  for (int mz = 0; mz <= zspan; ++mz) {
+    const int z = zc + ((mz & 1) ? zdn : -zdn) * ((mz + 1) >> 1);
+    if (z < za || z > zb) continue;
+    const float gz = cell_gap(qz, g.oz, g.h, z, g.slop);
+    const float gz2 = gz * gz;
+    if (gz2 > vis.prune2() * 1.00001f) continue;
+    const uint32_t* zrow = g.cell_start + static_cast<size_t>(z) * g.ny * g.nx;
+    for (int my = 0; my <= yspan; ++my) {
+      const int y = yc + ((my & 1) ? ydn : -ydn) * ((my + 1) >> 1);
+      if (y < ya || y > yb) continue;
+      const float w = vis.prune2() * 1.00001f;
+      const float gy = cell_gap(qy, g.oy, g.h, y, g.slop);
+      const float gyz = gy * gy + gz2;
+      if (gyz > w) continue;
+      const float rx = sqrtf(w - gyz) + g.slop;
+      const int xa = max(qcell(qx - rx, g.ox, g.inv_h), 0);
+      const int xb = min(qcell(qx + rx, g.ox, g.inv_h), g.nx - 1);
+      if (xa > xb) continue;
+      const uint32_t* row = zrow + static_cast<uint32_t>(y) * static_cast<uint32_t>(g.nx);
+      vis.range(g, row[xa], row[xb + 1]);
+    }
+  }
+}
 
 // radius-count visitor: counts points with float d2 < r2 (FLANN RadiusResultSet: dist < radius),
 // stopping as soon as `need` are found
@@ -680,6 +717,7 @@ __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_kernel(GridV
     if (pp != 0xffffffffu) vis.range(tg, pp, pp + 1);
   }
   if (tg.boxes) ring_search_boxed(tg, qx, qy, qz, vis);
+  else if (kSeedBox && vis.best != ~0ull) box_search(tg, qx, qy, qz, vis);
   else ring_search(tg, qx, qy, qz, vis);
   const bool ok = vis.best != ~0ull &&
                   static_cast<double>(__uint_as_float(static_cast<uint32_t>(vis.best >> 32))) < thr;
