@@ -303,6 +303,8 @@ struct mgicp_ctx {
   DevBuf<uint32_t> counts, keys, keys_sorted, vals;
   DevBuf<unsigned char> scratch;
   DevBuf<unsigned long long> u64;
+  DevBuf<uint32_t> knn_fb;          // points the logged k-NN kernel leaves to the register-list one
+  unsigned int knn_fallbacks = 0;   // their count in the last covariance launch
   DevBuf<float> fpartial;
   // multi-GPU
   int nranks = 1, rank = 0;
@@ -689,9 +691,33 @@ int compute_cov(mgicp_ctx* ctx, Cloud& cl, size_t p0, size_t p1) {
   // grid order, not Morton order: the k = 20 queries sit on the surface and the row-major order
   // measured faster (3.97 vs 4.42 ms at 5M, profiles/r01/ab_qorder/)
   const uint32_t* perm = nullptr;
+  const bool logged = knn_logged_enabled();
+  if (logged) {
+    HIPCK(ctx->knn_fb.reserve(p1 - p0));
+    HIPCK(ctx->u64.reserve(1));
+    HIPCK(hipMemsetAsync(ctx->u64.p, 0, sizeof(unsigned long long), ctx->stream));
+  }
+  unsigned int* fb_count = reinterpret_cast<unsigned int*>(ctx->u64.p);
   {
     ProfScope ps(ctx, kFamCov);
-    HIPCK(launch_knn_cov(cl.view, ctx->prm.k, ctx->prm.gicp_eps, p0, p1, cl.cov3(), perm, ctx->stream));
+    HIPCK(launch_knn_cov(cl.view, ctx->prm.k, ctx->prm.gicp_eps, p0, p1, cl.cov3(), perm,
+                         logged ? ctx->knn_fb.p : nullptr, logged ? fb_count : nullptr, ctx->stream));
+  }
+  if (logged) {
+    // the points the logged kernel left to the register-list kernel (log overflow, ties at tau)
+    HIPCK(hipMemcpyAsync(ctx->h_small, fb_count, sizeof(unsigned int), hipMemcpyDeviceToHost, ctx->stream));
+    int rc0 = sync(ctx);
+    if (rc0) return rc0;
+    unsigned int nfb = 0;
+    std::memcpy(&nfb, ctx->h_small, sizeof(nfb));
+    ctx->knn_fallbacks = nfb;
+    static const bool stats = std::getenv("MGICP_KNN_STATS") != nullptr;
+    if (stats) std::fprintf(stderr, "[knn] %zu points, %u left to the register-list kernel\n", p1 - p0, nfb);
+    if (nfb) {
+      ProfScope ps(ctx, kFamCov);
+      HIPCK(launch_knn_cov(cl.view, ctx->prm.k, ctx->prm.gicp_eps, 0, nfb, cl.cov3(), ctx->knn_fb.p, nullptr,
+                           nullptr, ctx->stream));
+    }
   }
   int rc = sync(ctx);
   if (rc) return rc;
@@ -1283,6 +1309,7 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   ctx->partial.release(); ctx->red.release(); ctx->mpartial.release(); ctx->mred.release(); ctx->counts.release(); ctx->keys.release();
   ctx->keys_sorted.release(); ctx->vals.release(); ctx->scratch.release(); ctx->u64.release();
   ctx->fpartial.release();
+  ctx->knn_fb.release();
   ctx->ticket.release();
   ctx->prev_pos.release(); ctx->flags.release(); ctx->cpos.release();
   ctx->corr_f.release(); ctx->corr_d.release(); ctx->cscratch.release();

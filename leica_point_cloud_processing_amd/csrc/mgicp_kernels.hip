@@ -39,6 +39,8 @@ constexpr bool kSeedBox = MGICP_SEED_BOX != 0;
 
 #include <hipcub/hipcub.hpp>
 
+#include <cstdlib>
+
 namespace mgicp {
 
 // ------------------------------------------------------------------------------------
@@ -609,6 +611,98 @@ __device__ __forceinline__ double sel3(int i, double a, double b, double c) {
   return i == 0 ? a : (i == 1 ? b : c);
 }
 
+// ---- two-phase k-NN selection (knn_cov2_kernel) ----------------------------------------------
+// Phase 1 finds the EXACT k-th smallest float d2 (tau) with a branch-free network over a register
+// list of float keys: key[j] = max(key[j-1], min(d2, key[j])) = med3(key[j-1], d2, key[j]) (the
+// list is ascending; d2 is finite) inserts d2 in ONE v_med3_f32 per slot (the (d2, index) insert
+// with 64-bit keys and positions costs ~8 per slot, and in SIMT every lane pays it whenever ANY
+// lane inserts: knn_cov was VALU-bound at 25k instructions per wave).
+// With a log (LOG > 0) every candidate whose d2 does not exceed the CURRENT k-th is appended to the
+// lane's LDS log as its sorted position (the (d2, original index) key is recomputed from the point,
+// bit-identically, when the log is read): thresholds only fall, so the log holds every member of the
+// final k-NN set (ties at the final k-th included) -- no second search.
+template <int K, int LOG>
+struct KthVisitor {
+  static constexpr bool kNearFirst = true;
+  float qx, qy, qz;
+  float key[K];  // ascending; the first nsent slots hold the sentinel -1 (always in front)
+  uint32_t* lpos;  // lane-strided LDS log of sorted positions (LOG > 0)
+  int cnt;
+  __device__ __forceinline__ void init(float x, float y, float z, int nsent) {
+    qx = x; qy = y; qz = z;
+    cnt = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) key[k] = k < nsent ? -1.f : INFINITY;
+  }
+  __device__ __forceinline__ bool done(float Ls) const { return Ls > 0.f && key[K - 1] < Ls * Ls; }
+  __device__ __forceinline__ float prune2() const { return key[K - 1]; }
+  const float4* pts;
+  // a full log drops the entries the threshold has since passed (d2 recomputed from the point)
+  __device__ __forceinline__ void compact() {
+    int m = 0;
+    for (int i = 0; i < cnt; ++i) {
+      const uint32_t j = lpos[i * 64];
+      if (dist2(qx, qy, qz, pts[j]) <= key[K - 1]) lpos[(m++) * 64] = j;
+    }
+    cnt = m;
+  }
+  __device__ __forceinline__ void test(float d, float w, uint32_t j) {
+    if (LOG > 0 && d <= key[K - 1]) {
+      if (cnt == LOG) compact();
+      if (cnt < LOG) lpos[cnt * 64] = j;
+      ++cnt;
+    }
+    if (d < key[K - 1]) {  // (a value equal to the k-th leaves the multiset of the k smallest as is)
+#pragma unroll
+      for (int k = K - 1; k > 0; --k) key[k] = __builtin_amdgcn_fmed3f(key[k - 1], d, key[k]);
+      key[0] = fminf(d, key[0]);
+    }
+  }
+  __device__ __forceinline__ void range(const GridView& g, uint32_t a, uint32_t b) {
+    const float4* q = g.pts + a;
+    uint32_t j = a;
+    for (; j + 4 <= b; j += 4, q += 4) {
+      const float4 p0 = q[0], p1 = q[1], p2 = q[2], p3 = q[3];
+      test(dist2(qx, qy, qz, p0), p0.w, j);
+      test(dist2(qx, qy, qz, p1), p1.w, j + 1);
+      test(dist2(qx, qy, qz, p2), p2.w, j + 2);
+      test(dist2(qx, qy, qz, p3), p3.w, j + 3);
+    }
+    for (; j < b; ++j, ++q) test(dist2(qx, qy, qz, *q), q->w, j);
+  }
+};
+
+// Batcher's odd-even merge sort of N (power of two) register-resident (key, pos) pairs, every
+// index a compile-time constant
+template <int N>
+__device__ __forceinline__ void oem_sort(unsigned long long (&k)[N], uint32_t (&v)[N]) {
+#pragma unroll
+  for (int p = 1; p < N; p <<= 1)
+#pragma unroll
+    for (int q = p; q >= 1; q >>= 1)
+#pragma unroll
+      for (int j = q % p; j <= N - 1 - q; j += 2 * q)
+#pragma unroll
+        for (int i = 0; i < q; ++i) {
+          if (i > N - j - q - 1) continue;
+          if ((i + j) / (2 * p) != (i + j + q) / (2 * p)) continue;
+          const int a = i + j, b = i + j + q;
+          const bool sw = k[b] < k[a];
+          const unsigned long long ka = k[a], kb = k[b];
+          const uint32_t va = v[a], vb = v[b];
+          k[a] = sw ? kb : ka;
+          k[b] = sw ? ka : kb;
+          v[a] = sw ? vb : va;
+          v[b] = sw ? va : vb;
+        }
+}
+
+// PCL's covariance of the k = K - nsent neighbours at sorted positions pos[nsent..K) (in (d2,
+// index) order), regularised and stored at p (shared by both k-NN kernels)
+template <int K>
+__device__ __forceinline__ void cov_from_sorted(const GridView& g, double eps, const uint32_t (&pos)[K],
+                                                int nsent, Cov3 cov, size_t p);
+
 // `perm` (optional): query order over [p0, p1) (Morton order: compact 3-D patch per wave)
 // k = K - nsent neighbours (nsent > 0 only on the generic rounded-up instantiations)
 template <int K>
@@ -622,13 +716,18 @@ __global__ __launch_bounds__(256, MGICP_COV_WAVES) void knn_cov_kernel(GridView 
   KnnVisitor<K> vis;
   vis.init(q.x, q.y, q.z, nsent);
   ring_search(g, q.x, q.y, q.z, vis);
+  cov_from_sorted<K>(g, eps, vis.pos, nsent, cov, p);
+}
 
+template <int K>
+__device__ __forceinline__ void cov_from_sorted(const GridView& g, double eps, const uint32_t (&pos)[K],
+                                                int nsent, Cov3 cov, size_t p) {
   double m0 = 0.0, m1 = 0.0, m2 = 0.0;
   double a[3][3] = {{0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}};
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     if (k < nsent) continue;
-    const float4 pt = g.pts[vis.pos[k]];
+    const float4 pt = g.pts[pos[k]];
     m0 += pt.x;
     m1 += pt.y;
     m2 += pt.z;
@@ -680,6 +779,74 @@ __global__ __launch_bounds__(256, MGICP_COV_WAVES) void knn_cov_kernel(GridView 
   cov.a[p] = make_double2(C00, C01);
   cov.b[p] = make_double2(C02, C11);
   cov.c[p] = make_double2(C12, C22);
+}
+
+// Logged-threshold k-NN covariance (default): ONE near-first ring search finds the exact k-th float
+// d2 (tau) with KthVisitor's min/max network while logging every candidate that was within the
+// threshold of its time into the lane's LDS log; the log entries with d2 <= tau are exactly the k
+// nearest plus any ties at tau, sorted by (d2, original index) with a static odd-even merge network
+// -- the first k are KnnVisitor's list.  A lane whose log overflows (or whose ties at tau exceed
+// the sort width) is listed in fb for KnnVisitor (knn_cov_kernel over that list).  64-thread blocks,
+// LOG x 4 bytes of LDS per lane (12 KB per wave: ~3 waves per SIMD).
+template <int K>
+constexpr int knn2_sort() { return K <= 8 ? 16 : 32; }
+constexpr int kKnnLog = 48;
+
+__device__ __forceinline__ unsigned long long knn_key(const GridView& g, float qx, float qy, float qz,
+                                                      uint32_t j) {
+  const float4 pt = g.pts[j];
+  return mkkey(dist2(qx, qy, qz, pt), pt.w);
+}
+
+template <int K>
+__global__ __launch_bounds__(64) void knn_cov2_kernel(GridView g, double eps, size_t p0, size_t p1, Cov3 cov,
+                                                      const uint32_t* __restrict__ perm, int nsent,
+                                                      uint32_t* __restrict__ fb, unsigned int* __restrict__ fb_count) {
+  constexpr int S = knn2_sort<K>();
+  __shared__ uint32_t s_pos[kKnnLog * 64];
+  const size_t t = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= p1 - p0) return;
+  const size_t p = p0 + (perm ? perm[t] : t);
+  const float4 q = g.pts[p];
+  KthVisitor<K, kKnnLog> v1;
+  v1.init(q.x, q.y, q.z, nsent);
+  v1.lpos = s_pos + threadIdx.x;
+  v1.pts = g.pts;
+  ring_search(g, q.x, q.y, q.z, v1);
+  if (v1.cnt > kKnnLog) {
+    // log overflow even after compaction (ties): KnnVisitor finishes this point in a follow-up
+    // launch over the list
+    fb[atomicAdd(fb_count, 1u)] = static_cast<uint32_t>(p);
+    return;
+  }
+  const float tau = v1.key[K - 1];
+  // the log entries within tau, compacted in place (log order kept)
+  int m = 0;
+  for (int i = 0; i < v1.cnt; ++i) {
+    const uint32_t j = s_pos[i * 64 + threadIdx.x];
+    if (dist2(q.x, q.y, q.z, g.pts[j]) <= tau) {
+      s_pos[m * 64 + threadIdx.x] = j;
+      ++m;
+    }
+  }
+  if (m > S) {  // more ties at tau than the sort width (lattices): KnnVisitor, as above
+    fb[atomicAdd(fb_count, 1u)] = static_cast<uint32_t>(p);
+    return;
+  }
+  unsigned long long kk[S];
+  uint32_t vv[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    const bool in = i < m;
+    vv[i] = in ? s_pos[i * 64 + threadIdx.x] : 0u;
+    kk[i] = in ? knn_key(g, q.x, q.y, q.z, vv[i]) : ~0ull;
+  }
+  oem_sort<S>(kk, vv);
+  // neighbour j of k sits in slot nsent + j (the sentinel slots of KnnVisitor)
+  uint32_t pos[K];
+#pragma unroll
+  for (int i = 0; i < K; ++i) pos[i] = i < nsent ? 0u : vv[i - nsent < 0 ? 0 : i - nsent];
+  cov_from_sorted<K>(g, eps, pos, nsent, cov, p);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1479,33 +1646,48 @@ hipError_t launch_iota(uint32_t* v, size_t n, hipStream_t s) {
   return hipGetLastError();
 }
 
+static bool knn_two_phase() {  // env MGICP_KNN2 (default 1): knn_cov2_kernel, else knn_cov_kernel
+  static const bool on = [] {
+    const char* e = std::getenv("MGICP_KNN2");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
+
 template <int K>
 static hipError_t knn_cov_k(const GridView& g, double eps, size_t p0, size_t p1, Cov3 cov,
-                            const uint32_t* perm, int k, hipStream_t s) {
-  knn_cov_kernel<K><<<nblk(p1 - p0), 256, 0, s>>>(g, eps, p0, p1, cov, perm, K - k);
+                            const uint32_t* perm, int k, uint32_t* fb, unsigned int* fb_count, hipStream_t s) {
+  if (fb && knn_two_phase())
+    knn_cov2_kernel<K><<<nblk(p1 - p0, 64), 64, 0, s>>>(g, eps, p0, p1, cov, perm, K - k, fb, fb_count);
+  else
+    knn_cov_kernel<K><<<nblk(p1 - p0), 256, 0, s>>>(g, eps, p0, p1, cov, perm, K - k);
   return hipGetLastError();
 }
 
 // exact instantiations for PCL's default (20) and its round neighbours; any other k in
-// [1, kMaxK] runs on the next multiple of 8 with K - k sentinel slots
+// [1, kMaxK] runs on the next multiple of 8 with K - k sentinel slots.  With fb / fb_count the
+// logged-threshold kernel runs and lists the points it leaves to KnnVisitor; without, (or for that
+// list: perm = fb, p0 = 0, p1 = count) the register-list kernel runs.
 hipError_t launch_knn_cov(const GridView& g, int k, double eps, size_t p0, size_t p1, Cov3 cov,
-                          const uint32_t* perm, hipStream_t s) {
+                          const uint32_t* perm, uint32_t* fb, unsigned int* fb_count, hipStream_t s) {
   if (p1 <= p0) return hipSuccess;
   switch (k) {
-    case 5: return knn_cov_k<5>(g, eps, p0, p1, cov, perm, k, s);
-    case 10: return knn_cov_k<10>(g, eps, p0, p1, cov, perm, k, s);
-    case 15: return knn_cov_k<15>(g, eps, p0, p1, cov, perm, k, s);
-    case 20: return knn_cov_k<20>(g, eps, p0, p1, cov, perm, k, s);
-    case 25: return knn_cov_k<25>(g, eps, p0, p1, cov, perm, k, s);
-    case 30: return knn_cov_k<30>(g, eps, p0, p1, cov, perm, k, s);
+    case 5: return knn_cov_k<5>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s);
+    case 10: return knn_cov_k<10>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s);
+    case 15: return knn_cov_k<15>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s);
+    case 20: return knn_cov_k<20>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s);
+    case 25: return knn_cov_k<25>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s);
+    case 30: return knn_cov_k<30>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s);
     default: break;
   }
   if (k < 1 || k > kMaxK) return hipErrorInvalidValue;
-  if (k <= 8) return knn_cov_k<8>(g, eps, p0, p1, cov, perm, k, s);
-  if (k <= 16) return knn_cov_k<16>(g, eps, p0, p1, cov, perm, k, s);
-  if (k <= 24) return knn_cov_k<24>(g, eps, p0, p1, cov, perm, k, s);
-  return knn_cov_k<32>(g, eps, p0, p1, cov, perm, k, s);
+  if (k <= 8) return knn_cov_k<8>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s);
+  if (k <= 16) return knn_cov_k<16>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s);
+  if (k <= 24) return knn_cov_k<24>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s);
+  return knn_cov_k<32>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s);
 }
+
+bool knn_logged_enabled() { return knn_two_phase(); }
 
 hipError_t launch_correspond(const GridView& tgt, const float4* src, size_t p0, size_t p1, Xf34 T,
                              double thr, int seeded, uint32_t* nn_pos, uint32_t* flags,
@@ -1705,6 +1887,16 @@ hipError_t preload_kernels(void* pinned, size_t pinned_bytes, hipStream_t s) {
       reinterpret_cast<const void*>(&knn_cov_kernel<16>),
       reinterpret_cast<const void*>(&knn_cov_kernel<24>),
       reinterpret_cast<const void*>(&knn_cov_kernel<32>),
+      reinterpret_cast<const void*>(&knn_cov2_kernel<5>),
+      reinterpret_cast<const void*>(&knn_cov2_kernel<10>),
+      reinterpret_cast<const void*>(&knn_cov2_kernel<15>),
+      reinterpret_cast<const void*>(&knn_cov2_kernel<20>),
+      reinterpret_cast<const void*>(&knn_cov2_kernel<25>),
+      reinterpret_cast<const void*>(&knn_cov2_kernel<30>),
+      reinterpret_cast<const void*>(&knn_cov2_kernel<8>),
+      reinterpret_cast<const void*>(&knn_cov2_kernel<16>),
+      reinterpret_cast<const void*>(&knn_cov2_kernel<24>),
+      reinterpret_cast<const void*>(&knn_cov2_kernel<32>),
       reinterpret_cast<const void*>(&correspond_kernel),
       reinterpret_cast<const void*>(&morton_key_kernel),
       reinterpret_cast<const void*>(&compact_kernel),
