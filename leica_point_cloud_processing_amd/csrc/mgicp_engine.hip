@@ -303,6 +303,7 @@ struct mgicp_ctx {
   DevBuf<uint32_t> counts, keys, keys_sorted, vals;
   DevBuf<unsigned char> scratch;
   DevBuf<unsigned long long> u64;
+  bool knn_logged = true;           // env MGICP_KNN2 at create: logged k-NN kernel, else register-list
   DevBuf<uint32_t> knn_fb;          // points the logged k-NN kernel leaves to the register-list one
   unsigned int knn_fallbacks = 0;   // their count in the last covariance launch
   DevBuf<float> fpartial;
@@ -691,7 +692,7 @@ int compute_cov(mgicp_ctx* ctx, Cloud& cl, size_t p0, size_t p1) {
   // grid order, not Morton order: the k = 20 queries sit on the surface and the row-major order
   // measured faster (3.97 vs 4.42 ms at 5M, profiles/r01/ab_qorder/)
   const uint32_t* perm = nullptr;
-  const bool logged = knn_logged_enabled();
+  const bool logged = ctx->knn_logged;
   if (logged) {
     HIPCK(ctx->knn_fb.reserve(p1 - p0));
     HIPCK(ctx->u64.reserve(1));
@@ -711,7 +712,7 @@ int compute_cov(mgicp_ctx* ctx, Cloud& cl, size_t p0, size_t p1) {
     unsigned int nfb = 0;
     std::memcpy(&nfb, ctx->h_small, sizeof(nfb));
     ctx->knn_fallbacks = nfb;
-    static const bool stats = std::getenv("MGICP_KNN_STATS") != nullptr;
+    const bool stats = std::getenv("MGICP_KNN_STATS") != nullptr;
     if (stats) std::fprintf(stderr, "[knn] %zu points, %u left to the register-list kernel\n", p1 - p0, nfb);
     if (nfb) {
       ProfScope ps(ctx, kFamCov);
@@ -1210,6 +1211,7 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
   if (const char* fa = std::getenv("MGICP_FDF_ALT")) ctx->alt_sweep = std::atoi(fa) != 0;
   if (const char* po = std::getenv("MGICP_POLL")) ctx->poll = std::atoi(po) != 0;
   if (const char* ga = std::getenv("MGICP_GATED")) ctx->gated = std::atoi(ga) != 0;
+  ctx->knn_logged = knn_logged_enabled();
   if (const char* ps = std::getenv("MGICP_PROF_STRIDE")) ctx->prof_stride = std::max(1, std::atoi(ps));
   if (const char* qo = std::getenv("MGICP_QUERY_ORDER")) ctx->query_order = std::atoi(qo) != 0;
   if (const char* so = std::getenv("MGICP_SRC_GRID_OCC")) {

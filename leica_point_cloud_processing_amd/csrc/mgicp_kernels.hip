@@ -617,17 +617,17 @@ __device__ __forceinline__ double sel3(int i, double a, double b, double c) {
 // list is ascending; d2 is finite) inserts d2 in ONE v_med3_f32 per slot (the (d2, index) insert
 // with 64-bit keys and positions costs ~8 per slot, and in SIMT every lane pays it whenever ANY
 // lane inserts: knn_cov was VALU-bound at 25k instructions per wave).
-// With a log (LOG > 0) every candidate whose d2 does not exceed the CURRENT k-th is appended to the
+// Every candidate whose d2 does not exceed the CURRENT k-th is appended to the
 // lane's LDS log as its sorted position (the (d2, original index) key is recomputed from the point,
 // bit-identically, when the log is read): thresholds only fall, so the log holds every member of the
 // final k-NN set (ties at the final k-th included) -- no second search.
-template <int K, int LOG>
+template <int K>
 struct KthVisitor {
   static constexpr bool kNearFirst = true;
   float qx, qy, qz;
   float key[K];  // ascending; the first nsent slots hold the sentinel -1 (always in front)
-  uint32_t* lpos;  // lane-strided LDS log of sorted positions (LOG > 0)
-  int cnt;
+  uint32_t* lpos;  // lane-strided LDS log of sorted positions, cap entries
+  int cnt, cap;
   __device__ __forceinline__ void init(float x, float y, float z, int nsent) {
     qx = x; qy = y; qz = z;
     cnt = 0;
@@ -647,9 +647,9 @@ struct KthVisitor {
     cnt = m;
   }
   __device__ __forceinline__ void test(float d, float w, uint32_t j) {
-    if (LOG > 0 && d <= key[K - 1]) {
-      if (cnt == LOG) compact();
-      if (cnt < LOG) lpos[cnt * 64] = j;
+    if (d <= key[K - 1]) {
+      if (cnt == cap) compact();
+      if (cnt < cap) lpos[cnt * 64] = j;
       ++cnt;
     }
     if (d < key[K - 1]) {  // (a value equal to the k-th leaves the multiset of the k smallest as is)
@@ -671,31 +671,6 @@ struct KthVisitor {
     for (; j < b; ++j, ++q) test(dist2(qx, qy, qz, *q), q->w, j);
   }
 };
-
-// Batcher's odd-even merge sort of N (power of two) register-resident (key, pos) pairs, every
-// index a compile-time constant
-template <int N>
-__device__ __forceinline__ void oem_sort(unsigned long long (&k)[N], uint32_t (&v)[N]) {
-#pragma unroll
-  for (int p = 1; p < N; p <<= 1)
-#pragma unroll
-    for (int q = p; q >= 1; q >>= 1)
-#pragma unroll
-      for (int j = q % p; j <= N - 1 - q; j += 2 * q)
-#pragma unroll
-        for (int i = 0; i < q; ++i) {
-          if (i > N - j - q - 1) continue;
-          if ((i + j) / (2 * p) != (i + j + q) / (2 * p)) continue;
-          const int a = i + j, b = i + j + q;
-          const bool sw = k[b] < k[a];
-          const unsigned long long ka = k[a], kb = k[b];
-          const uint32_t va = v[a], vb = v[b];
-          k[a] = sw ? kb : ka;
-          k[b] = sw ? ka : kb;
-          v[a] = sw ? vb : va;
-          v[b] = sw ? va : vb;
-        }
-}
 
 // PCL's covariance of the k = K - nsent neighbours at sorted positions pos[nsent..K) (in (d2,
 // index) order), regularised and stored at p (shared by both k-NN kernels)
@@ -719,26 +694,10 @@ __global__ __launch_bounds__(256, MGICP_COV_WAVES) void knn_cov_kernel(GridView 
   cov_from_sorted<K>(g, eps, vis.pos, nsent, cov, p);
 }
 
-template <int K>
-__device__ __forceinline__ void cov_from_sorted(const GridView& g, double eps, const uint32_t (&pos)[K],
-                                                int nsent, Cov3 cov, size_t p) {
-  double m0 = 0.0, m1 = 0.0, m2 = 0.0;
-  double a[3][3] = {{0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}};
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    if (k < nsent) continue;
-    const float4 pt = g.pts[pos[k]];
-    m0 += pt.x;
-    m1 += pt.y;
-    m2 += pt.z;
-    a[0][0] += static_cast<double>(pt.x * pt.x);
-    a[1][0] += static_cast<double>(pt.y * pt.x);
-    a[1][1] += static_cast<double>(pt.y * pt.y);
-    a[2][0] += static_cast<double>(pt.z * pt.x);
-    a[2][1] += static_cast<double>(pt.z * pt.y);
-    a[2][2] += static_cast<double>(pt.z * pt.z);
-  }
-  const double kd = static_cast<double>(K - nsent);
+// PCL's covariance from the raw moments of the k neighbours (sums in the oracle's order or proven
+// order-independent), regularised and stored at p
+__device__ __forceinline__ void cov_finish(double m0, double m1, double m2, double (&a)[3][3], double kd,
+                                           double eps, Cov3 cov, size_t p) {
   double mean[3] = {m0 / kd, m1 / kd, m2 / kd};
 #pragma unroll
   for (int i = 0; i < 3; ++i)
@@ -781,72 +740,111 @@ __device__ __forceinline__ void cov_from_sorted(const GridView& g, double eps, c
   cov.c[p] = make_double2(C12, C22);
 }
 
-// Logged-threshold k-NN covariance (default): ONE near-first ring search finds the exact k-th float
-// d2 (tau) with KthVisitor's min/max network while logging every candidate that was within the
-// threshold of its time into the lane's LDS log; the log entries with d2 <= tau are exactly the k
-// nearest plus any ties at tau, sorted by (d2, original index) with a static odd-even merge network
-// -- the first k are KnnVisitor's list.  A lane whose log overflows (or whose ties at tau exceed
-// the sort width) is listed in fb for KnnVisitor (knn_cov_kernel over that list).  64-thread blocks,
-// LOG x 4 bytes of LDS per lane (12 KB per wave: ~3 waves per SIMD).
 template <int K>
-constexpr int knn2_sort() { return K <= 8 ? 16 : 32; }
-constexpr int kKnnLog = 48;
-
-__device__ __forceinline__ unsigned long long knn_key(const GridView& g, float qx, float qy, float qz,
-                                                      uint32_t j) {
-  const float4 pt = g.pts[j];
-  return mkkey(dist2(qx, qy, qz, pt), pt.w);
+__device__ __forceinline__ void cov_from_sorted(const GridView& g, double eps, const uint32_t (&pos)[K],
+                                                int nsent, Cov3 cov, size_t p) {
+  double m0 = 0.0, m1 = 0.0, m2 = 0.0;
+  double a[3][3] = {{0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}};
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    if (k < nsent) continue;
+    const float4 pt = g.pts[pos[k]];
+    m0 += pt.x;
+    m1 += pt.y;
+    m2 += pt.z;
+    a[0][0] += static_cast<double>(pt.x * pt.x);
+    a[1][0] += static_cast<double>(pt.y * pt.x);
+    a[1][1] += static_cast<double>(pt.y * pt.y);
+    a[2][0] += static_cast<double>(pt.z * pt.x);
+    a[2][1] += static_cast<double>(pt.z * pt.y);
+    a[2][2] += static_cast<double>(pt.z * pt.z);
+  }
+  cov_finish(m0, m1, m2, a, static_cast<double>(K - nsent), eps, cov, p);
 }
+
+// Order-independence certificate for a double sum of n <= 32 floats: if every nonzero term is a
+// normal float with |f| in [2^Emin, 2^(Emax+1)) and Emax - Emin <= 24, every term is a multiple of
+// 2^(Emin-23) and every partial sum, in ANY order, is bounded by 32 * 2^(Emax+1) <= 2^(Emin-23+53):
+// all partial sums are exact doubles, so the result equals the oracle's sorted-order sum bit for
+// bit.  All-zero sums are trivially exact; a sum mixing zeros (or denormals) with nonzero terms is
+// not certified (the lane goes to the sorted kernel).
+struct SumCert {
+  float lo = INFINITY, hi = 0.f;
+  __device__ __forceinline__ void add(float f) {
+    lo = fminf(lo, fabsf(f));
+    hi = fmaxf(hi, fabsf(f));
+  }
+  __device__ __forceinline__ bool ok() const {
+    if (hi == 0.f) return true;
+    const int elo = static_cast<int>(__float_as_uint(lo) >> 23), ehi = static_cast<int>(__float_as_uint(hi) >> 23);
+    return elo > 0 && ehi - elo <= 24;
+  }
+};
+
+// Logged-threshold k-NN covariance (default): ONE near-first ring search finds the exact k-th float
+// d2 (tau) with KthVisitor's med3 network while logging every candidate that was within the
+// threshold of its time into the lane's LDS log (compacted to the entries within the current
+// threshold whenever it fills); at the end the log entries with d2 <= tau are the k-NN set.  With
+// exactly k of them (no ties at tau) and the nine moment sums certified order-independent
+// (SumCert), the moments are summed in log order -- bit-identical to the oracle's (d2, index)
+// order without sorting.  Any other lane (log overflow, ties at tau, uncertified sums) is listed in
+// fb for the register-list kernel.  64-thread blocks, cap x 4 bytes of dynamic LDS per lane.
 
 template <int K>
 __global__ __launch_bounds__(64) void knn_cov2_kernel(GridView g, double eps, size_t p0, size_t p1, Cov3 cov,
-                                                      const uint32_t* __restrict__ perm, int nsent,
+                                                      const uint32_t* __restrict__ perm, int nsent, int cap,
                                                       uint32_t* __restrict__ fb, unsigned int* __restrict__ fb_count) {
-  constexpr int S = knn2_sort<K>();
-  __shared__ uint32_t s_pos[kKnnLog * 64];
+  extern __shared__ uint32_t s_pos[];
   const size_t t = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (t >= p1 - p0) return;
   const size_t p = p0 + (perm ? perm[t] : t);
   const float4 q = g.pts[p];
-  KthVisitor<K, kKnnLog> v1;
+  KthVisitor<K> v1;
   v1.init(q.x, q.y, q.z, nsent);
   v1.lpos = s_pos + threadIdx.x;
   v1.pts = g.pts;
+  v1.cap = cap;
   ring_search(g, q.x, q.y, q.z, v1);
-  if (v1.cnt > kKnnLog) {
-    // log overflow even after compaction (ties): KnnVisitor finishes this point in a follow-up
-    // launch over the list
-    fb[atomicAdd(fb_count, 1u)] = static_cast<uint32_t>(p);
-    return;
-  }
-  const float tau = v1.key[K - 1];
-  // the log entries within tau, compacted in place (log order kept)
-  int m = 0;
-  for (int i = 0; i < v1.cnt; ++i) {
-    const uint32_t j = s_pos[i * 64 + threadIdx.x];
-    if (dist2(q.x, q.y, q.z, g.pts[j]) <= tau) {
-      s_pos[m * 64 + threadIdx.x] = j;
+  const int kreal = K - nsent;
+  bool ok = v1.cnt <= cap;
+  if (ok) {
+    const float tau = v1.key[K - 1];
+    double m0 = 0.0, m1 = 0.0, m2 = 0.0;
+    double a[3][3] = {{0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}};
+    SumCert c0, c1, c2, c00, c10, c11, c20, c21, c22;
+    int m = 0;
+    for (int i = 0; i < v1.cnt; ++i) {
+      const float4 pt = g.pts[s_pos[i * 64 + threadIdx.x]];
+      if (dist2(q.x, q.y, q.z, pt) > tau) continue;
       ++m;
+      const float xx = pt.x * pt.x, yx = pt.y * pt.x, yy = pt.y * pt.y;
+      const float zx = pt.z * pt.x, zy = pt.z * pt.y, zz = pt.z * pt.z;
+      m0 += pt.x;
+      m1 += pt.y;
+      m2 += pt.z;
+      a[0][0] += static_cast<double>(xx);
+      a[1][0] += static_cast<double>(yx);
+      a[1][1] += static_cast<double>(yy);
+      a[2][0] += static_cast<double>(zx);
+      a[2][1] += static_cast<double>(zy);
+      a[2][2] += static_cast<double>(zz);
+      c0.add(pt.x);
+      c1.add(pt.y);
+      c2.add(pt.z);
+      c00.add(xx);
+      c10.add(yx);
+      c11.add(yy);
+      c20.add(zx);
+      c21.add(zy);
+      c22.add(zz);
     }
+    ok = m == kreal && c0.ok() && c1.ok() && c2.ok() && c00.ok() && c10.ok() && c11.ok() && c20.ok() &&
+         c21.ok() && c22.ok();
+    if (ok) cov_finish(m0, m1, m2, a, static_cast<double>(kreal), eps, cov, p);
   }
-  if (m > S) {  // more ties at tau than the sort width (lattices): KnnVisitor, as above
-    fb[atomicAdd(fb_count, 1u)] = static_cast<uint32_t>(p);
-    return;
-  }
-  unsigned long long kk[S];
-  uint32_t vv[S];
-#pragma unroll
-  for (int i = 0; i < S; ++i) {
-    const bool in = i < m;
-    vv[i] = in ? s_pos[i * 64 + threadIdx.x] : 0u;
-    kk[i] = in ? knn_key(g, q.x, q.y, q.z, vv[i]) : ~0ull;
-  }
-  oem_sort<S>(kk, vv);
-  // neighbour j of k sits in slot nsent + j (the sentinel slots of KnnVisitor)
-  uint32_t pos[K];
-#pragma unroll
-  for (int i = 0; i < K; ++i) pos[i] = i < nsent ? 0u : vv[i - nsent < 0 ? 0 : i - nsent];
-  cov_from_sorted<K>(g, eps, pos, nsent, cov, p);
+  // log overflow, ties at tau or an uncertified sum: KnnVisitor's sorted (d2, index) list finishes
+  // this point in a follow-up launch over the list (knn_cov_kernel with perm = fb)
+  if (!ok) fb[atomicAdd(fb_count, 1u)] = static_cast<uint32_t>(p);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1646,21 +1644,28 @@ hipError_t launch_iota(uint32_t* v, size_t n, hipStream_t s) {
   return hipGetLastError();
 }
 
+// log capacity (entries per lane) of the logged k-NN kernel: env MGICP_KNN_LOG, default K + 28
+static int knn_log_cap(int K) {
+  int cap = K + 28;
+  if (const char* e = std::getenv("MGICP_KNN_LOG")) cap = std::atoi(e);
+  return std::min(std::max(cap, K + 1), 128);
+}
+
 static bool knn_two_phase() {  // env MGICP_KNN2 (default 1): knn_cov2_kernel, else knn_cov_kernel
-  static const bool on = [] {
-    const char* e = std::getenv("MGICP_KNN2");
-    return !(e && std::atoi(e) == 0);
-  }();
-  return on;
+  const char* e = std::getenv("MGICP_KNN2");
+  return !(e && std::atoi(e) == 0);
 }
 
 template <int K>
 static hipError_t knn_cov_k(const GridView& g, double eps, size_t p0, size_t p1, Cov3 cov,
                             const uint32_t* perm, int k, uint32_t* fb, unsigned int* fb_count, hipStream_t s) {
-  if (fb && knn_two_phase())
-    knn_cov2_kernel<K><<<nblk(p1 - p0, 64), 64, 0, s>>>(g, eps, p0, p1, cov, perm, K - k, fb, fb_count);
-  else
+  if (fb) {
+    const int cap = knn_log_cap(K);
+    knn_cov2_kernel<K><<<nblk(p1 - p0, 64), 64, cap * 64 * sizeof(uint32_t), s>>>(g, eps, p0, p1, cov, perm,
+                                                                                 K - k, cap, fb, fb_count);
+  } else {
     knn_cov_kernel<K><<<nblk(p1 - p0), 256, 0, s>>>(g, eps, p0, p1, cov, perm, K - k);
+  }
   return hipGetLastError();
 }
 

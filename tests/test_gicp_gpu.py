@@ -313,6 +313,46 @@ def test_seeded_correspondences_lattice_ties(engine_mod):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("k", [20, 7, 32])
+def test_logged_knn_matches_register_list(engine_mod, part_small, monkeypatch, capfd, k):
+    """The logged k-NN kernel (MGICP_KNN2=1, default) sums the moments in log order when exactly k
+    entries fall within tau and the nine sums are certified order-independent; every other point
+    goes to the register-list kernel.  Both paths must give the register-list kernel's covariances
+    bit for bit -- on clouds built to hit the hand-off: a part centred on the origin (neighbours
+    with coordinates near 0: uncertified sums), a lattice (ties at tau), a plane z = 0 (all-zero
+    sums), duplicated points."""
+    src = part_small[0][:20000]
+    g = np.arange(0.0, 1.0, 0.05, dtype=np.float32)
+    X, Y, Z = np.meshgrid(g, g, g[:6], indexing="ij")
+    lattice = np.stack([X.ravel(), Y.ravel(), Z.ravel()], 1).astype(np.float32)
+    plane = src.copy()
+    plane[:, 2] = 0.0
+    centred = (src - src.mean(0)).astype(np.float32)
+    centred[::50, 0] = 0.0  # exact zeros among nonzero terms: those sums are not certified
+    clouds = {"part": src, "centred": centred, "lattice": lattice,
+              "plane": plane, "dup": np.concatenate([src[:3000], src[:3000]])}
+    handed = {}
+    for name, pts in clouds.items():
+        res = {}
+        for knn2 in ("0", "1"):
+            monkeypatch.setenv("MGICP_KNN2", knn2)
+            monkeypatch.setenv("MGICP_KNN_STATS", "1")
+            e = engine_mod(k=k)
+            e.set_source_xyz(pts)
+            e.set_target_xyz(pts[: len(pts) // 2])
+            res[knn2] = e.debug_covariances("source", len(pts))
+            del e
+        np.testing.assert_array_equal(res["1"], res["0"], err_msg=name)
+        err = capfd.readouterr().err
+        left = [int(l.split()[3]) for l in err.splitlines() if l.startswith("[knn]") and f"] {len(pts)} points" in l]
+        handed[name] = left[-1] if left else None
+    # the hand-off really ran where the clouds were built for it, and stayed rare on the part
+    assert handed["lattice"] and handed["lattice"] > 0, handed
+    assert handed["centred"] and handed["centred"] > 0, handed
+    assert handed["part"] is not None and handed["part"] < 0.05 * len(src), handed
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("k", [1, 2, 7, 12, 20, 32])
 def test_covariances_any_k(engine_mod, part_small, k):
     """PCL's setCorrespondenceRandomness accepts any k: exact instantiations (5..30 step 5) and the
