@@ -214,11 +214,12 @@ struct Cloud {
   bool drop_nonfinite = false; // build the grid over the finite points only (KdTreeFLANN semantics)
   double occupancy = 0;        // grid sizing target (points per non-empty cell); 0 = context default
   size_t n_built = 0;          // points of the last grid built in this slot (cell-size hint)
-  DevBuf<double2> cov;        // 3 * n
+  DevBuf<double2> cov;        // 3 * cov_stride
+  size_t cov_stride = 0;      // entries per covariance array (n, or the padded all-gather size)
   float lo[3] = {0.f, 0.f, 0.f}, hi[3] = {0.f, 0.f, 0.f};  // bounding box (original coordinates)
   GridView view{};
   size_t ncells = 0;
-  Cov3 cov3() const { return Cov3{cov.p, cov.p + n, cov.p + 2 * n}; }
+  Cov3 cov3() const { return Cov3{cov.p, cov.p + cov_stride, cov.p + 2 * cov_stride}; }
 };
 
 enum { kFamCov = 0, kFamCorr = 1, kFamFdf = 2, kFamRed = 3, kFamCompact = 4, kFamMoments = 5, kFams = 6 };
@@ -239,14 +240,15 @@ struct mgicp_ctx {
   DevBuf<unsigned char> f_keep;
   DevBuf<unsigned int> f_count;
   double occupancy = kDefaultOccupancy;  // grid cell sizing target (env MGICP_GRID_OCC)
-  // objective-pass launch shape, A/B-measured on MI355X at 5M points (profiles/r01/ab3_*.json):
-  // fence-free in-launch finish at 256 blocks (one per CU) beats 128..2048 blocks and a
-  // separate finish kernel
+  // objective-pass launch shape over the fixed reduction tree, A/B-measured on MI355X at 5M points
+  // (profiles/r02/ab_tree): 1024 persistent 4-wave blocks (4 waves per SIMD: chunk reductions and
+  // tickets overlap other waves' streaming) 68 us vs 75 us at 256 blocks; in-launch finish
   bool fused_finish = true;              // in-launch reduction finish (env MGICP_FUSED_FINISH)
-  int fdf_max_blocks = 256;              // objective-pass grid cap (env MGICP_FDF_BLOCKS)
+  int fdf_max_blocks = 1024;             // objective-pass grid cap (env MGICP_FDF_BLOCKS)
   // alternate the objective-pass direction: 360 MB of streams at 5M points exceed the 256 MiB
   // Infinity Cache, so each pass re-reads the previous pass's tail from it (73 -> 68 us)
   bool alt_sweep = true;                 // (env MGICP_FDF_ALT)
+  int fdf_diag = 0;  // timing diagnostics of the objective pass (env MGICP_FDF_DIAG: 2 no reduction, 4 no tickets)
   double ms_upload_pending = 0;
   // host uploads go through the process-wide HostUploader (host_upload.hpp)
   int host_threads = 8;                  // packing workers (env MGICP_HOST_THREADS)
@@ -267,10 +269,17 @@ struct mgicp_ctx {
   bool query_order = true;
   bool qperm_valid = false;
   DevBuf<uint32_t> qperm;
-  DevBuf<double> partial;
-  DevBuf<double> red;      // kRedVals
-  // Gauss-Newton mode: block partials / finished moments of one pass, and their host copy
-  DevBuf<double> mpartial, mred;
+  // the fixed reduction tree (internal.hpp kChunkPts / kSuperChunks): chunk layout of the streams,
+  // chunk and super partials of this shard, the all-gathered supers of every rank, the total
+  DevBuf<uint32_t> chunk_base;  // chunk_count(ns) + 1
+  DevBuf<double> partial;       // chunk partials, kRedVals each
+  DevBuf<double> spart;         // super partials (max_supers() rows: the all-gather send size)
+  DevBuf<double> gath;          // nranks x max_supers() rows
+  DevBuf<double> red;           // kRedVals
+  DevBuf<unsigned int> tickets; // per super + 1: arrival counters of the in-launch finish
+  size_t tickets_n = 0;
+  // Gauss-Newton mode: chunk / super partials and the totals of one pass, and their host copy
+  DevBuf<double> mpartial, msuper, mred;
   double mom[kMomVals] = {};
   double out_ctr[3] = {0, 0, 0};  // moment expansion centre: bbox midpoint of the guess-applied source
   unsigned char* h_small = nullptr;  // pinned, mapped host scratch (kSmallBytes) for small readbacks
@@ -298,11 +307,11 @@ struct mgicp_ctx {
   std::vector<double> host_gt;             // 2 x 1024
   unsigned long long gated_seq = 0;     // sequence number of the queued gated pass (0 = none)
   unsigned long long gate_timeout = 0;  // wall_clock64 ticks a gated pass waits before giving up
-  DevBuf<unsigned int> ticket;  // arrival counter of the in-launch reduction finish
   // build scratch
   DevBuf<uint32_t> counts, keys, keys_sorted, vals;
   DevBuf<unsigned char> scratch;
   DevBuf<unsigned long long> u64;
+  bool split_target_cov = true;     // multi-GPU: target covariances split + all-gathered (env MGICP_SPLIT_TARGET_COV)
   bool knn_logged = true;           // env MGICP_KNN2 at create: logged k-NN kernel, else register-list
   DevBuf<uint32_t> knn_fb;          // points the logged k-NN kernel leaves to the register-list one
   unsigned int knn_fallbacks = 0;   // their count in the last covariance launch
@@ -325,8 +334,17 @@ struct mgicp_ctx {
   double fam_ms[kFams] = {};
   int fam_cnt[kFams] = {};
 
-  size_t shard_p0() const { return src.n * static_cast<size_t>(rank) / nranks; }
-  size_t shard_p1() const { return src.n * static_cast<size_t>(rank + 1) / nranks; }
+  // shards start on super boundaries: rank r owns supers [super_first(r), super_first(r + 1))
+  long long nsup_total() const { return static_cast<long long>((src.n + kSuperPts - 1) / kSuperPts); }
+  size_t shard_at(int r) const {
+    return std::min(src.n, static_cast<size_t>(super_first(r, nsup_total(), nranks)) * kSuperPts);
+  }
+  size_t shard_p0() const { return shard_at(rank); }
+  size_t shard_p1() const { return shard_at(rank + 1); }
+  long long nsup_local() const {
+    return super_first(rank + 1, nsup_total(), nranks) - super_first(rank, nsup_total(), nranks);
+  }
+  long long max_supers() const { return (nsup_total() + nranks - 1) / nranks; }
 };
 
 namespace {
@@ -685,9 +703,12 @@ const uint32_t* query_perm(mgicp_ctx* ctx) {
   return ctx->qperm.p;
 }
 
-int compute_cov(mgicp_ctx* ctx, Cloud& cl, size_t p0, size_t p1) {
+// covariances of sorted positions [p0, p1) into arrays of `stride` entries (default n)
+int compute_cov(mgicp_ctx* ctx, Cloud& cl, size_t p0, size_t p1, size_t stride = 0) {
   MGICP_TRACE_AT("cov: begin");
-  HIPCK(cl.cov.reserve(3 * cl.n));
+  if (stride < cl.n) stride = cl.n;
+  HIPCK(cl.cov.reserve(3 * stride));
+  cl.cov_stride = stride;
   MGICP_TRACE_AT("cov: reserved");
   // grid order, not Morton order: the k = 20 queries sit on the surface and the row-major order
   // measured faster (3.97 vs 4.42 ms at 5M, profiles/r01/ab_qorder/)
@@ -729,6 +750,29 @@ int compute_cov(mgicp_ctx* ctx, Cloud& cl, size_t p0, size_t p1) {
   return MGICP_OK;
 }
 
+// target covariances (computeCovariances on the target, once per target cloud).  Multi-GPU
+// (SURVEY.md 8e): rank r computes the r-th of N equal slices and one in-place all-gather per
+// covariance array (48 bytes per point in total) completes every rank's copy -- the values are
+// per point, so the result is the single-GPU one bit for bit (env MGICP_SPLIT_TARGET_COV=0: every
+// rank computes all of them).
+int target_cov(mgicp_ctx* ctx) {
+  Cloud& t = ctx->tgt;
+  if (!ctx->comm || ctx->nranks < 2 || !ctx->split_target_cov) return compute_cov(ctx, t, 0, t.n);
+  const size_t N = static_cast<size_t>(ctx->nranks), r = static_cast<size_t>(ctx->rank);
+  const size_t cnt = (t.n + N - 1) / N;
+  int rc = compute_cov(ctx, t, std::min(t.n, r * cnt), std::min(t.n, (r + 1) * cnt), N * cnt);
+  if (rc) return rc;
+  const Cov3 c = t.cov3();
+  NCCLCK(ncclGroupStart());
+  for (double2* a : {c.a, c.b, c.c})
+    NCCLCK(ncclAllGather(a + r * cnt, a, 2 * cnt, ncclDouble, ctx->comm, ctx->stream));
+  NCCLCK(ncclGroupEnd());
+  if ((rc = sync(ctx))) return rc;
+  t.cov_p0 = 0;
+  t.cov_p1 = t.n;
+  return MGICP_OK;
+}
+
 // Registration::initCompute + initComputeReciprocal + computeCovariances (both clouds)
 int prepare(mgicp_ctx* ctx, bool need_cov) {
   if (ctx->src.n == 0 || ctx->tgt.n == 0)
@@ -741,7 +785,7 @@ int prepare(mgicp_ctx* ctx, bool need_cov) {
   if (ctx->tgt.dirty && (rc = build_grid(ctx, ctx->tgt))) return rc;
   if (ctx->src.dirty && (rc = build_grid(ctx, ctx->src))) return rc;
   if (!need_cov) return MGICP_OK;
-  if (!ctx->tgt.have_cov && (rc = compute_cov(ctx, ctx->tgt, 0, ctx->tgt.n))) return rc;
+  if (!ctx->tgt.have_cov && (rc = target_cov(ctx))) return rc;
   if (!ctx->src.have_cov || ctx->src.cov_p0 != ctx->shard_p0() || ctx->src.cov_p1 != ctx->shard_p1())
     if ((rc = compute_cov(ctx, ctx->src, ctx->shard_p0(), ctx->shard_p1()))) return rc;
   return MGICP_OK;
@@ -803,14 +847,22 @@ int wait_pass(mgicp_ctx* ctx, unsigned long long seq) {
 }
 
 int ensure_iter_buffers(mgicp_ctx* ctx) {
-  const size_t n = ctx->src.n;
-  const int nb = std::max(fdf_grid_blocks(n), static_cast<int>((n + 255) / 256));
-  HIPCK(ctx->partial.reserve(static_cast<size_t>(nb) * kRedVals));
+  const size_t ns = ctx->shard_p1() - ctx->shard_p0();
+  const size_t nch = static_cast<size_t>(chunk_count(ns));
+  const size_t msup = static_cast<size_t>(ctx->max_supers());
+  HIPCK(ctx->partial.reserve(std::max<size_t>(nch, 1) * kRedVals));
+  HIPCK(ctx->spart.reserve(std::max<size_t>(msup, 1) * kRedVals));
+  HIPCK(ctx->chunk_base.reserve(nch + 1));
   HIPCK(ctx->red.reserve(kRedVals));
+  if (ctx->tickets_n < msup + 1) {  // zero between passes: every finishing wave re-arms its own
+    HIPCK(ctx->tickets.reserve(msup + 1));
+    HIPCK(hipMemsetAsync(ctx->tickets.p, 0, (msup + 1) * sizeof(unsigned int), ctx->stream));
+    ctx->tickets_n = msup + 1;
+  }
   int rc = ensure_host_red(ctx);
   if (rc) return rc;
-  const size_t ns = ctx->shard_p1() - ctx->shard_p0();
-  const size_t cap = (ns + 3) / 4 * 4 + 4;
+  // every chunk's run is padded to a multiple of 4 slots
+  const size_t cap = (ns + 3 * nch + 3) / 4 * 4 + 4;
   HIPCK(ctx->prev_pos.reserve(ns + 1));
   HIPCK(ctx->flags.reserve(ns + 1));
   HIPCK(ctx->cpos.reserve(ns + 1));
@@ -820,9 +872,21 @@ int ensure_iter_buffers(mgicp_ctx* ctx) {
     ctx->corr_cap = cap;
   }
   HIPCK(ctx->cscratch.reserve(scan_scratch_bytes(ns + 1)));
-  if (!ctx->ticket.p) {
-    HIPCK(ctx->ticket.reserve(1));
-    HIPCK(hipMemsetAsync(ctx->ticket.p, 0, sizeof(unsigned int), ctx->stream));
+  return MGICP_OK;
+}
+
+// totals (nv values) of the shard's super partials `sup`: all-gathered across ranks over RCCL and
+// finished in the fixed global order (launch_finish_supers), or -- single rank or detached shard
+// -- finished over this shard's own supers
+int combine_supers(mgicp_ctx* ctx, int nv, const double* sup, double* out) {
+  if (ctx->comm) {
+    const long long msup = ctx->max_supers();
+    HIPCK(ctx->gath.reserve(static_cast<size_t>(ctx->nranks) * msup * nv));
+    NCCLCK(ncclAllGather(sup, ctx->gath.p, static_cast<size_t>(msup) * nv, ncclDouble, ctx->comm, ctx->stream));
+    HIPCK(launch_finish_supers(ctx->gath.p, ctx->nsup_total(), msup, ctx->nranks, nv, out, ctx->stream));
+  } else {
+    const long long ns = ctx->nsup_local();
+    HIPCK(launch_finish_supers(sup, ns, ns, 1, nv, out, ctx->stream));
   }
   return MGICP_OK;
 }
@@ -914,8 +978,9 @@ int correspond(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
   HIPCK(launch_exclusive_scan(ctx->cscratch.p, sb, ctx->flags.p, ctx->cpos.p, ns + 1, s));
   {
     ProfScope ps(ctx, kFamCompact);
+    HIPCK(launch_chunk_base(ctx->cpos.p, ns, ctx->chunk_base.p, corr_soa(ctx), s));
     HIPCK(launch_compact(ctx->d_out, ctx->tgt.view.pts, ctx->src.cov3(), ctx->tgt.cov3(),
-                         rot_of(T, G), ctx->prev_pos.p, ctx->flags.p, ctx->cpos.p, p0, p1,
+                         rot_of(T, G), ctx->prev_pos.p, ctx->flags.p, ctx->cpos.p, ctx->chunk_base.p, p0, p1,
                          corr_soa(ctx), s));
   }
   HIPCK(hipMemcpyAsync(ctx->h_small, ctx->cpos.p + ns, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
@@ -926,20 +991,6 @@ int correspond(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
   ctx->m_local = m;
   ctx->have_corr = true;
   return MGICP_OK;
-}
-
-// finish the block partials (fixed order), all-reduce across ranks, copy to host
-int reduce_to_host(mgicp_ctx* ctx, int nb) {
-  {
-    ProfScope ps(ctx, kFamRed);
-    HIPCK(launch_reduce_finish(ctx->partial.p, nb, ctx->red.p, ctx->stream));
-  }
-  if (ctx->comm)
-    NCCLCK(ncclAllReduce(ctx->red.p, ctx->red.p, kRedVals, ncclDouble, ncclSum, ctx->comm,
-                         ctx->stream));
-  HIPCK(hipMemcpyAsync(ctx->h_red, ctx->red.p, kRedVals * sizeof(double), hipMemcpyDeviceToHost,
-                       ctx->stream));
-  return sync(ctx);
 }
 
 // OptimizationFunctorWithIndices::fdf on the device; memoises the last state
@@ -953,60 +1004,56 @@ struct DeviceFunctor {
 
   int pass(const Vec6& x, double sums[kRedVals]) {
     const Mat4 A = apply_state(x);
-    const int nb = fdf_grid_blocks(ctx->m_local, ctx->fdf_max_blocks);
+    const size_t ns = ctx->shard_p1() - ctx->shard_p0();
+    const int nb = fdf_grid_blocks(ns, ctx->fdf_max_blocks);
     int rc;
     // alternate the sweep direction so each pass starts on the Infinity-Cache-resident tail
-    // of the previous one (deterministic: the direction follows the pass index)
-    const int reverse = ctx->alt_sweep ? (ctx->n_evals & 1) : 0;
-    if (ctx->fused_finish) {
-      // the last block writes the sums straight into mapped pinned host memory (single GPU)
-      // or device memory (multi-GPU: then one 16-double RCCL all-reduce, and a one-wave kernel
-      // publishes the reduced sums plus the completion word into mapped host memory)
-      double* out = ctx->comm ? ctx->red.p : ctx->d_h_red;
-      const bool poll = ctx->poll;
-      const unsigned long long seq = ++ctx->pass_seq;
-      const bool gate = ctx->gated && poll && !ctx->comm && !ctx->profiling;
-      const Xf34 Ax = A.xf();
-      if (ctx->gated_seq == seq) {
-        // pass `seq` is already resident, waiting: hand it its state
-        publish_cmd(ctx, seq, kPassRun, reverse, &Ax);
-        if (ctx->h_gtrace) ctx->host_gt[2 * (seq & 1023) + 1] = now_ms() * 1e3;
-        ctx->gated_seq = 0;
-      } else {
-        cancel_gated(ctx);
-        ProfScope ps(ctx, kFamFdf);
-        HIPCK(launch_fdf_soa(corr_soa(ctx), ctx->m_local, Ax, ctx->partial.p, nb,
-                             ctx->ticket.p, out, reverse,
-                             (poll && !ctx->comm) ? ctx->d_flag : nullptr, seq, ctx->stream));
-      }
-      if (gate) {
-        // queue pass seq + 1 now (its launch overlaps this pass); it runs once the BFGS step has
-        // published x_{k+1}, or exits on cancel when the BFGS run ends
-        HIPCK(launch_fdf_soa_gated(corr_soa(ctx), ctx->m_local, ctx->partial.p, nb, ctx->ticket.p, out,
-                                   ctx->d_flag, seq + 1, ctx->d_cmd, ctx->mail, ctx->gate_timeout,
-                                   ctx->d_gtrace, ctx->gate_pollers, ctx->stream));
-        ctx->gated_seq = seq + 1;
-      }
-      if (ctx->comm) {
-        NCCLCK(ncclAllReduce(ctx->red.p, ctx->red.p, kRedVals, ncclDouble, ncclSum, ctx->comm,
-                             ctx->stream));
-        if (poll) {
-          HIPCK(launch_publish(ctx->red.p, kRedVals, ctx->d_h_red, ctx->d_flag, seq, ctx->stream));
-        } else {
-          HIPCK(hipMemcpyAsync(ctx->h_red, ctx->red.p, kRedVals * sizeof(double),
-                               hipMemcpyDeviceToHost, ctx->stream));
-        }
-      }
-      rc = poll ? wait_pass(ctx, seq) : sync(ctx);
-      if (ctx->h_gtrace) ctx->host_gt[2 * ((seq + 1) & 1023)] = now_ms() * 1e3;  // sums of seq seen
+    // of the previous one (deterministic: the sums do not depend on the direction)
+    const int reverse = (ctx->alt_sweep ? (ctx->n_evals & 1) : 0) | ctx->fdf_diag;
+    const bool poll = ctx->poll && !ctx->fdf_diag;
+    const unsigned long long seq = ++ctx->pass_seq;
+    // single GPU: the finishing wave writes the totals straight into mapped pinned host memory.
+    // Otherwise the pass leaves its super partials, then combine_supers (RCCL all-gather + the
+    // fixed-order total) and a one-wave kernel publishes the totals plus the completion word.
+    const bool inlaunch = ctx->fused_finish && !ctx->comm && ctx->nranks == 1;
+    double* out = inlaunch ? ctx->d_h_red : nullptr;
+    const bool gate = ctx->gated && poll && inlaunch && !ctx->profiling;
+    const Xf34 Ax = A.xf();
+    const CorrSoA c = corr_soa(ctx);
+    if (ctx->gated_seq == seq) {
+      // pass `seq` is already resident, waiting: hand it its state
+      publish_cmd(ctx, seq, kPassRun, reverse, &Ax);
+      if (ctx->h_gtrace) ctx->host_gt[2 * (seq & 1023) + 1] = now_ms() * 1e3;
+      ctx->gated_seq = 0;
     } else {
-      {
-        ProfScope ps(ctx, kFamFdf);
-        HIPCK(launch_fdf_soa(corr_soa(ctx), ctx->m_local, A.xf(), ctx->partial.p, nb, nullptr,
-                             nullptr, reverse, nullptr, 0, ctx->stream));
-      }
-      rc = reduce_to_host(ctx, nb);
+      cancel_gated(ctx);
+      ProfScope ps(ctx, kFamFdf);
+      HIPCK(launch_fdf_soa(c, ctx->cpos.p, ctx->chunk_base.p, ns, Ax, ctx->partial.p, ctx->spart.p, nb,
+                           ctx->tickets.p, out, reverse, (poll && inlaunch) ? ctx->d_flag : nullptr, seq,
+                           ctx->stream));
     }
+    if (gate) {
+      // queue pass seq + 1 now (its launch overlaps this pass); it runs once the BFGS step has
+      // published x_{k+1}, or exits on cancel when the BFGS run ends
+      HIPCK(launch_fdf_soa_gated(c, ctx->cpos.p, ctx->chunk_base.p, ns, ctx->partial.p, ctx->spart.p, nb,
+                                 ctx->tickets.p, out, ctx->d_flag, seq + 1, ctx->d_cmd, ctx->mail,
+                                 ctx->gate_timeout, ctx->d_gtrace, ctx->gate_pollers, ctx->stream));
+      ctx->gated_seq = seq + 1;
+    }
+    if (!inlaunch) {
+      {
+        ProfScope ps(ctx, kFamRed);
+        if ((rc = combine_supers(ctx, kRedVals, ctx->spart.p, ctx->red.p))) return rc;
+      }
+      if (poll) {
+        HIPCK(launch_publish(ctx->red.p, kRedVals, ctx->d_h_red, ctx->d_flag, seq, ctx->stream));
+      } else {
+        HIPCK(hipMemcpyAsync(ctx->h_red, ctx->red.p, kRedVals * sizeof(double), hipMemcpyDeviceToHost,
+                             ctx->stream));
+      }
+    }
+    rc = poll ? wait_pass(ctx, seq) : sync(ctx);
+    if (ctx->h_gtrace) ctx->host_gt[2 * ((seq + 1) & 1023)] = now_ms() * 1e3;  // sums of seq seen
     if (rc) return rc;
     std::memcpy(sums, ctx->h_red, kRedVals * sizeof(double));
     ctx->n_evals++;
@@ -1099,22 +1146,27 @@ int estimate_bfgs(mgicp_ctx* ctx, Mat4& T, int* n_corr) {
 
 // Gauss-Newton mode, one device pass per outer iteration: the 74 moments of the objective over
 // the accepted correspondences of the last sweep at T (Mahalanobis computed on the fly), finished
-// in a fixed block order, all-reduced across ranks (one 80-double RCCL call), copied to the host.
-int moments_pass(mgicp_ctx* ctx, const Mat4& T, const Mat4& G) {
+// over the fixed reduction tree (chunks, supers, all-gathered supers, fixed-order total), copied to
+// the host.
+int moments_pass(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool supers_only = false) {
   const size_t p0 = ctx->shard_p0(), p1 = ctx->shard_p1();
   hipStream_t s = ctx->stream;
-  const int nb = gn_grid_blocks(p1 - p0);
-  HIPCK(ctx->mpartial.reserve(static_cast<size_t>(nb) * kMomVals));
+  const int nch = chunk_count(p1 - p0);
+  HIPCK(ctx->mpartial.reserve(std::max(nch, 1) * static_cast<size_t>(kMomVals)));
+  HIPCK(ctx->msuper.reserve(std::max<long long>(ctx->max_supers(), 1) * static_cast<size_t>(kMomVals)));
   HIPCK(ctx->mred.reserve(kMomVals));
   {
     ProfScope ps(ctx, kFamMoments);
-    HIPCK(launch_gn_moments(ctx->d_out, ctx->tgt.view.pts, ctx->src.cov3(), ctx->tgt.cov3(),
-                            rot_of(T, G), T.xf(), ctx->out_ctr, ctx->prev_pos.p, ctx->flags.p, p0,
-                            p1, ctx->mpartial.p, nb, s));
-    HIPCK(launch_reduce_finish_moments(ctx->mpartial.p, nb, ctx->mred.p, s));
+    if (nch > 0) {
+      HIPCK(launch_gn_moments(ctx->d_out, ctx->tgt.view.pts, ctx->src.cov3(), ctx->tgt.cov3(),
+                              rot_of(T, G), T.xf(), ctx->out_ctr, ctx->prev_pos.p, ctx->flags.p, p0,
+                              p1, ctx->mpartial.p, chunk_grid_blocks(p1 - p0), s));
+      HIPCK(launch_super_reduce(ctx->mpartial.p, nch, kMomVals, ctx->msuper.p, s));
+    }
   }
-  if (ctx->comm)
-    NCCLCK(ncclAllReduce(ctx->mred.p, ctx->mred.p, kMomVals, ncclDouble, ncclSum, ctx->comm, s));
+  if (supers_only) return sync(ctx);
+  int rc0 = combine_supers(ctx, kMomVals, ctx->msuper.p, ctx->mred.p);
+  if (rc0) return rc0;
   HIPCK(hipMemcpyAsync(ctx->h_small, ctx->mred.p, kMomVals * sizeof(double), hipMemcpyDeviceToHost, s));
   int rc = sync(ctx);
   if (rc) return rc;
@@ -1209,9 +1261,11 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
   }
   if (const char* ff = std::getenv("MGICP_FUSED_FINISH")) ctx->fused_finish = std::atoi(ff) != 0;
   if (const char* fa = std::getenv("MGICP_FDF_ALT")) ctx->alt_sweep = std::atoi(fa) != 0;
+  if (const char* fd = std::getenv("MGICP_FDF_DIAG")) ctx->fdf_diag = std::atoi(fd) & 6;
   if (const char* po = std::getenv("MGICP_POLL")) ctx->poll = std::atoi(po) != 0;
   if (const char* ga = std::getenv("MGICP_GATED")) ctx->gated = std::atoi(ga) != 0;
   ctx->knn_logged = knn_logged_enabled();
+  if (const char* st = std::getenv("MGICP_SPLIT_TARGET_COV")) ctx->split_target_cov = std::atoi(st) != 0;
   if (const char* ps = std::getenv("MGICP_PROF_STRIDE")) ctx->prof_stride = std::max(1, std::atoi(ps));
   if (const char* qo = std::getenv("MGICP_QUERY_ORDER")) ctx->query_order = std::atoi(qo) != 0;
   if (const char* so = std::getenv("MGICP_SRC_GRID_OCC")) {
@@ -1312,7 +1366,9 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   ctx->keys_sorted.release(); ctx->vals.release(); ctx->scratch.release(); ctx->u64.release();
   ctx->fpartial.release();
   ctx->knn_fb.release();
-  ctx->ticket.release();
+  ctx->tickets.release();
+  ctx->tickets_n = 0;
+  ctx->chunk_base.release(); ctx->spart.release(); ctx->gath.release(); ctx->msuper.release();
   ctx->prev_pos.release(); ctx->flags.release(); ctx->cpos.release();
   ctx->corr_f.release(); ctx->corr_d.release(); ctx->cscratch.release();
   ctx->xyz_dev.release();
@@ -1454,6 +1510,17 @@ int mgicp_align(mgicp_ctx* ctx, const float guess_cm[16], float out_T_cm[16], mg
   return MGICP_OK;
 }
 
+// getFitnessScore's chunk and super partials of this shard ([0] sum d2, [13] count) in spart
+static int fitness_supers(mgicp_ctx* ctx, const Mat4& T, double max_range) {
+  const size_t p0 = ctx->shard_p0(), p1 = ctx->shard_p1();
+  const int nch = chunk_count(p1 - p0);
+  if (nch == 0) return MGICP_OK;
+  HIPCK(launch_fitness(ctx->tgt.view, ctx->src.pts.p, p0, p1, T.xf(), max_range, ctx->partial.p,
+                       chunk_grid_blocks(p1 - p0), ctx->stream));
+  HIPCK(launch_super_reduce(ctx->partial.p, nch, kRedVals, ctx->spart.p, ctx->stream));
+  return MGICP_OK;
+}
+
 int mgicp_fitness(mgicp_ctx* ctx, const float T_cm[16], double max_range, double* out) {
   if (!ctx || !T_cm || !out) return MGICP_E_INVALID;
   if (ctx->nranks > 1 && !ctx->comm)
@@ -1464,12 +1531,10 @@ int mgicp_fitness(mgicp_ctx* ctx, const float T_cm[16], double max_range, double
   if ((rc = ensure_iter_buffers(ctx))) return rc;
   if (!(max_range > 0)) max_range = 1.7976931348623157e308;
   const Mat4 T = Mat4::from_cm(T_cm);
-  const size_t p0 = ctx->shard_p0(), p1 = ctx->shard_p1();
-  const int nb = static_cast<int>(std::max<size_t>(1, (p1 - p0 + 255) / 256));
-  HIPCK(ctx->partial.reserve(static_cast<size_t>(nb) * kRedVals));
-  HIPCK(launch_fitness(ctx->tgt.view, ctx->src.pts.p, p0, p1, T.xf(), max_range, ctx->partial.p,
-                       nb, ctx->stream));
-  if ((rc = reduce_to_host(ctx, nb))) return rc;
+  if ((rc = fitness_supers(ctx, T, max_range))) return rc;
+  if ((rc = combine_supers(ctx, kRedVals, ctx->spart.p, ctx->red.p))) return rc;
+  HIPCK(hipMemcpyAsync(ctx->h_red, ctx->red.p, kRedVals * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+  if ((rc = sync(ctx))) return rc;
   const double nr = ctx->h_red[13];
   *out = nr > 0 ? ctx->h_red[0] / nr : 1.7976931348623157e308;
   return MGICP_OK;
@@ -1777,16 +1842,17 @@ int mgicp_debug_covariances(mgicp_ctx* ctx, int which, double* out_c6) {
   if (rc) return rc;
   Cloud& cl = which ? ctx->tgt : ctx->src;
   const size_t n = cl.n;
-  std::vector<double2> h(3 * n);
+  const size_t st = cl.cov_stride;
+  std::vector<double2> h(3 * st);
   std::vector<uint32_t> perm(n);
-  HIPCK(hipMemcpyAsync(h.data(), cl.cov.p, 3 * n * sizeof(double2), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCK(hipMemcpyAsync(h.data(), cl.cov.p, 3 * st * sizeof(double2), hipMemcpyDeviceToHost, ctx->stream));
   HIPCK(hipMemcpyAsync(perm.data(), cl.perm.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
   if ((rc = sync(ctx))) return rc;
   for (size_t p = 0; p < n; ++p) {
     double* o = out_c6 + 6 * static_cast<size_t>(perm[p]);
     o[0] = h[p].x; o[1] = h[p].y;
-    o[2] = h[n + p].x; o[3] = h[n + p].y;
-    o[4] = h[2 * n + p].x; o[5] = h[2 * n + p].y;
+    o[2] = h[st + p].x; o[3] = h[st + p].y;
+    o[4] = h[2 * st + p].x; o[5] = h[2 * st + p].y;
   }
   return MGICP_OK;
 }
@@ -1803,10 +1869,13 @@ static int debug_corr(mgicp_ctx* ctx, const float T_cm[16], bool seeded, int* ou
   if ((rc = set_output(ctx, G))) return rc;
   if ((rc = correspond(ctx, Mat4::from_cm(T_cm), G, seeded))) return rc;
   const size_t p0 = ctx->shard_p0(), p1 = ctx->shard_p1(), ns = p1 - p0;
-  std::vector<uint32_t> nn(ns), flag(ns), slot(ns), perm(n), tperm(ctx->tgt.n);
+  std::vector<uint32_t> nn(ns), flag(ns), slot(ns + 1), perm(n), tperm(ctx->tgt.n);
+  std::vector<uint32_t> cbase(static_cast<size_t>(chunk_count(ns)) + 1);
   HIPCK(hipMemcpyAsync(nn.data(), ctx->prev_pos.p, ns * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
   HIPCK(hipMemcpyAsync(flag.data(), ctx->flags.p, ns * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
-  HIPCK(hipMemcpyAsync(slot.data(), ctx->cpos.p, ns * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCK(hipMemcpyAsync(slot.data(), ctx->cpos.p, (ns + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCK(hipMemcpyAsync(cbase.data(), ctx->chunk_base.p, cbase.size() * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                       ctx->stream));
   HIPCK(hipMemcpyAsync(perm.data(), ctx->src.perm.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
   HIPCK(hipMemcpyAsync(tperm.data(), ctx->tgt.perm.p, ctx->tgt.n * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
   const size_t cap = ctx->corr_cap;
@@ -1821,7 +1890,9 @@ static int debug_corr(mgicp_ctx* ctx, const float T_cm[16], bool seeded, int* ou
     if (ok) cnt++;
     if (out_M6) {
       double* o = out_M6 + 6 * i;
-      for (int v = 0; v < 6; ++v) o[v] = ok ? M[v * cap + slot[k]] : 0.0;
+      const size_t ch = k / kChunkPts;  // the chunk's run of the streams
+      const size_t at = cbase[ch] + slot[k] - slot[ch * kChunkPts];
+      for (int v = 0; v < 6; ++v) o[v] = ok ? M[v * cap + at] : 0.0;
     }
   }
   return cnt;
@@ -1866,6 +1937,59 @@ int mgicp_debug_moments(mgicp_ctx* ctx, const float T_cm[16], double out80[80]) 
   if (rc) return rc;
   std::memcpy(out80, ctx->mom, kMomVals * sizeof(double));
   return MGICP_OK;
+}
+
+int mgicp_debug_supers(mgicp_ctx* ctx, int kind, const double* arg, double* out, int cap) {
+  if (!ctx || !arg || !out || kind < 0 || kind > 2) return MGICP_E_INVALID;
+  HIPCK(hipSetDevice(ctx->device));
+  const long long nsup = ctx->nsup_local();
+  if (nsup > cap) return fail(ctx, MGICP_E_INVALID, "debug_supers: output too small");
+  const int nv = kind == 1 ? kMomVals : kRedVals;
+  float Tcm[16];
+  for (int i = 0; i < 16 && kind != 0; ++i) Tcm[i] = static_cast<float>(arg[i]);
+  int rc;
+  const double* sup = ctx->spart.p;
+  if (kind == 0) {  // one objective pass at x over the last sweep, stopped at the supers
+    if (!ctx->have_corr) return fail(ctx, MGICP_E_INVALID, "no correspondence sweep yet");
+    cancel_gated(ctx);
+    Vec6 x;
+    for (int i = 0; i < 6; ++i) x[i] = arg[i];
+    const size_t ns = ctx->shard_p1() - ctx->shard_p0();
+    HIPCK(launch_fdf_soa(corr_soa(ctx), ctx->cpos.p, ctx->chunk_base.p, ns, apply_state(x).xf(), ctx->partial.p,
+                         ctx->spart.p, fdf_grid_blocks(ns, ctx->fdf_max_blocks), ctx->tickets.p, nullptr, 0,
+                         nullptr, 0, ctx->stream));
+  } else if (kind == 1) {
+    if (!ctx->seed_valid) return fail(ctx, MGICP_E_INVALID, "no correspondence sweep yet");
+    if ((rc = moments_pass(ctx, Mat4::from_cm(Tcm), ctx->last_guess, true))) return rc;
+    sup = ctx->msuper.p;
+  } else {
+    if ((rc = prepare(ctx, false)) || (rc = ensure_iter_buffers(ctx))) return rc;
+    const double mr = arg[16] > 0 ? arg[16] : 1.7976931348623157e308;
+    if ((rc = fitness_supers(ctx, Mat4::from_cm(Tcm), mr))) return rc;
+  }
+  if (nsup > 0)
+    HIPCK(hipMemcpyAsync(out, sup, static_cast<size_t>(nsup) * nv * sizeof(double), hipMemcpyDeviceToHost,
+                         ctx->stream));
+  if ((rc = sync(ctx))) return rc;
+  return static_cast<int>(nsup);
+}
+
+int mgicp_debug_finish_supers(mgicp_ctx* ctx, int nv, const double* rows, long long nsup, long long maxsup,
+                              int nranks, double* out) {
+  if (!ctx || !rows || !out || (nv != kRedVals && nv != kMomVals) || nsup < 0 || maxsup < 0 || nranks < 1)
+    return MGICP_E_INVALID;
+  HIPCK(hipSetDevice(ctx->device));
+  const size_t nrow = static_cast<size_t>(nranks) * maxsup * nv;
+  DevBuf<double> d, o;
+  HIPCK(d.reserve(std::max<size_t>(nrow, 1)));
+  HIPCK(o.reserve(nv));
+  if (nrow) HIPCK(hipMemcpyAsync(d.p, rows, nrow * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  HIPCK(launch_finish_supers(d.p, nsup, maxsup, nranks, nv, o.p, ctx->stream));
+  HIPCK(hipMemcpyAsync(out, o.p, nv * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+  int rc = sync(ctx);
+  d.release();
+  o.release();
+  return rc;
 }
 
 int mgicp_debug_trace(mgicp_ctx* ctx, float* out, int max_iters) {

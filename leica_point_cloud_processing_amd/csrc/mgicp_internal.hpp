@@ -60,6 +60,25 @@ constexpr int kRedThreads = 256;
 //   [0] sum r0'M r0  [1..12] sum (M r0) w'  [13..72] sum M_p (w w')_q  [73] count  [74..79] pad
 constexpr int kMomVals = 80;
 
+// The fixed global reduction tree of every sharded sum (objective passes, Gauss-Newton moments,
+// fitness): chunks of kChunkPts grid-sorted source positions (one wave each), supers of
+// kSuperChunks chunks, then the total over supers.  Shards start on super boundaries (rank r owns
+// supers [nsup * r / N, nsup * (r + 1) / N)), so every N reproduces the N = 1 sums bit for bit.
+constexpr int kChunkPts = 1024;
+constexpr int kSuperChunks = 32;
+constexpr size_t kSuperPts = static_cast<size_t>(kChunkPts) * kSuperChunks;
+inline int chunk_count(size_t n) { return static_cast<int>((n + kChunkPts - 1) / kChunkPts); }
+__host__ __device__ inline long long super_first(int r, long long nsup, int nranks) {
+  return nsup * r / nranks;
+}
+__host__ __device__ inline int super_owner(long long s, long long nsup, int nranks) {
+  int r = static_cast<int>(s * nranks / (nsup > 0 ? nsup : 1));
+  if (r > nranks - 1) r = nranks - 1;
+  while (r > 0 && s < super_first(r, nsup, nranks)) --r;
+  while (r < nranks - 1 && s >= super_first(r + 1, nsup, nranks)) ++r;
+  return r;
+}
+
 // Xform as 3x4 row-major float (the top three rows of an Eigen::Matrix4f).
 struct Xf34 { float m[12]; };
 
@@ -106,38 +125,49 @@ hipError_t launch_correspond(const GridView& tgt, const float4* src, size_t p0, 
 // Morton keys (30 bit, bbox lo, 1024 / extent = inv) of points [p0, p0 + n) and values 0..n-1
 hipError_t launch_morton_keys(const float4* pts, size_t p0, size_t n, const float lo[3], float inv,
                               uint32_t* keys, uint32_t* vals, hipStream_t s);
-// accepted correspondences -> compacted slots (pos = exclusive scan of flags), computing the
-// Mahalanobis matrices on the way
+// chunk layout of the compacted streams: base[c] (chunk_count(ns) + 1 entries, multiples of 4) from
+// pos = exclusive scan of the ns + 1 flags; zeroes each chunk's <= 3 pad slots
+hipError_t launch_chunk_base(const uint32_t* pos, size_t ns, uint32_t* base, CorrSoA out, hipStream_t s);
+// accepted correspondences -> their chunk's run of the streams, computing the Mahalanobis
+// matrices on the way
 hipError_t launch_compact(const float4* src, const float4* tpts, const Cov3& cov_s,
                           const Cov3& cov_t, Rot33d R, const uint32_t* nn_pos,
-                          const uint32_t* flags, const uint32_t* pos, size_t p0, size_t p1,
-                          CorrSoA out, hipStream_t s);
-// objective pass over m compacted correspondences (+ in-launch finish)
-// done_flag (nullable, mapped host memory): the last block stores `seq` there with a
-// system-scope release after `out`, so the host can poll instead of synchronising the stream
-hipError_t launch_fdf_soa(const CorrSoA& c, size_t m, Xf34 A, double* partial, int nb,
-                          unsigned int* ticket, double* out, int reverse,
+                          const uint32_t* flags, const uint32_t* pos, const uint32_t* chunk_base, size_t p0,
+                          size_t p1, CorrSoA out, hipStream_t s);
+// objective pass over the shard's chunks (ns source positions): chunk partials (partial,
+// chunk_count(ns) x kRedVals), super partials (spart), and with `out` the total (in-launch).
+// tickets: one per super + one, zero between passes.  done_flag (nullable, mapped host memory):
+// the finishing wave stores `seq` there with a system-scope release after `out`, so the host can
+// poll instead of synchronising the stream
+hipError_t launch_fdf_soa(const CorrSoA& c, const uint32_t* pos, const uint32_t* base, size_t ns, Xf34 A,
+                          double* partial, double* spart, int nb, unsigned int* tickets, double* out, int reverse,
                           unsigned long long* done_flag, unsigned long long seq, hipStream_t s);
 // the same pass pre-launched before its state is known: block 0 waits for cmd->seq == seq (or for
 // `timeout_ticks` of wall_clock64) and forwards the command to `mail` (device memory) for the other
 // blocks; then every block runs with its A / reverse, or exits on a cancel
-hipError_t launch_fdf_soa_gated(const CorrSoA& c, size_t m, double* partial, int nb, unsigned int* ticket,
-                                double* out, unsigned long long* done_flag, unsigned long long seq,
-                                const PassCmd* cmd, PassCmd* mail, unsigned long long timeout_ticks,
+hipError_t launch_fdf_soa_gated(const CorrSoA& c, const uint32_t* pos, const uint32_t* base, size_t ns,
+                                double* partial, double* spart, int nb, unsigned int* tickets, double* out,
+                                unsigned long long* done_flag, unsigned long long seq, const PassCmd* cmd,
+                                PassCmd* mail, unsigned long long timeout_ticks,
                                 unsigned long long* gtrace /*nullable: diagnostics*/,
                                 int host_pollers /*blocks [0, host_pollers) poll the host copy*/, hipStream_t s);
-int        fdf_grid_blocks(size_t n, int max_blocks = 2048);
+int        fdf_grid_blocks(size_t ns, int max_blocks = 2048);
+// super partials of nch chunk partials of nv (kRedVals or kMomVals) values
+hipError_t launch_super_reduce(const double* chunk, int nch, int nv, double* sup, hipStream_t s);
+// totals of nsup supers held as nranks rows of maxsup (row r: rank r's supers, from super_first(r))
+hipError_t launch_finish_supers(const double* sup, long long nsup, long long maxsup, int nranks, int nv,
+                                double* out, hipStream_t s);
 // Gauss-Newton moments of the accepted correspondences of [p0, p1) at T0 (R = rot(T0 * guess),
-// ctr = expansion centre): nb block partials of kMomVals doubles, then a one-block finish
-int        gn_grid_blocks(size_t n);
+// ctr = expansion centre): chunk partials of kMomVals doubles (grid: chunk_grid_blocks)
+int        chunk_grid_blocks(size_t ns);
 hipError_t launch_gn_moments(const float4* src, const float4* tpts, const Cov3& cov_s,
                              const Cov3& cov_t, Rot33d R, Xf34 T0, const double ctr[3],
                              const uint32_t* nn_pos, const uint32_t* flags, size_t p0, size_t p1,
                              double* partial, int nb, hipStream_t s);
-hipError_t launch_reduce_finish_moments(const double* partial, int nb, double* out, hipStream_t s);
 // n (<= 64) doubles -> mapped host memory, then seq -> the host-polled completion word
 hipError_t launch_publish(const double* in, int n, double* host_out, unsigned long long* flag,
                           unsigned long long seq, hipStream_t s);
+// fitness chunk partials ([0] sum d2, [13] count) of [p0, p1) (grid: chunk_grid_blocks)
 hipError_t launch_fitness(const GridView& tgt, const float4* src, size_t p0, size_t p1,
                           Xf34 T, double max_range, double* partial, int nb, hipStream_t s);
 hipError_t launch_reduce_finish(const double* partial, int nb, double* out, hipStream_t s);

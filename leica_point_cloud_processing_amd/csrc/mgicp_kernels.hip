@@ -969,19 +969,23 @@ __device__ __forceinline__ void mahalanobis(const Rot33d& R, const double (&C1)[
 #undef COF
 }
 
-// Accepted correspondence p -> compacted slot pos[p]: the matched target point and its
-// Mahalanobis matrix, written straight into the SoA streams.
+// Accepted correspondence p -> its slot in its chunk's run of the streams (chunk c = (p - p0) /
+// kChunkPts starts at chunk_base[c], a multiple of 4; within a chunk, grid-sorted order): the
+// matched target point and its Mahalanobis matrix, written straight into the SoA streams.
 __global__ __launch_bounds__(256) void compact_kernel(const float4* __restrict__ src,
                                                       const float4* __restrict__ tpts, Cov3 cov_s,
                                                       Cov3 cov_t, Rot33d R,
                                                       const uint32_t* __restrict__ nn_pos,
                                                       const uint32_t* __restrict__ flags,
-                                                      const uint32_t* __restrict__ pos, size_t p0,
+                                                      const uint32_t* __restrict__ pos,
+                                                      const uint32_t* __restrict__ chunk_base, size_t p0,
                                                       size_t p1, CorrSoA o) {
-  const size_t p = p0 + static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (p >= p1 || !flags[p - p0]) return;
-  const uint32_t j = nn_pos[p - p0];
-  const size_t i = pos[p - p0];
+  const size_t k = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const size_t p = p0 + k;
+  if (p >= p1 || !flags[k]) return;
+  const uint32_t j = nn_pos[k];
+  const size_t c = k / kChunkPts;
+  const size_t i = chunk_base[c] + (pos[k] - pos[c * kChunkPts]);
   const float4 s = src[p], t = tpts[j];
   double C1[3][3], C2[3][3], m6[6];
   load_cov(cov_s, p, C1);
@@ -991,6 +995,47 @@ __global__ __launch_bounds__(256) void compact_kernel(const float4* __restrict__
   o.m11[i] = m6[3]; o.m12[i] = m6[4]; o.m22[i] = m6[5];
   o.sx[i] = s.x; o.sy[i] = s.y; o.sz[i] = s.z;
   o.qx[i] = t.x; o.qy[i] = t.y; o.qz[i] = t.z;
+}
+
+// Chunk layout of the compacted streams (one 1024-thread block): chunk c of the shard (source
+// positions [c * kChunkPts, (c + 1) * kChunkPts) of the shard, a fixed global partition -- shards
+// start on super boundaries) holds cnt_c = pos[end] - pos[start] correspondences at
+// base[c] = sum_{c' < c} round_up_4(cnt_c'); base[nch] is the stream length.  The <= 3 pad slots
+// after each chunk's run are zeroed (M = 0: they add signed zeros only).
+__global__ __launch_bounds__(1024) void chunk_base_kernel(const uint32_t* __restrict__ pos, size_t ns, int nch,
+                                                          uint32_t* __restrict__ base, CorrSoA o) {
+  __shared__ uint32_t wsum[16];
+  const int per = (nch + 1023) / 1024;
+  const int c0 = min(nch, static_cast<int>(threadIdx.x) * per), c1 = min(nch, c0 + per);
+  auto count = [&](int c) {
+    const size_t e = min(static_cast<size_t>(c + 1) * kChunkPts, ns);
+    return pos[e] - pos[static_cast<size_t>(c) * kChunkPts];
+  };
+  uint32_t loc = 0;
+  for (int c = c0; c < c1; ++c) loc += (count(c) + 3u) & ~3u;
+  // block exclusive scan of loc
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t inc = loc;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t u = __shfl_up(inc, off, 64);
+    if (lane >= off) inc += u;
+  }
+  if (lane == 63) wsum[wid] = inc;
+  __syncthreads();
+  uint32_t before = 0;
+  for (int w = 0; w < wid; ++w) before += wsum[w];
+  uint32_t run = before + inc - loc;
+  for (int c = c0; c < c1; ++c) {
+    base[c] = run;
+    const uint32_t cnt = count(c), pad = (cnt + 3u) & ~3u;
+    for (uint32_t i = run + cnt; i < run + pad; ++i) {
+      o.sx[i] = 0.f; o.sy[i] = 0.f; o.sz[i] = 0.f; o.qx[i] = 0.f; o.qy[i] = 0.f; o.qz[i] = 0.f;
+      o.m00[i] = 0.0; o.m01[i] = 0.0; o.m02[i] = 0.0; o.m11[i] = 0.0; o.m12[i] = 0.0; o.m22[i] = 0.0;
+    }
+    run += pad;
+  }
+  if (threadIdx.x == 1023) base[nch] = before + inc;
 }
 
 // ------------------------------------------------------------------------------------
@@ -1023,68 +1068,74 @@ __device__ __forceinline__ void block_reduce_store(double (&acc)[kRedVals], doub
   }
 }
 
-// In-launch deterministic finish, fence-free form of cdna_hip_programming.md Guideline 16
-// (MI355X_MICROARCH.md "Valid forms", first table row): the 16 partial sums of each block are
-// stored write-through (sc1, relaxed agent-scope atomic stores) by wave 0, which drains them
-// (s_waitcnt vmcnt(0)) before one lane takes an agent-scope ticket; the block drawing the last
-// ticket reads every partial with sc1 loads (relaxed agent-scope atomic loads), sums them in block
-// order and writes `out` (device memory or mapped pinned host memory), then re-arms the ticket.
-// No buffer_wbl2 / buffer_inv: a release fence per block cost ~25 us per launch at 1024 blocks.
-__device__ __forceinline__ void store_partial_sc1(double (&acc)[kRedVals], double* dst) {
-  __shared__ double sm[4][kRedVals];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  __syncthreads();
+// ---- the fixed global reduction tree (identical for every rank count) ----------------------
+//   chunk  (kChunkPts source positions of the grid-sorted cloud): one wave; lane l accumulates
+//          its elements in order, then wave_sum's shuffle tree          -> partial[c][v]
+//   super  (kSuperChunks consecutive chunks): partial[c0][v] + partial[c0+1][v] + ... in order
+//   total  lane l sums supers l, l + 64, ... in order, then wave_sum    -> out[v]
+// Shards start on super boundaries, so a rank's supers are exactly the N = 1 run's supers with
+// the same indices; a multi-GPU pass all-gathers the supers and runs the same total.
+// In-launch finish, fence-free form of cdna_hip_programming.md Guideline 16 (MI355X_MICROARCH.md
+// "Valid forms", first table row): partials are stored write-through (sc1, relaxed agent-scope
+// atomic stores) and drained (s_waitcnt vmcnt(0)) before an agent-scope ticket is taken; the wave
+// drawing the last ticket reads them with sc1 loads.  No buffer_wbl2 / buffer_inv (a release
+// fence per block cost ~25 us per launch at 1024 blocks).
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __longlong_as_double(static_cast<long long>(__hip_atomic_load(
+      const_cast<unsigned long long*>(reinterpret_cast<const unsigned long long*>(p)), __ATOMIC_RELAXED,
+      __HIP_MEMORY_SCOPE_AGENT)));
+}
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), static_cast<unsigned long long>(__double_as_longlong(v)),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// one wave: values [v0, v0 + 16) of the total over nsup supers of NV values each, held as
+// nranks rows of maxsup supers (row r = the supers of rank r, super_first(r) onwards); lane 0
+// writes out[v0 + v]
+template <int NV, bool kSc1>
+__device__ __forceinline__ void wave_total(const double* sup, long long nsup, long long maxsup, int nranks, int v0,
+                                           double* out) {
+  const int lane = threadIdx.x & 63;
+  double acc[16];
 #pragma unroll
-  for (int v = 0; v < kRedVals; ++v) {
-    const double w = wave_sum(acc[v]);
-    if (lane == 0) sm[wid][v] = w;
+  for (int v = 0; v < 16; ++v) acc[v] = 0.0;
+  for (long long sg = lane; sg < nsup; sg += 64) {
+    size_t at = static_cast<size_t>(sg);
+    if (nranks > 1) {
+      const int r = super_owner(sg, nsup, nranks);
+      at = static_cast<size_t>(r) * maxsup + (sg - super_first(r, nsup, nranks));
+    }
+    const double* row = sup + at * NV + v0;
+#pragma unroll
+    for (int v = 0; v < 16; ++v)
+      if (v0 + v < NV) acc[v] += kSc1 ? ld_sc1(row + v) : row[v];
   }
-  __syncthreads();
-  if (threadIdx.x < kRedVals) {
-    const int v = threadIdx.x;
-    double s = sm[0][v];
-    s = s + sm[1][v];
-    s = s + sm[2][v];
-    s = s + sm[3][v];
-    __hip_atomic_store(reinterpret_cast<unsigned long long*>(dst + v),
-                       static_cast<unsigned long long>(__double_as_longlong(s)), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (int v = 0; v < 16; ++v) acc[v] = wave_sum(acc[v]);
+  if (lane == 0) {
+#pragma unroll
+    for (int v = 0; v < 16; ++v)
+      if (v0 + v < NV) out[v0 + v] = acc[v];
   }
 }
 
-__device__ __forceinline__ void finish_in_last_block(const double* partial, unsigned int* ticket,
-                                                     double* out,
-                                                     unsigned long long* done_flag = nullptr,
-                                                     unsigned long long seq = 0) {
-  __shared__ int last;
-  if (threadIdx.x < 64) {  // wave 0 issued every partial store of this block
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (threadIdx.x == 0) {
-      const unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      last = (prev == gridDim.x - 1) ? 1 : 0;
-    }
-  }
-  __syncthreads();
-  if (!last) return;
-  double acc[kRedVals];
-#pragma unroll
-  for (int v = 0; v < kRedVals; ++v) acc[v] = 0.0;
-  const int nb = gridDim.x;
-  const unsigned long long* pp = reinterpret_cast<const unsigned long long*>(partial);
-  for (int b = threadIdx.x; b < nb; b += blockDim.x) {
-#pragma unroll
-    for (int v = 0; v < kRedVals; ++v)
-      acc[v] += __longlong_as_double(static_cast<long long>(__hip_atomic_load(
-          const_cast<unsigned long long*>(pp + static_cast<size_t>(b) * kRedVals + v),
-          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
-  }
-  block_reduce_store(acc, out);
-  if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (done_flag && threadIdx.x < 64) {
-    // wave 0 wrote every out[v]; once they are drained, publish the pass number to the host
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (threadIdx.x == 0) __hip_atomic_store(done_flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+// super partials of nch chunk partials (NV values each): block s, thread v < NV
+template <int NV>
+__global__ void super_reduce_kernel(const double* __restrict__ chunk, int nch, double* __restrict__ sup) {
+  const int v = threadIdx.x, sj = blockIdx.x;
+  if (v >= NV) return;
+  const int c0 = sj * kSuperChunks, nin = min(kSuperChunks, nch - c0);
+  double a = chunk[static_cast<size_t>(c0) * NV + v];
+  for (int q = 1; q < nin; ++q) a = a + chunk[static_cast<size_t>(c0 + q) * NV + v];
+  sup[static_cast<size_t>(sj) * NV + v] = a;
+}
+
+// totals of all supers (one wave per 16 values); rows of maxsup supers per rank
+template <int NV>
+__global__ __launch_bounds__(64) void finish_supers_kernel(const double* __restrict__ sup, long long nsup,
+                                                           long long maxsup, int nranks, double* __restrict__ out) {
+  wave_total<NV, false>(sup, nsup, maxsup, nranks, 16 * blockIdx.x, out);
 }
 
 // the 8 x 16 bytes of a command block: system-coherent loads of the host's pinned copy
@@ -1140,7 +1191,6 @@ __device__ __forceinline__ void fdf_point(const Xf34& A, float sx, float sy, flo
   acc[4] += dx * t0; acc[5] += dx * t1; acc[6] += dx * t2;
   acc[7] += dy * t0; acc[8] += dy * t1; acc[9] += dy * t2;
   acc[10] += dz * t0; acc[11] += dz * t1; acc[12] += dz * t2;
-  acc[13] += 1.0;
 }
 
 // Objective pass over the compacted streams: 4 correspondences per thread-iteration, every load
@@ -1152,8 +1202,10 @@ __device__ __forceinline__ void fdf_point(const Xf34& A, float sx, float sy, flo
 // an exit).  The host pre-launches pass k + 1 while pass k runs, so the next pass is resident
 // when the host's BFGS step publishes x_{k+1}: no launch latency between consecutive passes.
 template <bool kGated>
-__device__ __forceinline__ void fdf_soa_body(CorrSoA c, size_t m, Xf34 A, double* __restrict__ partial,
-                                             unsigned int* __restrict__ ticket, double* __restrict__ out,
+__device__ __forceinline__ void fdf_soa_body(CorrSoA c, const uint32_t* __restrict__ pos,
+                                             const uint32_t* __restrict__ base, size_t ns, int nch, Xf34 A,
+                                             double* __restrict__ partial, double* __restrict__ spart,
+                                             unsigned int* __restrict__ tickets, double* __restrict__ out,
                                              int reverse, unsigned long long* done_flag,
                                              unsigned long long seq, const PassCmd* cmd, PassCmd* mail,
                                              unsigned long long timeout, unsigned long long* gtrace,
@@ -1201,90 +1253,141 @@ __device__ __forceinline__ void fdf_soa_body(CorrSoA c, size_t m, Xf34 A, double
     for (int i = 0; i < 12; ++i) A.m[i] = __uint_as_float(sw[i]);
     reverse = static_cast<int>(sw[13]);
   }
-  double acc[kRedVals];
+  // persistent waves over the shard's chunks (reverse: back to front, so the tail of the previous
+  // pass, still in the 256 MiB Infinity Cache, is consumed first)
+  const int lane = threadIdx.x & 63;
+  const int nw = gridDim.x * (blockDim.x >> 6);
+  const int nsup = (nch + kSuperChunks - 1) / kSuperChunks;
+  const int w0 = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
+  for (int w = w0; w < nch; w += nw) {
+    const int j = (reverse & 1) ? nch - 1 - w : w;
+    double acc[kRedVals];
 #pragma unroll
-  for (int v = 0; v < kRedVals; ++v) acc[v] = 0.0;
-  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
-  const size_t m4 = m / 4;
-  for (size_t k = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; k < m4; k += stride) {
-    // reverse: the chip walks the streams back to front, so the tail of the previous pass
-    // (still in the 256 MiB Infinity Cache) is consumed first
-    const size_t i = reverse ? m4 - 1 - k : k;
-    const float4 sx = reinterpret_cast<const float4*>(c.sx)[i];
-    const float4 sy = reinterpret_cast<const float4*>(c.sy)[i];
-    const float4 sz = reinterpret_cast<const float4*>(c.sz)[i];
-    const float4 qx = reinterpret_cast<const float4*>(c.qx)[i];
-    const float4 qy = reinterpret_cast<const float4*>(c.qy)[i];
-    const float4 qz = reinterpret_cast<const float4*>(c.qz)[i];
-    const double2* M00 = reinterpret_cast<const double2*>(c.m00) + 2 * i;
-    const double2* M01 = reinterpret_cast<const double2*>(c.m01) + 2 * i;
-    const double2* M02 = reinterpret_cast<const double2*>(c.m02) + 2 * i;
-    const double2* M11 = reinterpret_cast<const double2*>(c.m11) + 2 * i;
-    const double2* M12 = reinterpret_cast<const double2*>(c.m12) + 2 * i;
-    const double2* M22 = reinterpret_cast<const double2*>(c.m22) + 2 * i;
-    const double2 a0 = M00[0], a1 = M00[1], b0 = M01[0], b1 = M01[1], e0 = M02[0], e1 = M02[1];
-    const double2 f0 = M11[0], f1 = M11[1], g0 = M12[0], g1 = M12[1], h0 = M22[0], h1 = M22[1];
-    fdf_point(A, sx.x, sy.x, sz.x, qx.x, qy.x, qz.x, a0.x, b0.x, e0.x, f0.x, g0.x, h0.x, acc);
-    fdf_point(A, sx.y, sy.y, sz.y, qx.y, qy.y, qz.y, a0.y, b0.y, e0.y, f0.y, g0.y, h0.y, acc);
-    fdf_point(A, sx.z, sy.z, sz.z, qx.z, qy.z, qz.z, a1.x, b1.x, e1.x, f1.x, g1.x, h1.x, acc);
-    fdf_point(A, sx.w, sy.w, sz.w, qx.w, qy.w, qz.w, a1.y, b1.y, e1.y, f1.y, g1.y, h1.y, acc);
+    for (int v = 0; v < kRedVals; ++v) acc[v] = 0.0;
+    const uint32_t g1 = base[j + 1] >> 2;
+    for (uint32_t i = (base[j] >> 2) + lane; i < g1; i += 64) {
+      const float4 sx = reinterpret_cast<const float4*>(c.sx)[i];
+      const float4 sy = reinterpret_cast<const float4*>(c.sy)[i];
+      const float4 sz = reinterpret_cast<const float4*>(c.sz)[i];
+      const float4 qx = reinterpret_cast<const float4*>(c.qx)[i];
+      const float4 qy = reinterpret_cast<const float4*>(c.qy)[i];
+      const float4 qz = reinterpret_cast<const float4*>(c.qz)[i];
+      const double2* M00 = reinterpret_cast<const double2*>(c.m00) + 2 * static_cast<size_t>(i);
+      const double2* M01 = reinterpret_cast<const double2*>(c.m01) + 2 * static_cast<size_t>(i);
+      const double2* M02 = reinterpret_cast<const double2*>(c.m02) + 2 * static_cast<size_t>(i);
+      const double2* M11 = reinterpret_cast<const double2*>(c.m11) + 2 * static_cast<size_t>(i);
+      const double2* M12 = reinterpret_cast<const double2*>(c.m12) + 2 * static_cast<size_t>(i);
+      const double2* M22 = reinterpret_cast<const double2*>(c.m22) + 2 * static_cast<size_t>(i);
+      const double2 a0 = M00[0], a1 = M00[1], b0 = M01[0], b1 = M01[1], e0 = M02[0], e1 = M02[1];
+      const double2 f0 = M11[0], f1 = M11[1], g0 = M12[0], g1v = M12[1], h0 = M22[0], h1 = M22[1];
+      fdf_point(A, sx.x, sy.x, sz.x, qx.x, qy.x, qz.x, a0.x, b0.x, e0.x, f0.x, g0.x, h0.x, acc);
+      fdf_point(A, sx.y, sy.y, sz.y, qx.y, qy.y, qz.y, a0.y, b0.y, e0.y, f0.y, g0.y, h0.y, acc);
+      fdf_point(A, sx.z, sy.z, sz.z, qx.z, qy.z, qz.z, a1.x, b1.x, e1.x, f1.x, g1v.x, h1.x, acc);
+      fdf_point(A, sx.w, sy.w, sz.w, qx.w, qy.w, qz.w, a1.y, b1.y, e1.y, f1.y, g1v.y, h1.y, acc);
+    }
+    if (reverse & 2) {  // timing diagnostics only (MGICP_FDF_DIAG): stream, no reduction
+      if (acc[0] == 12345.0) partial[j] = acc[1];
+      continue;
+    }
+    // chunk partial; the count is exact from the scan (pad slots are not counted)
+    const size_t e = min(static_cast<size_t>(j + 1) * kChunkPts, ns);
+    const double cnt = static_cast<double>(pos[e] - pos[static_cast<size_t>(j) * kChunkPts]);
+#pragma unroll
+    for (int v = 0; v < 13; ++v) acc[v] = wave_sum(acc[v]);
+    double* pj = partial + static_cast<size_t>(j) * kRedVals;
+    if (reverse & 4) {  // timing diagnostics only: chunk partials, no tickets
+      if (lane == 0)
+        for (int v = 0; v < 13; ++v) pj[v] = acc[v];
+      continue;
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int v = 0; v < 13; ++v) st_sc1(pj + v, acc[v]);
+      st_sc1(pj + 13, cnt);
+      st_sc1(pj + 14, 0.0);
+      st_sc1(pj + 15, 0.0);
+    }
   }
-  // tail (m % 4 correspondences) on the first threads of the grid
-  const size_t t = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (t < m - 4 * m4) {
-    const size_t j = 4 * m4 + t;
-    fdf_point(A, c.sx[j], c.sy[j], c.sz[j], c.qx[j], c.qy[j], c.qz[j], c.m00[j], c.m01[j], c.m02[j],
-              c.m11[j], c.m12[j], c.m22[j], acc);
+  if (w0 >= nch || (reverse & 6)) return;
+  // tickets, once per wave after all of its chunks (a per-chunk drain + atomic round trip cost
+  // ~60 us per pass at 256 blocks): lane k takes the super of the wave's k-th chunk
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int nmine = (nch - w0 + nw - 1) / nw;  // <= 64: the grid has >= nch / 64 waves
+  int last = 0;
+  if (lane < nmine) {
+    const int w = w0 + lane * nw;
+    const int j = (reverse & 1) ? nch - 1 - w : w;
+    const int sj = j / kSuperChunks, nin = min(kSuperChunks, nch - sj * kSuperChunks);
+    last = __hip_atomic_fetch_add(tickets + sj, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                   static_cast<unsigned>(nin - 1) ? 1 : 0;
   }
-  if (ticket) {
-    store_partial_sc1(acc, partial + static_cast<size_t>(blockIdx.x) * kRedVals);
-    finish_in_last_block(partial, ticket, out, done_flag, seq);
-  } else {
-    block_reduce_store(acc, partial + static_cast<size_t>(blockIdx.x) * kRedVals);
+  unsigned long long done = __ballot(last);
+  while (done) {
+    // this wave completed super sj: its partial (chunk order), then the global ticket
+    const int k = __builtin_ctzll(done);
+    done &= done - 1;
+    const int w = w0 + k * nw;
+    const int j = (reverse & 1) ? nch - 1 - w : w;
+    const int sj = j / kSuperChunks, cfirst = sj * kSuperChunks, nin = min(kSuperChunks, nch - cfirst);
+    if (lane < kRedVals) {
+      // all kSuperChunks loads in flight at once (a runtime-bounded loop issued them one round
+      // trip at a time), then the chunk-order sum
+      double t[kSuperChunks];
+#pragma unroll
+      for (int q = 0; q < kSuperChunks; ++q)
+        t[q] = ld_sc1(partial + static_cast<size_t>(cfirst + min(q, nin - 1)) * kRedVals + lane);
+      double a = t[0];
+#pragma unroll
+      for (int q = 1; q < kSuperChunks; ++q)
+        if (q < nin) a = a + t[q];
+      st_sc1(spart + static_cast<size_t>(sj) * kRedVals + lane, a);
+    }
+    int lastg = 0;
+    if (lane == 0) {
+      __hip_atomic_store(tickets + sj, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lastg = __hip_atomic_fetch_add(tickets + nsup, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                      static_cast<unsigned>(nsup - 1) ? 1 : 0;
+    }
+    if (!__shfl(lastg, 0, 64)) continue;
+    // every super is stored: the total (single rank; with out == nullptr the supers are the result)
+    if (out) wave_total<kRedVals, true>(spart, nsup, nsup, 1, 0, out);
+    if (lane == 0) {
+      __hip_atomic_store(tickets + nsup, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (done_flag && out) {
+        // lane 0 wrote every out[v]; once they are drained, publish the pass number to the host
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(done_flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
   }
 }
 
-__global__ __launch_bounds__(256) void fdf_soa_kernel(CorrSoA c, size_t m, Xf34 A, double* __restrict__ partial,
-                                                      unsigned int* __restrict__ ticket, double* __restrict__ out,
+__global__ __launch_bounds__(256) void fdf_soa_kernel(CorrSoA c, const uint32_t* __restrict__ pos,
+                                                      const uint32_t* __restrict__ base, size_t ns, int nch, Xf34 A,
+                                                      double* __restrict__ partial, double* __restrict__ spart,
+                                                      unsigned int* __restrict__ tickets, double* __restrict__ out,
                                                       int reverse, unsigned long long* done_flag,
                                                       unsigned long long seq) {
-  fdf_soa_body<false>(c, m, A, partial, ticket, out, reverse, done_flag, seq, nullptr, nullptr, 0, nullptr, 0);
+  fdf_soa_body<false>(c, pos, base, ns, nch, A, partial, spart, tickets, out, reverse, done_flag, seq, nullptr,
+                      nullptr, 0, nullptr, 0);
 }
 
-__global__ __launch_bounds__(256) void fdf_soa_gated_kernel(CorrSoA c, size_t m, double* __restrict__ partial,
-                                                            unsigned int* __restrict__ ticket,
+__global__ __launch_bounds__(256) void fdf_soa_gated_kernel(CorrSoA c, const uint32_t* __restrict__ pos,
+                                                            const uint32_t* __restrict__ base, size_t ns, int nch,
+                                                            double* __restrict__ partial, double* __restrict__ spart,
+                                                            unsigned int* __restrict__ tickets,
                                                             double* __restrict__ out, unsigned long long* done_flag,
                                                             unsigned long long seq, const PassCmd* cmd,
                                                             PassCmd* mail, unsigned long long timeout,
                                                             unsigned long long* gtrace, int host_pollers) {
-  fdf_soa_body<true>(c, m, Xf34{}, partial, ticket, out, 0, done_flag, seq, cmd, mail, timeout, gtrace,
-                     host_pollers);
+  fdf_soa_body<true>(c, pos, base, ns, nch, Xf34{}, partial, spart, tickets, out, 0, done_flag, seq, cmd, mail,
+                     timeout, gtrace, host_pollers);
 }
 
 // ------------------------------------------------------------------------------------
 // Gauss-Newton moment pass (MGICP_SOLVER_GN)
 // ------------------------------------------------------------------------------------
-// NV doubles reduced across a 256-thread block; threads < NV write dst[0..NV-1]
-template <int NV>
-__device__ __forceinline__ void block_reduce_store_n(double (&acc)[NV], double* dst) {
-  __shared__ double sm[4][NV];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-  for (int v = 0; v < NV; ++v) {
-    const double w = wave_sum(acc[v]);
-    if (lane == 0) sm[wid][v] = w;
-  }
-  __syncthreads();
-  if (threadIdx.x < NV) {
-    const int v = threadIdx.x;
-    double s = sm[0][v];
-    s = s + sm[1][v];
-    s = s + sm[2][v];
-    s = s + sm[3][v];
-    dst[v] = s;
-  }
-}
-
 // For a fixed correspondence set the GICP objective is an exact quadratic in A = [R | t]
 // (DESIGN.md "The moment form"), so ONE pass per outer iteration collects everything the host
 // Gauss-Newton solve needs: with the correspondence transform T0, r0 = fl(fl(T0 s) - q) and
@@ -1292,16 +1395,20 @@ __device__ __forceinline__ void block_reduce_store_n(double (&acc)[NV], double* 
 //   [0] sum r0' M r0   [1 + 4a + k] sum (M r0)_a w_k   [13 + 10p + q] sum M_p (w w')_q   [73] count
 // (p over the 6 upper-triangle entries of M, q over the 10 of w w').  The Mahalanobis matrix is
 // computed on the fly (no compaction, no SoA streams): 136 B read per source point of the shard.
+// One wave per chunk of the shard (chunk partials of the fixed reduction tree); lane l takes the
+// chunk's positions l, l + 64, ... in order.
 __global__ __launch_bounds__(256) void gn_moments_kernel(
     const float4* __restrict__ src, const float4* __restrict__ tpts, Cov3 cov_s, Cov3 cov_t,
     Rot33d R, Xf34 T0, double cx, double cy, double cz, const uint32_t* __restrict__ nn_pos,
     const uint32_t* __restrict__ flags, size_t p0, size_t p1, double* __restrict__ partial) {
+  const size_t ch = (static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const size_t c0 = p0 + ch * kChunkPts;
+  if (c0 >= p1) return;
+  const size_t c1 = min(c0 + kChunkPts, p1);
   double acc[kMomVals];
 #pragma unroll
   for (int v = 0; v < kMomVals; ++v) acc[v] = 0.0;
-  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
-  for (size_t p = p0 + static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; p < p1;
-       p += stride) {
+  for (size_t p = c0 + (threadIdx.x & 63); p < c1; p += 64) {
     if (!flags[p - p0]) continue;
     const uint32_t j = nn_pos[p - p0];
     const float4 s = src[p], t = tpts[j];
@@ -1334,21 +1441,12 @@ __global__ __launch_bounds__(256) void gn_moments_kernel(
       for (int q = 0; q < 10; ++q) acc[13 + 10 * pp + q] += m6[pp] * ww[q];
     acc[73] += 1.0;
   }
-  block_reduce_store_n<kMomVals>(acc, partial + static_cast<size_t>(blockIdx.x) * kMomVals);
-}
-
-// one block per moment: block v sums column v of the nb block partials (thread-strided, then a
-// fixed shuffle / LDS tree: deterministic)
-__global__ __launch_bounds__(256) void reduce_finish_moments_kernel(const double* __restrict__ partial,
-                                                                    int nb, double* __restrict__ out) {
-  const int v = blockIdx.x;
-  double acc = 0.0;
-  for (int b = threadIdx.x; b < nb; b += blockDim.x) acc += partial[static_cast<size_t>(b) * kMomVals + v];
-  double one[1] = {acc};
-  __shared__ double res[1];
-  block_reduce_store_n<1>(one, res);
-  __syncthreads();
-  if (threadIdx.x == 0) out[v] = res[0];
+#pragma unroll
+  for (int v = 0; v < kMomVals; ++v) acc[v] = wave_sum(acc[v]);
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int v = 0; v < kMomVals; ++v) partial[ch * kMomVals + v] = acc[v];
+  }
 }
 
 // n doubles of device memory -> mapped host memory, then `seq` into the host-polled completion
@@ -1361,15 +1459,19 @@ __global__ void publish_kernel(const double* __restrict__ in, int n, double* out
   if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// one wave per chunk of the shard, like gn_moments_kernel: chunk partials [0] sum d2, [13] count
 __global__ __launch_bounds__(256) void fitness_kernel(GridView tg, const float4* __restrict__ src,
                                                       size_t p0, size_t p1, Xf34 T,
                                                       double max_range,
                                                       double* __restrict__ partial) {
+  const size_t ch = (static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const size_t c0 = p0 + ch * kChunkPts;
+  if (c0 >= p1) return;
+  const size_t c1 = min(c0 + kChunkPts, p1);
   double acc[kRedVals];
 #pragma unroll
   for (int v = 0; v < kRedVals; ++v) acc[v] = 0.0;
-  const size_t p = p0 + static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (p < p1) {
+  for (size_t p = c0 + (threadIdx.x & 63); p < c1; p += 64) {
     const float4 s = src[p];
     float qx, qy, qz;
     xform(T, s.x, s.y, s.z, qx, qy, qz);
@@ -1380,12 +1482,17 @@ __global__ __launch_bounds__(256) void fitness_kernel(GridView tg, const float4*
     if (vis.best != ~0ull) {
       const float d2 = __uint_as_float(static_cast<uint32_t>(vis.best >> 32));
       if (static_cast<double>(d2) <= max_range) {
-        acc[0] = d2;
-        acc[13] = 1.0;
+        acc[0] += d2;
+        acc[13] += 1.0;
       }
     }
   }
-  block_reduce_store(acc, partial + static_cast<size_t>(blockIdx.x) * kRedVals);
+  acc[0] = wave_sum(acc[0]);
+  acc[13] = wave_sum(acc[13]);
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int v = 0; v < kRedVals; ++v) partial[ch * kRedVals + v] = acc[v];
+  }
 }
 
 // Utils::computeCloudResolution: sqrt of the 2nd-nearest (self is 1st) float d2, summed in fp64
@@ -1709,29 +1816,58 @@ hipError_t launch_morton_keys(const float4* pts, size_t p0, size_t n, const floa
   return hipGetLastError();
 }
 
+hipError_t launch_chunk_base(const uint32_t* pos, size_t ns, uint32_t* base, CorrSoA out, hipStream_t s) {
+  const int nch = chunk_count(ns);
+  if (nch == 0) return hipSuccess;
+  chunk_base_kernel<<<1, 1024, 0, s>>>(pos, ns, nch, base, out);
+  return hipGetLastError();
+}
 hipError_t launch_compact(const float4* src, const float4* tpts, const Cov3& cov_s,
                           const Cov3& cov_t, Rot33d R, const uint32_t* nn_pos,
-                          const uint32_t* flags, const uint32_t* pos, size_t p0, size_t p1,
-                          CorrSoA out, hipStream_t s) {
+                          const uint32_t* flags, const uint32_t* pos, const uint32_t* chunk_base, size_t p0,
+                          size_t p1, CorrSoA out, hipStream_t s) {
   if (p1 <= p0) return hipSuccess;
-  compact_kernel<<<nblk(p1 - p0), 256, 0, s>>>(src, tpts, cov_s, cov_t, R, nn_pos, flags, pos, p0,
-                                               p1, out);
+  compact_kernel<<<nblk(p1 - p0), 256, 0, s>>>(src, tpts, cov_s, cov_t, R, nn_pos, flags, pos, chunk_base,
+                                               p0, p1, out);
   return hipGetLastError();
 }
 
-hipError_t launch_fdf_soa(const CorrSoA& c, size_t m, Xf34 A, double* partial, int nb,
-                          unsigned int* ticket, double* out, int reverse,
+hipError_t launch_fdf_soa(const CorrSoA& c, const uint32_t* pos, const uint32_t* base, size_t ns, Xf34 A,
+                          double* partial, double* spart, int nb, unsigned int* tickets, double* out, int reverse,
                           unsigned long long* done_flag, unsigned long long seq, hipStream_t s) {
-  fdf_soa_kernel<<<nb, 256, 0, s>>>(c, m, A, partial, ticket, out, reverse, done_flag, seq);
+  const int nch = chunk_count(ns);
+  if (nch == 0) return hipSuccess;
+  fdf_soa_kernel<<<nb, 256, 0, s>>>(c, pos, base, ns, nch, A, partial, spart, tickets, out, reverse, done_flag,
+                                    seq);
   return hipGetLastError();
 }
 
-hipError_t launch_fdf_soa_gated(const CorrSoA& c, size_t m, double* partial, int nb, unsigned int* ticket,
-                                double* out, unsigned long long* done_flag, unsigned long long seq,
-                                const PassCmd* cmd, PassCmd* mail, unsigned long long timeout_ticks,
-                                unsigned long long* gtrace, int host_pollers, hipStream_t s) {
-  fdf_soa_gated_kernel<<<nb, 256, 0, s>>>(c, m, partial, ticket, out, done_flag, seq, cmd, mail, timeout_ticks,
-                                          gtrace, host_pollers);
+hipError_t launch_fdf_soa_gated(const CorrSoA& c, const uint32_t* pos, const uint32_t* base, size_t ns,
+                                double* partial, double* spart, int nb, unsigned int* tickets, double* out,
+                                unsigned long long* done_flag, unsigned long long seq, const PassCmd* cmd,
+                                PassCmd* mail, unsigned long long timeout_ticks, unsigned long long* gtrace,
+                                int host_pollers, hipStream_t s) {
+  const int nch = chunk_count(ns);
+  if (nch == 0) return hipSuccess;
+  fdf_soa_gated_kernel<<<nb, 256, 0, s>>>(c, pos, base, ns, nch, partial, spart, tickets, out, done_flag, seq,
+                                          cmd, mail, timeout_ticks, gtrace, host_pollers);
+  return hipGetLastError();
+}
+
+hipError_t launch_super_reduce(const double* chunk, int nch, int nv, double* sup, hipStream_t s) {
+  if (nch <= 0) return hipSuccess;
+  const int nsup = (nch + kSuperChunks - 1) / kSuperChunks;
+  if (nv == kRedVals) super_reduce_kernel<kRedVals><<<nsup, 64, 0, s>>>(chunk, nch, sup);
+  else if (nv == kMomVals) super_reduce_kernel<kMomVals><<<nsup, 128, 0, s>>>(chunk, nch, sup);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t launch_finish_supers(const double* sup, long long nsup, long long maxsup, int nranks, int nv,
+                                double* out, hipStream_t s) {
+  if (nv == kRedVals) finish_supers_kernel<kRedVals><<<1, 64, 0, s>>>(sup, nsup, maxsup, nranks, out);
+  else if (nv == kMomVals) finish_supers_kernel<kMomVals><<<kMomVals / 16, 64, 0, s>>>(sup, nsup, maxsup, nranks, out);
+  else return hipErrorInvalidValue;
   return hipGetLastError();
 }
 
@@ -1741,10 +1877,8 @@ hipError_t launch_publish(const double* in, int n, double* host_out, unsigned lo
   return hipGetLastError();
 }
 
-int gn_grid_blocks(size_t n) {
-  // ~16 source points per thread, at most 1024 blocks (the finish reads nb x 80 doubles)
-  const size_t want = (n + 256 * 16 - 1) / (256 * 16);
-  return static_cast<int>(std::max<size_t>(1, std::min<size_t>(want, 1024)));
+int chunk_grid_blocks(size_t ns) {  // one wave per chunk, 4 waves per block
+  return static_cast<int>(std::max<size_t>(1, (static_cast<size_t>(chunk_count(ns)) + 3) / 4));
 }
 
 hipError_t launch_gn_moments(const float4* src, const float4* tpts, const Cov3& cov_s,
@@ -1756,15 +1890,13 @@ hipError_t launch_gn_moments(const float4* src, const float4* tpts, const Cov3& 
   return hipGetLastError();
 }
 
-hipError_t launch_reduce_finish_moments(const double* partial, int nb, double* out, hipStream_t s) {
-  reduce_finish_moments_kernel<<<kMomVals, 256, 0, s>>>(partial, nb, out);
-  return hipGetLastError();
-}
 
-int fdf_grid_blocks(size_t n, int max_blocks) {
-  // ~8 points per thread keeps >= 8 waves per CU resident on 256 CUs at 5M points
-  const size_t want = (n + 256 * 8 - 1) / (256 * 8);
-  return static_cast<int>(std::max<size_t>(1, std::min<size_t>(want, max_blocks)));
+int fdf_grid_blocks(size_t ns, int max_blocks) {
+  // persistent 4-wave blocks over the chunks; a wave takes at most 64 chunks (its lanes draw the
+  // tickets of its chunks at once)
+  const size_t nch = static_cast<size_t>(chunk_count(ns));
+  const size_t want = std::min<size_t>((nch + 3) / 4, static_cast<size_t>(std::max(max_blocks, 1)));
+  return static_cast<int>(std::max<size_t>({want, (nch + 255) / 256, 1}));
 }
 
 hipError_t launch_fitness(const GridView& tgt, const float4* src, size_t p0, size_t p1, Xf34 T,
@@ -1913,7 +2045,11 @@ hipError_t preload_kernels(void* pinned, size_t pinned_bytes, hipStream_t s) {
       reinterpret_cast<const void*>(&reduce_finish_kernel),
       reinterpret_cast<const void*>(&gn_moments_kernel),
       reinterpret_cast<const void*>(&publish_kernel),
-      reinterpret_cast<const void*>(&reduce_finish_moments_kernel),
+      reinterpret_cast<const void*>(&chunk_base_kernel),
+      reinterpret_cast<const void*>(&super_reduce_kernel<kRedVals>),
+      reinterpret_cast<const void*>(&super_reduce_kernel<kMomVals>),
+      reinterpret_cast<const void*>(&finish_supers_kernel<kRedVals>),
+      reinterpret_cast<const void*>(&finish_supers_kernel<kMomVals>),
       reinterpret_cast<const void*>(&finite_flags_kernel),
       reinterpret_cast<const void*>(&scatter_flagged_kernel),
       reinterpret_cast<const void*>(&segdiff_kernel),

@@ -317,6 +317,33 @@ class GICPEngine:
         self._check(self._lib.mgicp_debug_moments(self._h, _fp(_cm(T)), _dp(out)), "debug_moments")
         return out
 
+    def debug_supers(self, kind: str, arg) -> np.ndarray:
+        """This shard's super partials of one pass of the fixed reduction tree: kind "fdf" (arg = x),
+        "moments" (arg = T) or "fitness" (arg = (T, max_range)); shape (nsup_local, 16 or 80)."""
+        if kind == "fdf":
+            k, a, nv = 0, np.asarray(arg, np.float64), 16
+        elif kind == "moments":
+            k, a, nv = 1, np.asarray(_cm(arg), np.float64), 80
+        elif kind == "fitness":
+            T, max_range = arg
+            k, a, nv = 2, np.concatenate([np.asarray(_cm(T), np.float64), [float(max_range)]]), 16
+        else:
+            raise ValueError(kind)
+        cap = 1 << 16
+        out = np.zeros((cap, nv), np.float64)
+        n = self._check(self._lib.mgicp_debug_supers(self._h, k, _dp(np.ascontiguousarray(a)), _dp(out), cap),
+                        "debug_supers")
+        return out[:n].copy()
+
+    def debug_finish_supers(self, rows: np.ndarray, nsup: int, maxsup: int, nranks: int) -> np.ndarray:
+        """The multi-GPU finish: fixed-order total of nsup supers held as nranks rows of maxsup."""
+        rows = np.ascontiguousarray(rows, np.float64)
+        nv = rows.shape[-1]
+        out = np.zeros(nv, np.float64)
+        self._check(self._lib.mgicp_debug_finish_supers(self._h, nv, _dp(rows), nsup, maxsup, nranks, _dp(out)),
+                    "debug_finish_supers")
+        return out
+
     def kernel_times(self):
         nf = _lib.MGICP_KERNEL_FAMILIES
         ms = np.zeros(nf, np.float64)

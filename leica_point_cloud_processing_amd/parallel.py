@@ -1,7 +1,8 @@
 """Multi-GPU plumbing: one process per GPU, point-range shards of the source cloud.
 
-Data path: libmgicp.so all-reduces the 16 objective sums of every BFGS pass over RCCL (xGMI);
-the communicator is created from a 128-byte unique id (mgicp_get_unique_id / mgicp_comm_init).
+Data path: libmgicp.so all-gathers the ranks' super partials of every BFGS pass over RCCL (xGMI)
+and sums them in a fixed order, so N GPUs reproduce the single-GPU sums bit for bit; the
+communicator is created from a 128-byte unique id (mgicp_get_unique_id / mgicp_comm_init).
 
 Control path (this module): a tiny TCP rendezvous for the id broadcast, barriers and the
 max-over-ranks timer.  It deliberately does not use torch.distributed: importing torch loads
@@ -29,10 +30,36 @@ _T_NONE, _T_BYTES, _T_F64 = 0, 1, 2
 _MAX_FRAME = 1 << 20  # control messages are tiny (the unique id is 128 bytes)
 
 
+# The fixed reduction tree (csrc/mgicp_internal.hpp): chunks of CHUNK_PTS grid-sorted source
+# positions, supers of SUPER_CHUNKS chunks; shards start on super boundaries.
+CHUNK_PTS = 1024
+SUPER_CHUNKS = 32
+SUPER_PTS = CHUNK_PTS * SUPER_CHUNKS
+
+
+def super_first(rank: int, nsup: int, world: int) -> int:
+    """First super of `rank` (mirrors mgicp::super_first)."""
+    return nsup * rank // world
+
+
 def shard_range(n: int, world: int, rank: int) -> tuple[int, int]:
     """Source points [p0, p1) (grid-sorted order) owned by `rank` -- mirrors the engine's
-    mgicp_ctx::shard_p0/shard_p1 (contiguous, sizes differ by at most one)."""
-    return n * rank // world, n * (rank + 1) // world
+    mgicp_ctx::shard_p0/shard_p1: rank r owns supers [nsup * r / N, nsup * (r + 1) / N), so
+    shards are contiguous, start on super boundaries and differ by at most one super."""
+    nsup = -(-n // SUPER_PTS)
+    return (min(n, super_first(rank, nsup, world) * SUPER_PTS),
+            min(n, super_first(rank + 1, nsup, world) * SUPER_PTS))
+
+
+def combine_supers(rows, nsup: int, world: int):
+    """Host mirror of the multi-GPU finish's indexing: the supers of every rank (rows[r] = rank r's
+    supers, padded to a common length) in global order."""
+    out = []
+    for r in range(world):
+        cnt = super_first(r + 1, nsup, world) - super_first(r, nsup, world)
+        out.extend(rows[r][:cnt])
+    assert len(out) == nsup
+    return out
 
 
 def _secret_digest() -> bytes:

@@ -1,13 +1,14 @@
-"""N > 1 path: source point-range shards, target replicated, one all-reduce of
-the 16 objective sums per BFGS pass.
+"""N > 1 path: super-aligned source point-range shards, target covariances split
+and all-gathered, one all-gather of the super partials per BFGS pass and a fixed-order total --
+every N gives the single-GPU sums bit for bit.
 
-CPU (world_size 2):
-  * the decomposition itself -- per-shard partial sums of the oracle's objective all-reduced
-    over torch.distributed gloo equal the single-process sums;
+CPU (gloo, world_size 2 and 3):
+  * the decomposition itself -- the fixed tree over the oracle's objective, shards all-gathered
+    over torch.distributed gloo, is bit-identical to the single-process tree;
   * the TCP control plane bench.py uses (id broadcast, barrier, max-over-ranks timer).
-GPU (one device): two "detached" shard contexts (mgicp_comm_init(ctx, 2, r, NULL)) whose
-partial sums must add up to the unsharded context's -- the engine's shard bookkeeping
-(covariance ranges, correspondence ranges, pass ranges) without RCCL.
+GPU (one device): N = 2, 3, 4 "detached" shard contexts (mgicp_comm_init(ctx, N, r, NULL)) whose
+super partials (objective, GN moments, fitness) equal the unsharded context's bit for bit, and the
+multi-GPU finish over them reproduces the unsharded totals bit for bit.
 """
 import multiprocessing as mp
 import os
@@ -25,58 +26,86 @@ def _free_port():
     return p
 
 
+def _tree_sums(o, x, cpos, n, lo, hi):
+    """Chunk partials of chunks [lo, hi) (oracle sums over each chunk's correspondences), then
+    super partials (sequential in chunk order) -- the engine's fixed tree, emulated on the oracle."""
+    from leica_point_cloud_processing_amd.parallel import CHUNK_PTS, SUPER_CHUNKS
+
+    chunks = {j: np.asarray(o.fdf_sums(x, int(cpos[j * CHUNK_PTS]), int(cpos[min((j + 1) * CHUNK_PTS, n)])))
+              for j in range(lo, hi)}
+    sups = []
+    for s0 in range(lo, hi, SUPER_CHUNKS):
+        acc = chunks[s0].copy()
+        for j in range(s0 + 1, min(s0 + SUPER_CHUNKS, hi)):
+            acc = acc + chunks[j]
+        sups.append(acc)
+    return sups
+
+
+def _fixed_total(sups):
+    tot = np.zeros_like(sups[0])
+    for v in sups:  # any fixed order: the same function for every N
+        tot = tot + v
+    return tot
+
+
 def _gloo_worker(rank, world, port, q):
     import torch
     import torch.distributed as dist
 
     from leica_point_cloud_processing_amd import synth
-    from leica_point_cloud_processing_amd.parallel import shard_range
+    from leica_point_cloud_processing_amd.parallel import CHUNK_PTS, SUPER_PTS, combine_supers, shard_range
     from oracle import ref
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    scan, cad, _ = synth.scan_vs_cad(6000, 6000)
+    scan, cad, _ = synth.scan_vs_cad(140000, 60000)
     o = ref.RefGICP()
     o.set_source(scan)
     o.set_target(cad)
-    m, _, _, _ = o.correspondences(np.eye(4, dtype=np.float32))
+    m, tj, _, _ = o.correspondences(np.eye(4, dtype=np.float32))
+    n = len(scan)
+    cpos = np.concatenate([[0], np.cumsum(tj >= 0)])
     x = np.array([0.003, -0.002, 0.001, 0.001, -0.0005, 0.002])
-    c0, c1 = shard_range(m, world, rank)
-    part = torch.tensor(o.fdf_sums(x, c0, c1), dtype=torch.float64)
-    dist.all_reduce(part, op=dist.ReduceOp.SUM)
-    full = o.fdf_sums(x, 0, m)
-    f_ref, g_ref = o.fdf(x)
-    s = part.numpy()
-    f = s[0] / s[13]
-    # Gauss-Newton mode: one all-reduce of the 74 moments per outer iteration
-    T0 = np.eye(4, dtype=np.float32)
-    mom = torch.tensor(o.moments_range(T0, c0, c1), dtype=torch.float64)
-    dist.all_reduce(mom, op=dist.ReduceOp.SUM)
-    mfull = o.moments(T0)
-    rel_mom = max(float(np.abs(mom.numpy()[a:b] - mfull[a:b]).max() / np.abs(mfull[a:b]).max())
-                  for a, b in ((0, 1), (1, 13), (13, 74)))
-    q.put((rank, float(np.abs(s - full).max() / np.abs(full).max()), abs(f - f_ref) / abs(f_ref), int(s[13]), m,
-           rel_mom))
+    nsup = -(-n // SUPER_PTS)
+    p0, p1 = shard_range(n, world, rank)
+    mine = _tree_sums(o, x, cpos, n, p0 // CHUNK_PTS, -(-p1 // CHUNK_PTS)) if p1 > p0 else []
+    maxsup = -(-nsup // world)
+    rows = np.full((maxsup, 14), np.nan)  # padding is never read (the oracle reports 14 sums)
+    if mine:
+        rows[: len(mine)] = np.stack(mine)
+    parts = [torch.zeros(maxsup, 14, dtype=torch.float64) for _ in range(world)]
+    dist.all_gather(parts, torch.from_numpy(rows))
+    total = _fixed_total(combine_supers([p.numpy() for p in parts], nsup, world))
+    single = _fixed_total(_tree_sums(o, x, cpos, n, 0, -(-n // CHUNK_PTS)))
+    full = np.asarray(o.fdf_sums(x, 0, m))
+    q.put((rank, bool(np.array_equal(total, single)), float(np.abs(total - full).max() / np.abs(full).max()),
+           int(total[13]), m, (p0, p1)))
     dist.destroy_process_group()
 
 
-def test_sharded_objective_gloo_world2():
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_objective_gloo_bitwise_across_world(world):
+    """N ranks (gloo, CPU) each reduce their super-aligned shard with the fixed tree, all-gather the
+    supers and sum them in the fixed order: bit-identical to the single-process tree for N = 2, 3
+    (and within 1e-12 of the oracle's straight sum)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_gloo_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_gloo_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=240) for _ in procs]
+    res = sorted(q.get(timeout=300) for _ in procs)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, rel_sums, rel_f, cnt, m, rel_mom in res:
+    ranges = [r[5] for r in res]
+    assert ranges[0][0] == 0 and all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))
+    for rank, same, rel, cnt, m, _ in res:
+        assert same, rank
         assert cnt == m
-        assert rel_sums <= 1e-12
-        assert rel_f <= 1e-12
-        assert rel_mom <= 1e-12
+        assert rel <= 1e-12
 
 
 def _rdv_worker(rank, world, port, q):
@@ -166,56 +195,103 @@ def test_rendezvous_rejects_bogus_peers():
 
 
 def test_shard_ranges_partition():
-    from leica_point_cloud_processing_amd.parallel import shard_range
+    from leica_point_cloud_processing_amd.parallel import SUPER_PTS, shard_range
 
     for n in (0, 1, 7, 5_000_000, 20_000_001):
         for w in (1, 2, 3, 8):
             rs = [shard_range(n, w, r) for r in range(w)]
             assert rs[0][0] == 0 and rs[-1][1] == n
             assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
-            assert max(b - a for a, b in rs) - min(b - a for a, b in rs) <= 1
+            assert all(a % SUPER_PTS == 0 for a, _ in rs if a < n)  # super-aligned starts
+            assert max(b - a for a, b in rs) - min(b - a for a, b in rs) <= SUPER_PTS
+
+
+@pytest.fixture(scope="module")
+def five_supers():
+    from leica_point_cloud_processing_amd import synth
+
+    scan, cad, Ttrue = synth.scan_vs_cad(150000, 80000)  # 5 supers of 32768 source points
+    return scan, cad, Ttrue
 
 
 @pytest.mark.gpu
-def test_detached_shards_sum_to_full(part_small):
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_detached_shards_bitwise_equal_single(five_supers, world):
+    """N detached shards (mgicp_comm_init(ctx, N, r, NULL): the engine's shard bookkeeping without
+    RCCL) on one device: their correspondences and super partials -- objective pass, GN moments,
+    fitness -- are the unsharded context's bit for bit, and the multi-GPU finish over the padded
+    rows (padding = NaN, never read) gives the unsharded totals bit for bit."""
     from leica_point_cloud_processing_amd.engine import GICPEngine
+    from leica_point_cloud_processing_amd.parallel import SUPER_PTS, super_first
 
-    scan, cad, Ttrue = part_small
+    scan, cad, Ttrue = five_supers
     T = np.linalg.inv(Ttrue).astype(np.float32)
+    x = np.array([0.001, -0.002, 0.0005, 0.0003, -0.0002, 0.0004])
     full = GICPEngine()
     full.set_source_xyz(scan)
     full.set_target_xyz(cad)
-    m_full, tj_full, _ = full.debug_correspondences(T, len(scan))
-    x = np.array([0.001, -0.002, 0.0005, 0.0003, -0.0002, 0.0004])
-    s_full = full.debug_fdf_sums(x)
-    mom_full = full.debug_moments(T)
-    mom_total = np.zeros(80)
-    total = np.zeros(16)
+    m_full, tj_full, M_full = full.debug_correspondences(T, len(scan))
+    ref = {"fdf": full.debug_supers("fdf", x), "moments": full.debug_supers("moments", T),
+           "fitness": full.debug_supers("fitness", (T, 0.0))}
+    tot = {"fdf": full.debug_fdf_sums(x), "moments": full.debug_moments(T)}
+    nsup = -(-len(scan) // SUPER_PTS)
+    assert all(len(v) == nsup for v in ref.values())
+    maxsup = -(-nsup // world)
+    rows = {k: np.full((world, maxsup, v.shape[1]), np.nan) for k, v in ref.items()}
     tj = np.full(len(scan), -1, np.int32)
+    M = np.zeros_like(M_full)
     m_sum = 0
-    world = 3
     for r in range(world):
         e = GICPEngine()
         e.comm_init(world, r, None)
         e.set_source_xyz(scan)
         e.set_target_xyz(cad)
-        m_r, tj_r, _ = e.debug_correspondences(T, len(scan))
+        m_r, tj_r, M_r = e.debug_correspondences(T, len(scan))
         m_sum += m_r
         own = tj_r >= 0
         tj[own] = tj_r[own]
-        total += e.debug_fdf_sums(x)
-        mom_total += e.debug_moments(T)
+        M[own] = M_r[own]
+        for k in rows:
+            arg = x if k == "fdf" else (T if k == "moments" else (T, 0.0))
+            sup = e.debug_supers(k, arg)
+            a, b = super_first(r, nsup, world), super_first(r + 1, nsup, world)
+            assert len(sup) == b - a
+            np.testing.assert_array_equal(sup, ref[k][a:b], err_msg=f"{k} rank {r}")
+            rows[k][r, : b - a] = sup
         with pytest.raises(Exception):
             e.align()  # detached shards cannot run the collective path
         e.close()
     assert m_sum == m_full
     np.testing.assert_array_equal(tj, tj_full)
-    assert total[13] == s_full[13] == m_full
-    assert np.abs(total - s_full).max() <= 1e-11 * np.abs(s_full).max()
-    # Gauss-Newton mode: the shards' moments add up to the unsharded moment pass
-    assert mom_total[73] == mom_full[73] == m_full
-    for a, b in ((0, 1), (1, 13), (13, 73)):
-        assert np.abs(mom_total[a:b] - mom_full[a:b]).max() <= 1e-11 * np.abs(mom_full[a:b]).max()
+    np.testing.assert_array_equal(M, M_full)
+    np.testing.assert_array_equal(full.debug_finish_supers(rows["fdf"], nsup, maxsup, world), tot["fdf"])
+    np.testing.assert_array_equal(full.debug_finish_supers(rows["moments"], nsup, maxsup, world), tot["moments"])
+    fit = full.debug_finish_supers(rows["fitness"], nsup, maxsup, world)
+    assert fit[0] / fit[13] == full.fitness(T)
+    full.close()
+
+
+@pytest.mark.gpu
+def test_pass_sums_independent_of_direction_and_finish(part_small, monkeypatch):
+    """The fixed tree makes an objective pass's sums independent of the sweep direction (passes
+    alternate it) and of where the total is taken (in-launch vs the separate finish kernel)."""
+    from leica_point_cloud_processing_amd.engine import GICPEngine
+
+    scan, cad, Ttrue = part_small
+    T = np.linalg.inv(Ttrue).astype(np.float32)
+    x = np.array([0.001, -0.002, 0.0005, 0.0003, -0.0002, 0.0004])
+    res = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("MGICP_FUSED_FINISH", fused)
+        e = GICPEngine()
+        e.set_source_xyz(scan)
+        e.set_target_xyz(cad)
+        e.debug_correspondences(T, len(scan))
+        a, b = e.debug_fdf_sums(x), e.debug_fdf_sums(x)  # consecutive passes: opposite directions
+        np.testing.assert_array_equal(a, b)
+        res[fused] = a
+        e.close()
+    np.testing.assert_array_equal(res["0"], res["1"])
 
 
 @pytest.mark.gpu
