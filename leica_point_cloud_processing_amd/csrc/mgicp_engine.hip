@@ -241,10 +241,12 @@ struct mgicp_ctx {
   DevBuf<unsigned int> f_count;
   double occupancy = kDefaultOccupancy;  // grid cell sizing target (env MGICP_GRID_OCC)
   // objective-pass launch shape over the fixed reduction tree, A/B-measured on MI355X at 5M points
-  // (profiles/r02/ab_tree): 1024 persistent 4-wave blocks (4 waves per SIMD: chunk reductions and
-  // tickets overlap other waves' streaming) 68 us vs 75 us at 256 blocks; in-launch finish
+  // (profiles/r02/ab_tree): 512 persistent 4-wave blocks -- 2 waves per SIMD, so chunk reductions
+  // and tickets overlap other waves' streaming (71 us vs 76 us at 256 blocks), and the gated
+  // grid (134 VGPRs: 3 waves per SIMD) stays resident while it waits at the gate (14.5 ms per C4
+  // align vs 14.9 ms at 1024 blocks); in-launch finish
   bool fused_finish = true;              // in-launch reduction finish (env MGICP_FUSED_FINISH)
-  int fdf_max_blocks = 1024;             // objective-pass grid cap (env MGICP_FDF_BLOCKS)
+  int fdf_max_blocks = 512;              // objective-pass grid cap (env MGICP_FDF_BLOCKS)
   // alternate the objective-pass direction: 360 MB of streams at 5M points exceed the 256 MiB
   // Infinity Cache, so each pass re-reads the previous pass's tail from it (73 -> 68 us)
   bool alt_sweep = true;                 // (env MGICP_FDF_ALT)
