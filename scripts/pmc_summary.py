@@ -20,8 +20,9 @@ import os
 import sys
 
 STREAMING = {"fdf_soa_kernel"}
-KERNELS = ("fdf_soa_kernel", "correspond_kernel", "compact_kernel", "knn_cov_kernel", "fitness_kernel",
-           "gn_moments_kernel", "segdiff_kernel", "voxel_key_kernel", "voxel_centroid_kernel")
+KERNELS = ("fdf_soa_kernel", "correspond_kernel", "compact_kernel", "chunk_base_kernel", "knn_cov2_kernel",
+           "knn_cov_kernel", "fitness_kernel", "gn_moments_kernel", "segdiff_kernel", "voxel_key_kernel",
+           "voxel_centroid_kernel")
 
 
 def per_dispatch(directory, counter, kernel):
