@@ -177,6 +177,13 @@ int mgicp_debug_fdf(mgicp_ctx* ctx, const double x[6], double* f, double g6[6]);
  * NULL) (a "detached" shard, no RCCL) they cover rank r's source range only, so sharding can
  * be verified on one device; align/fitness refuse to run in that mode. */
 int mgicp_debug_fdf_sums(mgicp_ctx* ctx, const double x[6], double out16[16]);
+/* Objective-pass timing (bench.py's roofline leg): npasses passes at state x over the last
+ * correspondence sweep, back to back on the device, bracketed by HIP events on the context's
+ * stream.  mode 0: the resident pass server (one cooperative launch running all passes; the pass
+ * the aligns use on one GPU), mode 1: one fdf_soa_kernel launch per pass.  out_ms: average per
+ * pass; out16: the sums of the last pass (as mgicp_debug_fdf_sums).  Single-rank contexts only. */
+int mgicp_debug_pass_bench(mgicp_ctx* ctx, const double x[6], int npasses, int mode, double* out_ms,
+                           double out16[16]);
 /* MGICP_SOLVER_GN's moment pass at T (col-major) over the last correspondence sweep
  * (mgicp_debug_correspondences or an align): out80[0] sum r'Mr, [1..12] sum (Mr) w' (row-major
  * 3x4), [13..72] sum M_p (w w')_q (p: m00 m01 m02 m11 m12 m22; q: upper triangle of the 4x4

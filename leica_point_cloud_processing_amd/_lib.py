@@ -95,6 +95,7 @@ _SIGNATURES = {
     "mgicp_debug_correspondences_seeded": (ctypes.c_int, [_P, _FP, _IP, _DP]),
     "mgicp_debug_fdf": (ctypes.c_int, [_P, _DP, _DP, _DP]),
     "mgicp_debug_fdf_sums": (ctypes.c_int, [_P, _DP, _DP]),
+    "mgicp_debug_pass_bench": (ctypes.c_int, [_P, _DP, ctypes.c_int, ctypes.c_int, _DP, _DP]),
     "mgicp_debug_moments": (ctypes.c_int, [_P, _FP, _DP]),
     "mgicp_debug_supers": (ctypes.c_int, [_P, ctypes.c_int, _DP, _DP, ctypes.c_int]),
     "mgicp_debug_finish_supers": (ctypes.c_int, [_P, ctypes.c_int, _DP, ctypes.c_longlong, ctypes.c_longlong,

@@ -309,6 +309,20 @@ struct mgicp_ctx {
   std::vector<double> host_gt;             // 2 x 1024
   unsigned long long gated_seq = 0;     // sequence number of the queued gated pass (0 = none)
   unsigned long long gate_timeout = 0;  // wall_clock64 ticks a gated pass waits before giving up
+  // the resident pass server (env MGICP_RESIDENT, single-GPU polled mode): one cooperative launch per
+  // BFGS run keeps part of the compacted streams in registers / LDS across all its passes
+  bool resident = true;
+  bool srv_live = false;                // a server is running and waits for pass srv_next
+  unsigned long long srv_next = 0;
+  int cus = 0;                          // compute units (the server's grid)
+  unsigned long long* h_ptimes = nullptr;  // MGICP_PASS_TIMES=1: per pass gate exit / finish (wall clock)
+  unsigned long long* d_ptimes = nullptr;
+  // the server's super partials as stamped host rows (32 words per super; env MGICP_HOST_ROWS)
+  bool host_rows = true;
+  unsigned long long* h_rows = nullptr;
+  unsigned long long* d_rows = nullptr;
+  size_t rows_cap = 0;                  // supers
+  std::vector<double> row_sums;         // decoded super partials
   // build scratch
   DevBuf<uint32_t> counts, keys, keys_sorted, vals;
   DevBuf<unsigned char> scratch;
@@ -427,8 +441,17 @@ void publish_cmd(mgicp_ctx* ctx, unsigned long long seq, unsigned int op, int re
   for (int i = 0; i < kCmdWords; ++i) __atomic_store_n(&ctx->h_cmd->h[i], stamp | w[i], __ATOMIC_RELEASE);
 }
 
-// release a queued gated pass without running it (end of a BFGS run, any stream drain)
+// release a queued gated pass (or the resident server) without running it (end of a BFGS run,
+// any stream drain)
 void cancel_gated(mgicp_ctx* ctx) {
+  if (ctx->srv_live) {
+    publish_cmd(ctx, ctx->srv_next, kPassCancel, 0, nullptr);
+    ctx->pass_seq = std::max(ctx->pass_seq, ctx->srv_next);  // its sequence number is spent
+    ctx->srv_live = false;
+    // host-row passes leave the tickets as multiples of their supers' sizes: re-arm them for the
+    // launched passes (stream order: after the server has exited)
+    (void)hipMemsetAsync(ctx->tickets.p, 0, ctx->tickets_n * sizeof(unsigned int), ctx->stream);
+  }
   if (!ctx->gated_seq) return;
   publish_cmd(ctx, ctx->gated_seq, kPassCancel, 0, nullptr);
   ctx->pass_seq = std::max(ctx->pass_seq, ctx->gated_seq);  // its sequence number is spent
@@ -812,6 +835,12 @@ int ensure_host_red(mgicp_ctx* ctx) {
       if (const char* gp = std::getenv("MGICP_GATE_POLLERS")) ctx->gate_pollers = std::max(1, std::atoi(gp));
     }
     HIPCK(hipMemsetAsync(ctx->mail, 0, sizeof(PassCmd), ctx->stream));
+    if (const char* pt = std::getenv("MGICP_PASS_TIMES"); pt && std::atoi(pt)) {
+      HIPCK(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_ptimes), 2 * 1024 * sizeof(unsigned long long),
+                          hipHostMallocMapped | hipHostMallocCoherent));
+      HIPCK(hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->d_ptimes), ctx->h_ptimes, 0));
+      std::memset(ctx->h_ptimes, 0, 2 * 1024 * sizeof(unsigned long long));
+    }
     if (const char* gt = std::getenv("MGICP_GATE_TRACE"); gt && std::atoi(gt)) {
       HIPCK(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_gtrace), 4 * 1024 * sizeof(unsigned long long),
                           hipHostMallocMapped | hipHostMallocCoherent));
@@ -845,6 +874,59 @@ int wait_pass(mgicp_ctx* ctx, unsigned long long seq) {
   if (rc) return rc;
   if (__atomic_load_n(ctx->h_flag, __ATOMIC_ACQUIRE) != seq)
     return fail(ctx, MGICP_E_HIP, "objective pass finished without publishing its sums");
+  return MGICP_OK;
+}
+
+// Wait for the host rows of pass `seq` (every super's 32 stamped words), then take the total exactly
+// as wave_total / wave_sum would on one wave: lane l sums supers l, l + 64, ... in order from 0.0,
+// then the shuffle tree v[i] += v[i + off] for off = 32 ... 1 (lane 0's value)
+int wait_rows(mgicp_ctx* ctx, unsigned long long seq, long long nsup, double out[kRedVals]) {
+  const unsigned int st = static_cast<unsigned int>(seq);
+  ctx->row_sums.resize(static_cast<size_t>(nsup) * kRedVals);
+  const auto t0 = std::chrono::steady_clock::now();
+  for (long long r = 0; r < nsup; ++r) {
+    const unsigned long long* row = ctx->h_rows + 32 * r;
+    for (unsigned spins = 0;; ++spins) {
+      bool all = true;
+      for (int w = 0; w < 32 && all; ++w) all = static_cast<unsigned int>(__atomic_load_n(row + w, __ATOMIC_ACQUIRE) >> 32) == st;
+      if (all) break;
+      if ((spins & 1023u) == 1023u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(500)) {
+        int rc = sync(ctx);
+        if (rc) return rc;
+        return fail(ctx, MGICP_E_HIP, "objective pass finished without publishing its super rows");
+      }
+    }
+    for (int v = 0; v < kRedVals; ++v) {
+      const unsigned long long lo = __atomic_load_n(row + 2 * v, __ATOMIC_ACQUIRE) & 0xffffffffull;
+      const unsigned long long hi = __atomic_load_n(row + 2 * v + 1, __ATOMIC_ACQUIRE) & 0xffffffffull;
+      const unsigned long long bits = (hi << 32) | lo;
+      std::memcpy(&ctx->row_sums[static_cast<size_t>(r) * kRedVals + v], &bits, sizeof(double));
+    }
+  }
+  for (int v = 0; v < kRedVals; ++v) {
+    double lanes[64];
+    for (int l = 0; l < 64; ++l) {
+      double a = 0.0;
+      for (long long sg = l; sg < nsup; sg += 64) a += ctx->row_sums[static_cast<size_t>(sg) * kRedVals + v];
+      lanes[l] = a;
+    }
+    for (int off = 32; off > 0; off >>= 1)
+      for (int i = 0; i < off; ++i) lanes[i] = lanes[i] + lanes[i + off];
+    out[v] = lanes[0];
+  }
+  return MGICP_OK;
+}
+
+int ensure_rows(mgicp_ctx* ctx, long long nsup) {
+  if (ctx->h_rows && ctx->rows_cap >= static_cast<size_t>(nsup)) return MGICP_OK;
+  if (ctx->h_rows) HIPCK(hipHostFree(ctx->h_rows));
+  ctx->h_rows = nullptr;
+  const size_t cap = static_cast<size_t>(std::max<long long>(nsup, 64));
+  HIPCK(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_rows), cap * 32 * sizeof(unsigned long long),
+                      hipHostMallocMapped | hipHostMallocCoherent));
+  HIPCK(hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->d_rows), ctx->h_rows, 0));
+  std::memset(ctx->h_rows, 0, cap * 32 * sizeof(unsigned long long));
+  ctx->rows_cap = cap;
   return MGICP_OK;
 }
 
@@ -1022,6 +1104,31 @@ struct DeviceFunctor {
     const bool gate = ctx->gated && poll && inlaunch && !ctx->profiling;
     const Xf34 Ax = A.xf();
     const CorrSoA c = corr_soa(ctx);
+    const int nsrv = (gate && ctx->resident) ? fdf_server_blocks(ns, ctx->cus) : 0;
+    if (nsrv > 0) {
+      // the resident server runs every pass of this BFGS run: start it with the first one
+      const long long nsup = ctx->nsup_local();
+      if (!ctx->srv_live) {
+        cancel_gated(ctx);
+        if (ctx->host_rows && (rc = ensure_rows(ctx, nsup))) return rc;
+        HIPCK(hipMemsetAsync(ctx->tickets.p, 0, ctx->tickets_n * sizeof(unsigned int), ctx->stream));
+        ProfScope ps(ctx, kFamFdf);
+        HIPCK(launch_fdf_server(c, ctx->cpos.p, ctx->chunk_base.p, ns, ctx->partial.p, ctx->spart.p,
+                                ctx->tickets.p, out, ctx->d_flag, seq, ctx->d_cmd, ctx->mail, ctx->gate_timeout,
+                                ctx->d_ptimes, 0, Ax, ctx->host_rows ? ctx->d_rows : nullptr, nsrv, ctx->stream));
+        ctx->srv_live = true;
+      }
+      publish_cmd(ctx, seq, kPassRun, 0, &Ax);
+      ctx->srv_next = seq + 1;
+      if (ctx->host_rows) {
+        if ((rc = wait_rows(ctx, seq, nsup, sums))) return rc;
+      } else {
+        if ((rc = wait_pass(ctx, seq))) return rc;
+        std::memcpy(sums, ctx->h_red, kRedVals * sizeof(double));
+      }
+      ctx->n_evals++;
+      return MGICP_OK;
+    }
     if (ctx->gated_seq == seq) {
       // pass `seq` is already resident, waiting: hand it its state
       publish_cmd(ctx, seq, kPassRun, reverse, &Ax);
@@ -1266,6 +1373,8 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
   if (const char* fd = std::getenv("MGICP_FDF_DIAG")) ctx->fdf_diag = std::atoi(fd) & 6;
   if (const char* po = std::getenv("MGICP_POLL")) ctx->poll = std::atoi(po) != 0;
   if (const char* ga = std::getenv("MGICP_GATED")) ctx->gated = std::atoi(ga) != 0;
+  if (const char* rs = std::getenv("MGICP_RESIDENT")) ctx->resident = std::atoi(rs) != 0;
+  if (const char* hr = std::getenv("MGICP_HOST_ROWS")) ctx->host_rows = std::atoi(hr) != 0;
   ctx->knn_logged = knn_logged_enabled();
   if (const char* st = std::getenv("MGICP_SPLIT_TARGET_COV")) ctx->split_target_cov = std::atoi(st) != 0;
   if (const char* ps = std::getenv("MGICP_PROF_STRIDE")) ctx->prof_stride = std::max(1, std::atoi(ps));
@@ -1308,6 +1417,8 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
     delete ctx;
     return MGICP_E_HIP;
   }
+  if (hipDeviceGetAttribute(&ctx->cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess)
+    ctx->cus = 0;  // no resident server
   ctx->tgt.want_empty_map = true;  // correspondence / fitness queries start off the surface
   if (const char* em = std::getenv("MGICP_EMPTY_MAP")) ctx->tgt.want_empty_map = std::atoi(em) != 0;
   // per-cell point boxes in the 1-NN sweeps: exact and 1.75x fewer candidates in sweep 1, but the
@@ -1378,6 +1489,8 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   if (ctx->h_red) (void)hipHostFree(ctx->h_red);
   if (ctx->h_cmd) (void)hipHostFree(ctx->h_cmd);
   if (ctx->h_gtrace) (void)hipHostFree(ctx->h_gtrace);
+  if (ctx->h_ptimes) (void)hipHostFree(ctx->h_ptimes);
+  if (ctx->h_rows) (void)hipHostFree(ctx->h_rows);
   if (ctx->h_small) (void)hipHostFree(ctx->h_small);
   prof_resolve(ctx);
   for (hipEvent_t e : ctx->pool) (void)hipEventDestroy(e);
@@ -1486,6 +1599,22 @@ int mgicp_align(mgicp_ctx* ctx, const float guess_cm[16], float out_T_cm[16], mg
                    cnt, w / cnt, sp / cnt, hd / cnt);
     std::memset(ctx->h_gtrace, 0, 4 * 1024 * sizeof(unsigned long long));
     std::fill(ctx->host_gt.begin(), ctx->host_gt.end(), 0.0);
+  }
+  if (ctx->h_ptimes) {
+    // diagnostics of the resident server: per pass, block 0's gate exit -> the finishing wave
+    // (device active time) and the previous finish -> this gate exit (host turnaround + gate)
+    double act = 0, gap = 0;
+    int na = 0, ng = 0;
+    for (int i = 0; i < 1024; ++i) {
+      const unsigned long long* t = ctx->h_ptimes + 2 * i;
+      if (t[0] && t[1] && t[1] > t[0]) { act += (t[1] - t[0]) * 0.01; ++na; }
+      const unsigned long long* pv = ctx->h_ptimes + 2 * ((i + 1023) & 1023);
+      if (t[0] && pv[1] && t[0] > pv[1] && t[0] - pv[1] < 100000) { gap += (t[0] - pv[1]) * 0.01; ++ng; }
+    }
+    if (na)
+      std::fprintf(stderr, "[pass-times] passes %d | active %.2f us | finish -> next gate exit %.2f us (%d)\n", na,
+                   act / na, ng ? gap / ng : 0.0, ng);
+    std::memset(ctx->h_ptimes, 0, 2 * 1024 * sizeof(unsigned long long));
   }
   // final_transformation_ = previous_transformation_ (3x3) * guess (3x3); t = prev t + guess t
   Mat4 F = Mat4::identity();
@@ -1911,6 +2040,7 @@ int mgicp_debug_correspondences_seeded(mgicp_ctx* ctx, const float T_cm[16], int
 int mgicp_debug_fdf(mgicp_ctx* ctx, const double x[6], double* f, double g6[6]) {
   if (!ctx || !x || !ctx->have_corr) return MGICP_E_INVALID;
   HIPCK(hipSetDevice(ctx->device));
+  GateGuard guard{ctx};  // no queued pass / live server outlives the call
   DeviceFunctor fn{ctx};
   Vec6 xv, gv;
   for (int i = 0; i < 6; ++i) xv[i] = x[i];
@@ -1926,10 +2056,63 @@ int mgicp_debug_fdf(mgicp_ctx* ctx, const double x[6], double* f, double g6[6]) 
 int mgicp_debug_fdf_sums(mgicp_ctx* ctx, const double x[6], double out16[16]) {
   if (!ctx || !x || !out16 || !ctx->have_corr) return MGICP_E_INVALID;
   HIPCK(hipSetDevice(ctx->device));
+  GateGuard guard{ctx};
   DeviceFunctor fn{ctx};
   Vec6 xv;
   for (int i = 0; i < 6; ++i) xv[i] = x[i];
   return fn.pass(xv, out16);
+}
+
+int mgicp_debug_pass_bench(mgicp_ctx* ctx, const double x[6], int npasses, int mode, double* out_ms,
+                           double out16[16]) {
+  if (!ctx || !x || npasses < 1 || npasses > 100000 || (mode != 0 && mode != 1) || !ctx->have_corr)
+    return MGICP_E_INVALID;
+  if (ctx->comm || ctx->nranks != 1)
+    return fail(ctx, MGICP_E_INVALID, "pass bench: single-rank contexts only");
+  HIPCK(hipSetDevice(ctx->device));
+  int rc = sync(ctx);  // cancels any queued pass / live server
+  if (rc) return rc;
+  if ((rc = ensure_host_red(ctx))) return rc;
+  Vec6 xv;
+  for (int i = 0; i < 6; ++i) xv[i] = x[i];
+  const Xf34 A = apply_state(xv).xf();
+  const size_t ns = ctx->shard_p1() - ctx->shard_p0();
+  const CorrSoA c = corr_soa(ctx);
+  hipEvent_t a = nullptr, b = nullptr;
+  HIPCK(hipEventCreate(&a));
+  HIPCK(hipEventCreate(&b));
+  HIPCK(hipEventRecord(a, ctx->stream));
+  hipError_t e = hipSuccess;
+  if (mode == 0) {
+    const int nb = fdf_server_blocks(ns, ctx->cus);
+    if (nb <= 0) {
+      (void)hipEventDestroy(a);
+      (void)hipEventDestroy(b);
+      return fail(ctx, MGICP_E_INVALID, "pass bench: shard not servable by the resident server");
+    }
+    const unsigned long long seq0 = ++ctx->pass_seq;
+    e = launch_fdf_server(c, ctx->cpos.p, ctx->chunk_base.p, ns, ctx->partial.p, ctx->spart.p, ctx->tickets.p,
+                          ctx->d_h_red, ctx->d_flag, seq0, ctx->d_cmd, ctx->mail, ctx->gate_timeout, ctx->d_ptimes,
+                          npasses, A, nullptr, nb, ctx->stream);
+    ctx->pass_seq = seq0 + static_cast<unsigned long long>(npasses);  // the closing cancel's stamp too
+  } else {
+    const int nb = fdf_grid_blocks(ns, ctx->fdf_max_blocks);
+    for (int k = 0; k < npasses && e == hipSuccess; ++k)
+      e = launch_fdf_soa(c, ctx->cpos.p, ctx->chunk_base.p, ns, A, ctx->partial.p, ctx->spart.p, nb, ctx->tickets.p,
+                         ctx->d_h_red, ctx->alt_sweep ? (k & 1) : 0, ctx->d_flag, ++ctx->pass_seq, ctx->stream);
+  }
+  if (e == hipSuccess) e = hipEventRecord(b, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  float ms = 0.f;
+  if (e == hipSuccess) e = hipEventElapsedTime(&ms, a, b);
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  HIPCK(e);
+  if (__atomic_load_n(ctx->h_flag, __ATOMIC_ACQUIRE) != ctx->pass_seq - (mode == 0 ? 1 : 0))
+    return fail(ctx, MGICP_E_HIP, "pass bench: the last pass did not publish its sums");
+  if (out_ms) *out_ms = static_cast<double>(ms) / npasses;
+  if (out16) std::memcpy(out16, ctx->h_red, kRedVals * sizeof(double));
+  return MGICP_OK;
 }
 
 int mgicp_debug_moments(mgicp_ctx* ctx, const float T_cm[16], double out80[80]) {

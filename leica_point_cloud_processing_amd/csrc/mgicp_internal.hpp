@@ -152,6 +152,19 @@ hipError_t launch_fdf_soa_gated(const CorrSoA& c, const uint32_t* pos, const uin
                                 unsigned long long* gtrace /*nullable: diagnostics*/,
                                 int host_pollers /*blocks [0, host_pollers) poll the host copy*/, hipStream_t s);
 int        fdf_grid_blocks(size_t ns, int max_blocks = 2048);
+// the resident pass server (one cooperative launch per BFGS run, see mgicp_kernels.hip): passes
+// seq0, seq0 + 1, ... each run on the command with that stamp, until a cancel; bench_passes > 0
+// (timing): that many passes of A back to back without commands.  fdf_server_blocks: its grid for a
+// shard of ns positions on `cus` CUs (0: not servable, use the launched passes)
+int        fdf_server_blocks(size_t ns, int cus);
+hipError_t launch_fdf_server(const CorrSoA& c, const uint32_t* pos, const uint32_t* base, size_t ns, double* partial,
+                             double* spart, unsigned int* tickets, double* out, unsigned long long* done_flag,
+                             unsigned long long seq0, const PassCmd* cmd, PassCmd* mail,
+                             unsigned long long timeout_ticks, unsigned long long* ptimes /*nullable*/,
+                             int bench_passes, Xf34 A,
+                             unsigned long long* host_rows /*nullable: super rows to the host*/, int nb,
+                             hipStream_t s);
+
 // super partials of nch chunk partials of nv (kRedVals or kMomVals) values
 hipError_t launch_super_reduce(const double* chunk, int nch, int nv, double* sup, hipStream_t s);
 // totals of nsup supers held as nranks rows of maxsup (row r: rank r's supers, from super_first(r))

@@ -1193,6 +1193,201 @@ __device__ __forceinline__ void fdf_point(const Xf34& A, float sx, float sy, flo
   acc[10] += dz * t0; acc[11] += dz * t1; acc[12] += dz * t2;
 }
 
+// 4 consecutive correspondences of the compacted streams (one 16-byte load per stream and lane):
+// f = sx sy sz qx qy qz (float4 of 4 coordinates), d = m00 m00' m01 m01' m02 m02' m11 m11' m12 m12'
+// m22 m22' (double2 of 2 matrix entries) -- 72 dwords
+struct CorrGroup {
+  float4 f[6];
+  double2 d[12];
+};
+
+__device__ __forceinline__ void load_group(const CorrSoA& c, uint32_t i, CorrGroup& g) {
+  g.f[0] = reinterpret_cast<const float4*>(c.sx)[i];
+  g.f[1] = reinterpret_cast<const float4*>(c.sy)[i];
+  g.f[2] = reinterpret_cast<const float4*>(c.sz)[i];
+  g.f[3] = reinterpret_cast<const float4*>(c.qx)[i];
+  g.f[4] = reinterpret_cast<const float4*>(c.qy)[i];
+  g.f[5] = reinterpret_cast<const float4*>(c.qz)[i];
+  const size_t i2 = 2 * static_cast<size_t>(i);
+  const double* const m[6] = {c.m00, c.m01, c.m02, c.m11, c.m12, c.m22};
+#pragma unroll
+  for (int e = 0; e < 6; ++e) {
+    const double2* M = reinterpret_cast<const double2*>(m[e]) + i2;
+    g.d[2 * e] = M[0];
+    g.d[2 * e + 1] = M[1];
+  }
+}
+
+// the group's 4 correspondences in stream order
+__device__ __forceinline__ void fdf_group(const Xf34& A, const CorrGroup& g, double (&acc)[kRedVals]) {
+  fdf_point(A, g.f[0].x, g.f[1].x, g.f[2].x, g.f[3].x, g.f[4].x, g.f[5].x, g.d[0].x, g.d[2].x, g.d[4].x,
+            g.d[6].x, g.d[8].x, g.d[10].x, acc);
+  fdf_point(A, g.f[0].y, g.f[1].y, g.f[2].y, g.f[3].y, g.f[4].y, g.f[5].y, g.d[0].y, g.d[2].y, g.d[4].y,
+            g.d[6].y, g.d[8].y, g.d[10].y, acc);
+  fdf_point(A, g.f[0].z, g.f[1].z, g.f[2].z, g.f[3].z, g.f[4].z, g.f[5].z, g.d[1].x, g.d[3].x, g.d[5].x,
+            g.d[7].x, g.d[9].x, g.d[11].x, acc);
+  fdf_point(A, g.f[0].w, g.f[1].w, g.f[2].w, g.f[3].w, g.f[4].w, g.f[5].w, g.d[1].y, g.d[3].y, g.d[5].y,
+            g.d[7].y, g.d[9].y, g.d[11].y, acc);
+}
+
+// The gate of a pass whose state is not known at launch (pre-launched gated passes and the
+// resident pass server).  Every block's thread 0 polls a command block until it carries this
+// pass's sequence number: blocks [0, host_pollers) the host-written copy (pinned, mapped,
+// system-coherent loads), the others the device mailbox block 0 forwards it to.  Returns false on a
+// cancel command or after `timeout` wall-clock ticks (every wave reaches an exit).
+__device__ __forceinline__ bool pass_gate(unsigned long long seq, const PassCmd* cmd, PassCmd* mail,
+                                          unsigned long long timeout, unsigned long long* gtrace,
+                                          int host_pollers, Xf34& A, int& reverse) {
+  __shared__ unsigned int sw[kCmdWords];
+  __shared__ int sok;
+  __syncthreads();  // sw / sok of the previous gate of this block are consumed
+  if (threadIdx.x == 0) {
+    // block 0 alone polls the host's command block over PCIe (256 pollers of host memory were
+    // measured to delay the command by ~320 us) and forwards it to the device mailbox the
+    // other blocks poll; both blocks are read whole (8 x 16 B per poll) and validated by stamp
+    const bool host_poller = blockIdx.x < host_pollers;
+    const unsigned int stamp = static_cast<unsigned int>(seq);
+    const unsigned long long t0 = wall_clock64();
+    unsigned long long v[16];
+    bool got = false;
+    for (;;) {
+      if (host_poller) read_cmd<true>(cmd, v);
+      else read_cmd<false>(mail, v);
+      bool all = true;
+#pragma unroll
+      for (int i = 0; i < kCmdWords; ++i) all = all && static_cast<unsigned int>(v[i] >> 32) == stamp;
+      if (all) { got = true; break; }
+      if (wall_clock64() - t0 > timeout) break;  // no command: give up as if cancelled
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (gtrace && host_poller) {  // diagnostics: kernel start and command seen (wall clock)
+      gtrace[4 * (seq & 1023)] = t0;
+      gtrace[4 * (seq & 1023) + 1] = wall_clock64();
+    }
+    if (!got) {  // a timeout forwards a cancel, so every block exits promptly
+#pragma unroll
+      for (int i = 0; i < kCmdWords; ++i) v[i] = (static_cast<unsigned long long>(stamp) << 32) | (i == 12 ? kPassCancel : 0u);
+    }
+#pragma unroll
+    for (int i = 0; i < kCmdWords; ++i) sw[i] = static_cast<unsigned int>(v[i]);
+    if (blockIdx.x == 0 && host_pollers > 0 && host_pollers < static_cast<int>(gridDim.x)) write_mail(mail, v);
+    sok = got ? 1 : 0;
+  }
+  __syncthreads();
+  if (gtrace && threadIdx.x == 0)  // diagnostics: the latest block to pass the gate
+    atomicMax(&gtrace[4 * (seq & 1023) + 2], wall_clock64());
+  if (!sok || sw[12] != kPassRun) return false;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) A.m[i] = __uint_as_float(sw[i]);
+  reverse = static_cast<int>(sw[13]);
+  return true;
+}
+
+// chunk j's partial (wave_sum's shuffle tree of the lanes' in-order sums) and its exact count from
+// the scan (pad slots are not counted), stored write-through (sc1)
+__device__ __forceinline__ void chunk_store(int j, double (&acc)[kRedVals], const uint32_t* __restrict__ pos,
+                                            size_t ns, double* __restrict__ partial, int lane) {
+  const size_t e = min(static_cast<size_t>(j + 1) * kChunkPts, ns);
+  const double cnt = static_cast<double>(pos[e] - pos[static_cast<size_t>(j) * kChunkPts]);
+#pragma unroll
+  for (int v = 0; v < 13; ++v) acc[v] = wave_sum(acc[v]);
+  double* pj = partial + static_cast<size_t>(j) * kRedVals;
+  if (lane == 0) {
+#pragma unroll
+    for (int v = 0; v < 13; ++v) st_sc1(pj + v, acc[v]);
+    st_sc1(pj + 13, cnt);
+    st_sc1(pj + 14, 0.0);
+    st_sc1(pj + 15, 0.0);
+  }
+}
+
+// After a wave stored all its chunk partials (chunks w0, w0 + nw, ...; reverse & 1: counted from
+// the back): tickets, the supers it completes, and -- for the wave completing the last super -- the
+// total into `out` and `seq` into done_flag.  Returns true on that finishing wave.
+// host_rows (nullable, mapped host memory, 32 words per super): each super partial goes straight to
+// the host as one 256-byte store of stamped halves ((seq << 32) | 32-bit half, value v in words 2v
+// (low) and 2v + 1 (high)); the host takes the total in wave_total's order, so there is no global
+// ticket, device total or completion flag on the pass's critical path (returns false).
+__device__ __forceinline__ bool wave_tickets(int w0, int nw, int nch, int reverse, unsigned int* __restrict__ tickets,
+                                             const double* __restrict__ partial, double* __restrict__ spart,
+                                             double* __restrict__ out, unsigned long long* done_flag,
+                                             unsigned long long seq, int lane,
+                                             unsigned long long* host_rows = nullptr) {
+  const int nsup = (nch + kSuperChunks - 1) / kSuperChunks;
+  // tickets, once per wave after all of its chunks (a per-chunk drain + atomic round trip cost
+  // ~60 us per pass at 256 blocks): lane k takes the super of the wave's k-th chunk
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int nmine = (nch - w0 + nw - 1) / nw;  // <= 64: the grid has >= nch / 64 waves
+  int last = 0;
+  if (lane < nmine) {
+    const int w = w0 + lane * nw;
+    const int j = (reverse & 1) ? nch - 1 - w : w;
+    const int sj = j / kSuperChunks, nin = min(kSuperChunks, nch - sj * kSuperChunks);
+    const unsigned old = __hip_atomic_fetch_add(tickets + sj, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // host-row mode never re-arms a ticket (a reset racing the host's next command is avoided by
+    // construction): every pass adds exactly nin to each super's counter, zeroed at server launch
+    last = (host_rows ? old % static_cast<unsigned>(nin) : old) == static_cast<unsigned>(nin - 1) ? 1 : 0;
+  }
+  unsigned long long done = __ballot(last);
+  bool fin = false;
+  while (done) {
+    // this wave completed super sj: its partial (chunk order), then the global ticket
+    const int k = __builtin_ctzll(done);
+    done &= done - 1;
+    const int w = w0 + k * nw;
+    const int j = (reverse & 1) ? nch - 1 - w : w;
+    const int sj = j / kSuperChunks, cfirst = sj * kSuperChunks, nin = min(kSuperChunks, nch - cfirst);
+    double a = 0.0;
+    if (lane < kRedVals) {
+      // all kSuperChunks loads in flight at once (a runtime-bounded loop issued them one round
+      // trip at a time), then the chunk-order sum
+      double t[kSuperChunks];
+#pragma unroll
+      for (int q = 0; q < kSuperChunks; ++q)
+        t[q] = ld_sc1(partial + static_cast<size_t>(cfirst + min(q, nin - 1)) * kRedVals + lane);
+      a = t[0];
+#pragma unroll
+      for (int q = 1; q < kSuperChunks; ++q)
+        if (q < nin) a = a + t[q];
+      if (!host_rows) st_sc1(spart + static_cast<size_t>(sj) * kRedVals + lane, a);
+    }
+    if (host_rows) {
+      // lane l < 32: half l & 1 of value l >> 1, stamped; one 256-byte store per super
+      const long long bits = __double_as_longlong(__shfl(a, lane >> 1, 64));
+      const unsigned int half = static_cast<unsigned int>((lane & 1) ? (bits >> 32) : bits);
+      // system-coherent write-through (sc0 sc1): a plain store to mapped host memory may sit in the
+      // L2 until something releases it; the 32 lanes' 8-byte words leave as one 256-byte burst
+      if (lane < 32) {
+        const unsigned long long w = (static_cast<unsigned long long>(static_cast<unsigned int>(seq)) << 32) | half;
+        asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1" ::"v"(host_rows + static_cast<size_t>(sj) * 32 + lane),
+                     "v"(w)
+                     : "memory");
+      }
+      continue;
+    }
+    int lastg = 0;
+    if (lane == 0) {
+      __hip_atomic_store(tickets + sj, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lastg = __hip_atomic_fetch_add(tickets + nsup, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                      static_cast<unsigned>(nsup - 1) ? 1 : 0;
+    }
+    if (!__shfl(lastg, 0, 64)) continue;
+    // every super is stored: the total (single rank; with out == nullptr the supers are the result)
+    if (out) wave_total<kRedVals, true>(spart, nsup, nsup, 1, 0, out);
+    fin = true;
+    if (lane == 0) {
+      __hip_atomic_store(tickets + nsup, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (done_flag && out) {
+        // lane 0 wrote every out[v]; once they are drained, publish the pass number to the host
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(done_flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  }
+  return fin;
+}
+
 // Objective pass over the compacted streams: 4 correspondences per thread-iteration, every load
 // 16 bytes per lane (float4 of 4 coordinates, double2 of 2 matrix entries).
 // kGated (fdf_soa_gated_kernel): the pass is launched BEFORE the host knows its state.  Every
@@ -1211,53 +1406,12 @@ __device__ __forceinline__ void fdf_soa_body(CorrSoA c, const uint32_t* __restri
                                              unsigned long long timeout, unsigned long long* gtrace,
                                              int host_pollers) {
   if constexpr (kGated) {
-    __shared__ unsigned int sw[kCmdWords];
-    __shared__ int sok;
-    if (threadIdx.x == 0) {
-      // block 0 alone polls the host's command block over PCIe (256 pollers of host memory were
-      // measured to delay the command by ~320 us) and forwards it to the device mailbox the
-      // other blocks poll; both blocks are read whole (8 x 16 B per poll) and validated by stamp
-      const bool host_poller = blockIdx.x < host_pollers;
-      const unsigned int stamp = static_cast<unsigned int>(seq);
-      const unsigned long long t0 = wall_clock64();
-      unsigned long long v[16];
-      bool got = false;
-      for (;;) {
-        if (host_poller) read_cmd<true>(cmd, v);
-        else read_cmd<false>(mail, v);
-        bool all = true;
-#pragma unroll
-        for (int i = 0; i < kCmdWords; ++i) all = all && static_cast<unsigned int>(v[i] >> 32) == stamp;
-        if (all) { got = true; break; }
-        if (wall_clock64() - t0 > timeout) break;  // no command: give up as if cancelled
-        __builtin_amdgcn_s_sleep(1);
-      }
-      if (gtrace && host_poller) {  // diagnostics: kernel start and command seen (wall clock)
-        gtrace[4 * (seq & 1023)] = t0;
-        gtrace[4 * (seq & 1023) + 1] = wall_clock64();
-      }
-      if (!got) {  // a timeout forwards a cancel, so every block exits promptly
-#pragma unroll
-        for (int i = 0; i < kCmdWords; ++i) v[i] = (static_cast<unsigned long long>(stamp) << 32) | (i == 12 ? kPassCancel : 0u);
-      }
-#pragma unroll
-      for (int i = 0; i < kCmdWords; ++i) sw[i] = static_cast<unsigned int>(v[i]);
-      if (blockIdx.x == 0 && host_pollers < static_cast<int>(gridDim.x)) write_mail(mail, v);
-      sok = got ? 1 : 0;
-    }
-    __syncthreads();
-    if (gtrace && threadIdx.x == 0)  // diagnostics: the latest block to pass the gate
-      atomicMax(&gtrace[4 * (seq & 1023) + 2], wall_clock64());
-    if (!sok || sw[12] != kPassRun) return;
-#pragma unroll
-    for (int i = 0; i < 12; ++i) A.m[i] = __uint_as_float(sw[i]);
-    reverse = static_cast<int>(sw[13]);
+    if (!pass_gate(seq, cmd, mail, timeout, gtrace, host_pollers, A, reverse)) return;
   }
   // persistent waves over the shard's chunks (reverse: back to front, so the tail of the previous
   // pass, still in the 256 MiB Infinity Cache, is consumed first)
   const int lane = threadIdx.x & 63;
   const int nw = gridDim.x * (blockDim.x >> 6);
-  const int nsup = (nch + kSuperChunks - 1) / kSuperChunks;
   const int w0 = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
   for (int w = w0; w < nch; w += nw) {
     const int j = (reverse & 1) ? nch - 1 - w : w;
@@ -1266,98 +1420,149 @@ __device__ __forceinline__ void fdf_soa_body(CorrSoA c, const uint32_t* __restri
     for (int v = 0; v < kRedVals; ++v) acc[v] = 0.0;
     const uint32_t g1 = base[j + 1] >> 2;
     for (uint32_t i = (base[j] >> 2) + lane; i < g1; i += 64) {
-      const float4 sx = reinterpret_cast<const float4*>(c.sx)[i];
-      const float4 sy = reinterpret_cast<const float4*>(c.sy)[i];
-      const float4 sz = reinterpret_cast<const float4*>(c.sz)[i];
-      const float4 qx = reinterpret_cast<const float4*>(c.qx)[i];
-      const float4 qy = reinterpret_cast<const float4*>(c.qy)[i];
-      const float4 qz = reinterpret_cast<const float4*>(c.qz)[i];
-      const double2* M00 = reinterpret_cast<const double2*>(c.m00) + 2 * static_cast<size_t>(i);
-      const double2* M01 = reinterpret_cast<const double2*>(c.m01) + 2 * static_cast<size_t>(i);
-      const double2* M02 = reinterpret_cast<const double2*>(c.m02) + 2 * static_cast<size_t>(i);
-      const double2* M11 = reinterpret_cast<const double2*>(c.m11) + 2 * static_cast<size_t>(i);
-      const double2* M12 = reinterpret_cast<const double2*>(c.m12) + 2 * static_cast<size_t>(i);
-      const double2* M22 = reinterpret_cast<const double2*>(c.m22) + 2 * static_cast<size_t>(i);
-      const double2 a0 = M00[0], a1 = M00[1], b0 = M01[0], b1 = M01[1], e0 = M02[0], e1 = M02[1];
-      const double2 f0 = M11[0], f1 = M11[1], g0 = M12[0], g1v = M12[1], h0 = M22[0], h1 = M22[1];
-      fdf_point(A, sx.x, sy.x, sz.x, qx.x, qy.x, qz.x, a0.x, b0.x, e0.x, f0.x, g0.x, h0.x, acc);
-      fdf_point(A, sx.y, sy.y, sz.y, qx.y, qy.y, qz.y, a0.y, b0.y, e0.y, f0.y, g0.y, h0.y, acc);
-      fdf_point(A, sx.z, sy.z, sz.z, qx.z, qy.z, qz.z, a1.x, b1.x, e1.x, f1.x, g1v.x, h1.x, acc);
-      fdf_point(A, sx.w, sy.w, sz.w, qx.w, qy.w, qz.w, a1.y, b1.y, e1.y, f1.y, g1v.y, h1.y, acc);
+      CorrGroup g;
+      load_group(c, i, g);
+      fdf_group(A, g, acc);
     }
     if (reverse & 2) {  // timing diagnostics only (MGICP_FDF_DIAG): stream, no reduction
       if (acc[0] == 12345.0) partial[j] = acc[1];
       continue;
     }
-    // chunk partial; the count is exact from the scan (pad slots are not counted)
-    const size_t e = min(static_cast<size_t>(j + 1) * kChunkPts, ns);
-    const double cnt = static_cast<double>(pos[e] - pos[static_cast<size_t>(j) * kChunkPts]);
-#pragma unroll
-    for (int v = 0; v < 13; ++v) acc[v] = wave_sum(acc[v]);
-    double* pj = partial + static_cast<size_t>(j) * kRedVals;
     if (reverse & 4) {  // timing diagnostics only: chunk partials, no tickets
+#pragma unroll
+      for (int v = 0; v < 13; ++v) acc[v] = wave_sum(acc[v]);
       if (lane == 0)
-        for (int v = 0; v < 13; ++v) pj[v] = acc[v];
+        for (int v = 0; v < 13; ++v) partial[static_cast<size_t>(j) * kRedVals + v] = acc[v];
       continue;
     }
-    if (lane == 0) {
-#pragma unroll
-      for (int v = 0; v < 13; ++v) st_sc1(pj + v, acc[v]);
-      st_sc1(pj + 13, cnt);
-      st_sc1(pj + 14, 0.0);
-      st_sc1(pj + 15, 0.0);
-    }
+    chunk_store(j, acc, pos, ns, partial, lane);
   }
   if (w0 >= nch || (reverse & 6)) return;
-  // tickets, once per wave after all of its chunks (a per-chunk drain + atomic round trip cost
-  // ~60 us per pass at 256 blocks): lane k takes the super of the wave's k-th chunk
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const int nmine = (nch - w0 + nw - 1) / nw;  // <= 64: the grid has >= nch / 64 waves
-  int last = 0;
-  if (lane < nmine) {
-    const int w = w0 + lane * nw;
-    const int j = (reverse & 1) ? nch - 1 - w : w;
-    const int sj = j / kSuperChunks, nin = min(kSuperChunks, nch - sj * kSuperChunks);
-    last = __hip_atomic_fetch_add(tickets + sj, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                   static_cast<unsigned>(nin - 1) ? 1 : 0;
+  wave_tickets(w0, nw, nch, reverse, tickets, partial, spart, out, done_flag, seq, lane);
+}
+
+// ---- the resident pass server --------------------------------------------------------------
+// All objective passes of one BFGS run read the SAME compacted streams (72 B per correspondence,
+// 360 MB at C4).  The server is ONE cooperative launch per BFGS run with one 4-wave block per CU
+// (1 wave per SIMD, up to 512 VGPR+AGPR per lane): each wave keeps its first chunk (4 groups per
+// lane, 288 dwords) in registers and half of its second chunk (2 groups per lane, 36 KiB per wave,
+// 144 KiB per CU) in LDS for the whole run, and streams only the rest from HBM / Infinity Cache.
+// Between passes every block waits at the gate for the host's next command (pass_gate); the
+// chunk -> wave assignment, the lanes' element order and the reduction tree are those of
+// fdf_soa_body with reverse = 0, so every pass gives bit-identical sums.  bench_passes > 0 (timing
+// only): run that many passes of state A back to back, the finishing wave forwarding the next
+// command itself.  ptimes (nullable): per pass, block 0's gate exit and the finish (wall clock).
+// A/B (profiles/r02/ab_server): the 31 % of the bytes this keeps on chip buy less than expected,
+// because one wave per SIMD keeps few loads in flight; software-pipelining the streamed groups in
+// registers (2-3 resident groups, spills) or through an LDS-DMA ring (3 resident groups) measured
+// 67-77 us per pass against ~65 us for this form and ~66-70 us for launched passes.
+constexpr int kSrvRegGroups = 4;  // = one full chunk: kChunkPts / 4 / 64
+constexpr int kSrvLdsGroups = 2;
+constexpr int kSrvWaves = 4;
+
+__global__ __launch_bounds__(256, 1) void fdf_server_kernel(
+    CorrSoA c, const uint32_t* __restrict__ pos, const uint32_t* __restrict__ base, size_t ns, int nch,
+    double* __restrict__ partial, double* __restrict__ spart, unsigned int* __restrict__ tickets,
+    double* __restrict__ out, unsigned long long* done_flag, unsigned long long seq0, const PassCmd* cmd,
+    PassCmd* mail, unsigned long long timeout, unsigned long long* ptimes, int bench_passes, Xf34 Abench,
+    unsigned long long* host_rows) {
+  __shared__ float4 lf[kSrvWaves][kSrvLdsGroups][6][64];
+  __shared__ double2 ld[kSrvWaves][kSrvLdsGroups][12][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nw = gridDim.x * kSrvWaves;
+  const int w0 = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x * kSrvWaves + wid));
+  // resident data: chunk w0 in registers, groups 0..kSrvLdsGroups-1 of chunk w0 + nw in LDS (each
+  // lane reads back only its own slots, so no barrier is needed)
+  CorrGroup R[kSrvRegGroups];
+  uint32_t rb = 0, re = 0, lb = 0, le = 0;
+  if (w0 < nch) {
+    rb = base[w0] >> 2;
+    re = base[w0 + 1] >> 2;
   }
-  unsigned long long done = __ballot(last);
-  while (done) {
-    // this wave completed super sj: its partial (chunk order), then the global ticket
-    const int k = __builtin_ctzll(done);
-    done &= done - 1;
-    const int w = w0 + k * nw;
-    const int j = (reverse & 1) ? nch - 1 - w : w;
-    const int sj = j / kSuperChunks, cfirst = sj * kSuperChunks, nin = min(kSuperChunks, nch - cfirst);
-    if (lane < kRedVals) {
-      // all kSuperChunks loads in flight at once (a runtime-bounded loop issued them one round
-      // trip at a time), then the chunk-order sum
-      double t[kSuperChunks];
 #pragma unroll
-      for (int q = 0; q < kSuperChunks; ++q)
-        t[q] = ld_sc1(partial + static_cast<size_t>(cfirst + min(q, nin - 1)) * kRedVals + lane);
-      double a = t[0];
+  for (int k = 0; k < kSrvRegGroups; ++k)
+    if (rb + lane + 64 * k < re) load_group(c, rb + lane + 64 * k, R[k]);
+  const int w1 = w0 + nw;
+  if (w1 < nch) {
+    lb = base[w1] >> 2;
+    le = base[w1 + 1] >> 2;
+  }
 #pragma unroll
-      for (int q = 1; q < kSuperChunks; ++q)
-        if (q < nin) a = a + t[q];
-      st_sc1(spart + static_cast<size_t>(sj) * kRedVals + lane, a);
+  for (int k = 0; k < kSrvLdsGroups; ++k) {
+    if (lb + lane + 64 * k < le) {
+      CorrGroup g;
+      load_group(c, lb + lane + 64 * k, g);
+#pragma unroll
+      for (int q = 0; q < 6; ++q) lf[wid][k][q][lane] = g.f[q];
+#pragma unroll
+      for (int q = 0; q < 12; ++q) ld[wid][k][q][lane] = g.d[q];
     }
-    int lastg = 0;
-    if (lane == 0) {
-      __hip_atomic_store(tickets + sj, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      lastg = __hip_atomic_fetch_add(tickets + nsup, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                      static_cast<unsigned>(nsup - 1) ? 1 : 0;
+  }
+  const int host_pollers = bench_passes > 0 ? 0 : 1;
+  for (unsigned long long seq = seq0;; ++seq) {
+    Xf34 A = Abench;
+    int rev = 0;
+    if (!(bench_passes > 0 && seq == seq0) && !pass_gate(seq, cmd, mail, timeout, nullptr, host_pollers, A, rev))
+      return;
+    if (ptimes && blockIdx.x == 0 && threadIdx.x == 0) ptimes[2 * (seq & 1023)] = wall_clock64();
+    if (w0 < nch) {
+      double acc[kRedVals];
+#pragma unroll
+      for (int v = 0; v < kRedVals; ++v) acc[v] = 0.0;
+#pragma unroll
+      for (int k = 0; k < kSrvRegGroups; ++k)
+        if (rb + lane + 64 * k < re) fdf_group(A, R[k], acc);
+      chunk_store(w0, acc, pos, ns, partial, lane);
     }
-    if (!__shfl(lastg, 0, 64)) continue;
-    // every super is stored: the total (single rank; with out == nullptr the supers are the result)
-    if (out) wave_total<kRedVals, true>(spart, nsup, nsup, 1, 0, out);
-    if (lane == 0) {
-      __hip_atomic_store(tickets + nsup, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (done_flag && out) {
-        // lane 0 wrote every out[v]; once they are drained, publish the pass number to the host
+    if (w1 < nch) {
+      double acc[kRedVals];
+#pragma unroll
+      for (int v = 0; v < kRedVals; ++v) acc[v] = 0.0;
+#pragma unroll
+      for (int k = 0; k < kSrvLdsGroups; ++k) {
+        if (lb + lane + 64 * k < le) {
+          CorrGroup g;
+#pragma unroll
+          for (int q = 0; q < 6; ++q) g.f[q] = lf[wid][k][q][lane];
+#pragma unroll
+          for (int q = 0; q < 12; ++q) g.d[q] = ld[wid][k][q][lane];
+          fdf_group(A, g, acc);
+        }
+      }
+      for (uint32_t i = lb + lane + 64 * kSrvLdsGroups; i < le; i += 64) {
+        CorrGroup g;
+        load_group(c, i, g);
+        fdf_group(A, g, acc);
+      }
+      chunk_store(w1, acc, pos, ns, partial, lane);
+    }
+    for (int w = w1 + nw; w < nch; w += nw) {
+      double acc[kRedVals];
+#pragma unroll
+      for (int v = 0; v < kRedVals; ++v) acc[v] = 0.0;
+      const uint32_t g1 = base[w + 1] >> 2;
+      for (uint32_t i = (base[w] >> 2) + lane; i < g1; i += 64) {
+        CorrGroup g;
+        load_group(c, i, g);
+        fdf_group(A, g, acc);
+      }
+      chunk_store(w, acc, pos, ns, partial, lane);
+    }
+    if (w0 >= nch) continue;
+    const bool fin = wave_tickets(w0, nw, nch, 0, tickets, partial, spart, out, done_flag, seq, lane,
+                                  bench_passes > 0 ? nullptr : host_rows);
+    if (fin && lane == 0) {
+      if (ptimes) ptimes[2 * (seq & 1023) + 1] = wall_clock64();
+      if (bench_passes > 0) {
+        // the next bench pass (or a cancel after the last), forwarded like block 0 forwards the host's
+        unsigned long long v[16] = {};
+        const bool more = seq + 1 < seq0 + static_cast<unsigned long long>(bench_passes);
+        const unsigned long long st = static_cast<unsigned long long>(static_cast<unsigned int>(seq + 1)) << 32;
+#pragma unroll
+        for (int i = 0; i < kCmdWords; ++i)
+          v[i] = st | (i < 12 ? (more ? __float_as_uint(Abench.m[i]) : 0u) : (i == 12 ? (more ? kPassRun : kPassCancel) : 0u));
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(done_flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        write_mail(mail, v);
       }
     }
   }
@@ -1852,6 +2057,31 @@ hipError_t launch_fdf_soa_gated(const CorrSoA& c, const uint32_t* pos, const uin
   fdf_soa_gated_kernel<<<nb, 256, 0, s>>>(c, pos, base, ns, nch, partial, spart, tickets, out, done_flag, seq,
                                           cmd, mail, timeout_ticks, gtrace, host_pollers);
   return hipGetLastError();
+}
+
+int fdf_server_blocks(size_t ns, int cus) {
+  // one 4-wave block per CU, fewer when the shard has fewer chunks; 0 when a wave would hold more
+  // than 64 chunks (its lanes draw the tickets of all its chunks at once)
+  const int nch = chunk_count(ns);
+  if (nch == 0 || cus <= 0) return 0;
+  const int nb = std::min(cus, (nch + kSrvWaves - 1) / kSrvWaves);
+  if (nch > 64 * kSrvWaves * nb) return 0;
+  return nb;
+}
+
+hipError_t launch_fdf_server(const CorrSoA& c, const uint32_t* pos, const uint32_t* base, size_t ns, double* partial,
+                             double* spart, unsigned int* tickets, double* out, unsigned long long* done_flag,
+                             unsigned long long seq0, const PassCmd* cmd, PassCmd* mail,
+                             unsigned long long timeout_ticks, unsigned long long* ptimes, int bench_passes,
+                             Xf34 A, unsigned long long* host_rows, int nb, hipStream_t s) {
+  int nch = chunk_count(ns);
+  if (nch == 0 || nb <= 0) return hipErrorInvalidValue;
+  // every block must be resident at once (the blocks wait on each other's commands): a
+  // cooperative launch refuses a grid that cannot be
+  void* args[] = {const_cast<CorrSoA*>(&c), &pos, &base, &ns, &nch, &partial, &spart, &tickets, &out,
+                  &done_flag, &seq0, &cmd, &mail, &timeout_ticks, &ptimes, &bench_passes, &A, &host_rows};
+  return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(fdf_server_kernel), dim3(nb), dim3(256), args,
+                                    0, s);
 }
 
 hipError_t launch_super_reduce(const double* chunk, int nch, int nv, double* sup, hipStream_t s) {

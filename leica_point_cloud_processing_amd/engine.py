@@ -303,6 +303,16 @@ class GICPEngine:
         self._check(self._lib.mgicp_debug_fdf_sums(self._h, _dp(x), _dp(out)), "debug_fdf_sums")
         return out
 
+    def debug_pass_bench(self, x, npasses: int, mode: int = 0):
+        """(ms per pass, sums of the last pass): npasses objective passes at x over the last sweep,
+        back to back (mode 0: the resident pass server, 1: one launch per pass), HIP-event timed"""
+        x = np.asarray(x, np.float64)
+        ms = ctypes.c_double()
+        out = np.zeros(16, np.float64)
+        self._check(self._lib.mgicp_debug_pass_bench(self._h, _dp(x), int(npasses), int(mode), ctypes.byref(ms),
+                                                     _dp(out)), "debug_pass_bench")
+        return ms.value, out
+
     def debug_trace(self, max_iters: int = 1000):
         buf = np.zeros(16 * max_iters, np.float32)
         n = self._check(self._lib.mgicp_debug_trace(self._h, _fp(buf), max_iters), "debug_trace")

@@ -295,6 +295,41 @@ def test_pass_sums_independent_of_direction_and_finish(part_small, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n", [20_000, 2_500_000])
+def test_resident_server_matches_launched_passes(part_small, monkeypatch, n):
+    """The resident pass server (one cooperative launch per BFGS run, chunks kept in registers /
+    LDS across passes) gives the launched passes' sums bit for bit -- at 20k points (every chunk in
+    registers) and 2.5M points (register, LDS and streamed chunks) -- and aligns identically."""
+    from leica_point_cloud_processing_amd import synth
+    from leica_point_cloud_processing_amd.engine import GICPEngine
+
+    scan, cad, Ttrue = part_small if n == 20_000 else synth.scan_vs_cad(n, n)
+    T = np.linalg.inv(Ttrue).astype(np.float32)
+    x = np.array([0.001, -0.002, 0.0005, 0.0003, -0.0002, 0.0004])
+    e = GICPEngine()
+    e.set_source_xyz(scan)
+    e.set_target_xyz(cad)
+    e.debug_correspondences(T, len(scan))
+    ms0, s0 = e.debug_pass_bench(x, 7, 0)
+    ms1, s1 = e.debug_pass_bench(x, 7, 1)
+    s2 = e.debug_fdf_sums(x)  # through the live-server path of the aligns
+    np.testing.assert_array_equal(s0, s1)
+    np.testing.assert_array_equal(s0, s2)
+    assert ms0 > 0 and ms1 > 0
+    T_on = e.align()
+    it_on = e.last_result["iterations"]
+    e.close()
+    monkeypatch.setenv("MGICP_RESIDENT", "0")
+    f = GICPEngine()
+    f.set_source_xyz(scan)
+    f.set_target_xyz(cad)
+    T_off = f.align()
+    assert f.last_result["iterations"] == it_on
+    np.testing.assert_array_equal(T_on, T_off)
+    f.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("solver", [0, 1])
 def test_single_rank_comm_matches_plain(part_small, solver):
     """The collective code path (RCCL all-reduce per BFGS pass / per GN iteration, publish kernel,
