@@ -75,6 +75,10 @@ def parse():
                     help="points of the CPU-oracle sample for the FOD-side rows (0 = skip those rows)")
     ap.add_argument("--no-events", action="store_true",
                     help="skip the kernel-time (HIP event) leg")
+    ap.add_argument("--pass-bench", type=int, default=5,
+                    help="roofline leg of the resident pass server: this many server launches of "
+                         "--pass-bench-passes back-to-back objective passes each (0: off)")
+    ap.add_argument("--pass-bench-passes", type=int, default=50)
     ap.add_argument("--prof-steps", type=int, default=3,
                     help="aligns of the kernel-time leg (HIP events around every kernel family)")
     args = ap.parse_args()
@@ -256,6 +260,20 @@ def main():
             eng.align()
         kt = eng.kernel_times()
         eng.set_profiling(False)
+    # roofline leg of the pass the aligns run on one GPU: the resident pass server (one cooperative
+    # launch holding part of the streams on chip across passes) in its timing form -- P passes of
+    # one state back to back, chained on the device -- bracketed by HIP events on the engine's
+    # stream; rocprofv3 lists it as fdf_server_kernel<true> (duration / P = one pass).  Beside it the
+    # launched form (one fdf_soa_kernel per pass) over the same correspondences.
+    srv = None
+    if args.pass_bench > 0 and world == 1:
+        x0 = np.zeros(6)
+        P = args.pass_bench_passes
+        ms_srv = [eng.debug_pass_bench(x0, P, 0)[0] for _ in range(args.pass_bench)]
+        ms_lau = [eng.debug_pass_bench(x0, P, 1)[0] for _ in range(args.pass_bench)]
+        srv = {"ms_per_pass": float(np.mean(ms_srv)), "ms_per_pass_runs": [round(v, 5) for v in ms_srv],
+               "launched_ms_per_pass": float(np.mean(ms_lau)), "passes_per_launch": P,
+               "launches": args.pass_bench}
     T_final = eng.getFinalTransformation()
     trace_final = eng.debug_trace(args.max_iter + 1)  # per-iteration transforms of the last timed align
     result = dict(eng.last_result)
@@ -346,17 +364,36 @@ def main():
                 "algorithmic_bytes_per_launch": int(alg), "avg_launch_ms": avg_ms,
                 "launches_timed": launches_timed, "numerator": note}
 
-    roofline = roof("fdf_soa_kernel (BFGS objective pass, dominant: ~48 launches per outer iteration)",
-                    FDF_BYTES_SURVEY, m_shard, fdf_ms, kt["fdf"]["count"], "fdf_soa_kernel",
+    if srv is not None:
+        # the pass the aligns use: the resident server (timing form), per pass
+        pass_ms, pass_n = srv["ms_per_pass"], srv["passes_per_launch"] * srv["launches"]
+        pass_name = ("fdf_server_kernel (resident pass server: BFGS objective pass, dominant: 145 passes per C4 "
+                     "align; timing form fdf_server_kernel<true>, duration / passes_per_launch = one pass)")
+        pass_pmc = "fdf_server_kernel"
+    else:
+        pass_ms, pass_n = fdf_ms, kt["fdf"]["count"]
+        pass_name = "fdf_soa_kernel (BFGS objective pass, dominant: ~48 launches per outer iteration)"
+        pass_pmc = "fdf_soa_kernel"
+    roofline = roof(pass_name, FDF_BYTES_SURVEY, m_shard, pass_ms, pass_n, pass_pmc,
                     "SURVEY 8d / BASELINE.md: 52 B per accepted correspondence per pass (M as 6 fp32)")
     roofline["launches"] = n_evals
-    roofline["timing"] = ("HIP events on the engine stream around every 8th objective pass of the timed region "
-                          "(identical work per pass; sampling keeps the events' own cost out of value)")
-    stored = roof("fdf_soa_kernel", FDF_BYTES_STORED, m_shard, fdf_ms, kt["fdf"]["count"], "fdf_soa_kernel",
+    if srv is not None:
+        roofline["timing"] = (f"HIP events on the engine stream around {srv['launches']} server launches of "
+                              f"{srv['passes_per_launch']} back-to-back passes each (mgicp_debug_pass_bench mode 0) "
+                              "over the last timed align's correspondences; ~31 % of the bytes are register / "
+                              "LDS resident, the rest stream from HBM / Infinity Cache")
+        roofline["server"] = srv
+    else:
+        roofline["timing"] = ("HIP events on the engine stream around every 8th objective pass of the timed region "
+                              "(identical work per pass; sampling keeps the events' own cost out of value)")
+    stored = roof(pass_name, FDF_BYTES_STORED, m_shard, pass_ms, pass_n, pass_pmc,
                   "72 B per accepted correspondence: the bytes the pass actually reads (M stored as 6 fp64 "
                   "for bit parity with PCL's Matrix3d)")
     roofline["frac_72B_stored"] = stored["frac"]
     roofline["achieved_72B_stored"] = stored["achieved"]
+    launched = roof("fdf_soa_kernel (launched form, one launch per pass)", FDF_BYTES_SURVEY, m_shard,
+                    srv["launched_ms_per_pass"] if srv else fdf_ms, pass_n, "fdf_soa_kernel",
+                    "52 B per accepted correspondence per pass")
     corr_ms = kt["correspond"]["avg_ms"] + kt["compact"]["avg_ms"]
     # per cloud: the logged k-NN launch plus its (rare) register-list hand-off launch, 2 clouds
     cov_ms = kt_cov["knn_cov"]["avg_ms"] * kt_cov["knn_cov"]["count"] / 2
@@ -364,6 +401,7 @@ def main():
     rooflines = {
         "fdf_52B": roofline,
         "fdf_72B_stored": stored,
+        "fdf_launched_52B": launched,
         "correspondence_plus_mahalanobis": roof(
             "correspond_kernel + compact_kernel (1-NN sweep, Mahalanobis, compaction; once per outer iteration)",
             CORR_BYTES, n_shard, corr_ms, kt["correspond"]["count"], "correspond_plus_compact",

@@ -1460,6 +1460,9 @@ constexpr int kSrvRegGroups = 4;  // = one full chunk: kChunkPts / 4 / 64
 constexpr int kSrvLdsGroups = 2;
 constexpr int kSrvWaves = 4;
 
+// kBench: the timing instantiation (bench_passes > 0) -- a symbol of its own, so a rocprofv3 kernel
+// trace separates it from the servers of the aligns (its duration / bench_passes = one pass)
+template <bool kBench>
 __global__ __launch_bounds__(256, 1) void fdf_server_kernel(
     CorrSoA c, const uint32_t* __restrict__ pos, const uint32_t* __restrict__ base, size_t ns, int nch,
     double* __restrict__ partial, double* __restrict__ spart, unsigned int* __restrict__ tickets,
@@ -2076,12 +2079,25 @@ hipError_t launch_fdf_server(const CorrSoA& c, const uint32_t* pos, const uint32
                              Xf34 A, unsigned long long* host_rows, int nb, hipStream_t s) {
   int nch = chunk_count(ns);
   if (nch == 0 || nb <= 0) return hipErrorInvalidValue;
-  // every block must be resident at once (the blocks wait on each other's commands): a
-  // cooperative launch refuses a grid that cannot be
-  void* args[] = {const_cast<CorrSoA*>(&c), &pos, &base, &ns, &nch, &partial, &spart, &tickets, &out,
-                  &done_flag, &seq0, &cmd, &mail, &timeout_ticks, &ptimes, &bench_passes, &A, &host_rows};
-  return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(fdf_server_kernel), dim3(nb), dim3(256), args,
-                                    0, s);
+  // every block must be resident at once (the blocks wait on each other's commands): refuse a grid
+  // the device cannot hold (one block per CU, at most one per CU by its LDS and registers).  A plain
+  // launch after this check: a cooperative launch checks the same, but under rocprofv3 the process
+  // then crashed in the runtime's teardown after the profiler had finalised (r02)
+  const void* fn = bench_passes > 0 ? reinterpret_cast<const void*>(fdf_server_kernel<true>)
+                                    : reinterpret_cast<const void*>(fdf_server_kernel<false>);
+  int per_cu = 0, dev = 0, cus = 0;
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, 0);
+  if (e == hipSuccess) e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e != hipSuccess) return e;
+  if (per_cu < 1 || static_cast<long long>(per_cu) * cus < nb) return hipErrorCooperativeLaunchTooLarge;
+  if (bench_passes > 0)
+    fdf_server_kernel<true><<<nb, 256, 0, s>>>(c, pos, base, ns, nch, partial, spart, tickets, out, done_flag, seq0,
+                                                cmd, mail, timeout_ticks, ptimes, bench_passes, A, host_rows);
+  else
+    fdf_server_kernel<false><<<nb, 256, 0, s>>>(c, pos, base, ns, nch, partial, spart, tickets, out, done_flag, seq0,
+                                                 cmd, mail, timeout_ticks, ptimes, bench_passes, A, host_rows);
+  return hipGetLastError();
 }
 
 hipError_t launch_super_reduce(const double* chunk, int nch, int nv, double* sup, hipStream_t s) {
@@ -2269,6 +2285,8 @@ hipError_t preload_kernels(void* pinned, size_t pinned_bytes, hipStream_t s) {
       reinterpret_cast<const void*>(&compact_kernel),
       reinterpret_cast<const void*>(&fdf_soa_kernel),
       reinterpret_cast<const void*>(&fdf_soa_gated_kernel),
+      reinterpret_cast<const void*>(&fdf_server_kernel<false>),
+      reinterpret_cast<const void*>(&fdf_server_kernel<true>),
       reinterpret_cast<const void*>(&fitness_kernel),
       reinterpret_cast<const void*>(&resolution_kernel),
       reinterpret_cast<const void*>(&radius_keep_kernel),

@@ -5,7 +5,8 @@ Corrections follow /opt/skills/guides/MI355X_MICROARCH.md "HBM": FETCH_SIZE / WR
 KiB; on gfx950 FETCH_SIZE reports exactly HALF of the bytes of a wide (16 B/lane) coalesced
 STREAMING read, and "other access widths are uncalibrated".  So the x2 correction is applied per
 kernel only where the kernel's reads are all 16-byte-per-lane coalesced streams:
-  * fdf_soa_kernel -- every load is a float4 / double2 stream at consecutive addresses: x2;
+  * fdf_soa_kernel and the resident server's streamed part (fdf_server_kernel<true>) -- every load
+    is a float4 / double2 stream at consecutive addresses: x2;
   * correspond_kernel, knn_cov_kernel, fitness / segdiff (grid gathers), compact_kernel and
     gn_moments_kernel (coalesced 4 B index loads mixed with 16 B gathers): raw FETCH_SIZE,
     labelled uncalibrated -- the true HBM bytes lie between 1x and 2x the raw figure.
@@ -19,8 +20,12 @@ import json
 import os
 import sys
 
-STREAMING = {"fdf_soa_kernel"}
-KERNELS = ("fdf_soa_kernel", "correspond_kernel", "compact_kernel", "chunk_base_kernel", "knn_cov2_kernel",
+STREAMING = {"fdf_soa_kernel", "fdf_server_kernel<true>"}
+# the resident pass server's timing form runs PASSES passes per dispatch (bench.py
+# --pass-bench-passes): its figures are per pass (dispatch / PASSES, the one-time resident load
+# included pro rata)
+PASSES = {"fdf_server_kernel<true>": int(os.environ.get("PASS_BENCH_PASSES", "50"))}
+KERNELS = ("fdf_server_kernel<true>", "fdf_soa_kernel", "correspond_kernel", "compact_kernel", "chunk_base_kernel", "knn_cov2_kernel",
            "knn_cov_kernel", "fitness_kernel", "gn_moments_kernel", "segdiff_kernel", "voxel_key_kernel",
            "voxel_centroid_kernel")
 
@@ -35,9 +40,9 @@ def per_dispatch(directory, counter, kernel):
     return vals
 
 
-def entry(fk, wk, streaming):
-    f_kib = sum(fk) / len(fk)
-    w_kib = sum(wk) / len(wk)
+def entry(fk, wk, streaming, passes=1):
+    f_kib = sum(fk) / len(fk) / passes
+    w_kib = sum(wk) / len(wk) / passes
     mult = 2.0 if streaming else 1.0
     return {
         "dispatches": len(fk),
@@ -57,7 +62,11 @@ def main():
     for k in KERNELS:
         fk, wk = per_dispatch(fdir, "FETCH_SIZE", k), per_dispatch(wdir, "WRITE_SIZE", k)
         if fk and wk:
-            kernels[k] = entry(fk, wk, k in STREAMING)
+            kernels[k] = entry(fk, wk, k in STREAMING, PASSES.get(k, 1))
+            if k in PASSES:
+                kernels[k]["per"] = f"pass (dispatch / {PASSES[k]})"
+    if "fdf_server_kernel<true>" in kernels:  # bench.py's key for the server's roofline traffic
+        kernels["fdf_server_kernel"] = kernels["fdf_server_kernel<true>"]
     if "correspond_kernel" in kernels and "compact_kernel" in kernels:
         a, b = kernels["correspond_kernel"], kernels["compact_kernel"]
         kernels["correspond_plus_compact"] = {
