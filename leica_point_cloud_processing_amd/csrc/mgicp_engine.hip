@@ -315,6 +315,7 @@ struct mgicp_ctx {
   bool srv_live = false;                // a server is running and waits for pass srv_next
   unsigned long long srv_next = 0;
   int cus = 0;                          // compute units (the server's grid)
+  int srv_waves = 4;                    // server shape: 4 or 8 waves per CU (env MGICP_SRV_WAVES)
   unsigned long long* h_ptimes = nullptr;  // MGICP_PASS_TIMES=1: per pass gate exit / finish (wall clock)
   unsigned long long* d_ptimes = nullptr;
   // the server's super partials as stamped host rows (32 words per super; env MGICP_HOST_ROWS)
@@ -1104,7 +1105,7 @@ struct DeviceFunctor {
     const bool gate = ctx->gated && poll && inlaunch && !ctx->profiling;
     const Xf34 Ax = A.xf();
     const CorrSoA c = corr_soa(ctx);
-    const int nsrv = (gate && ctx->resident) ? fdf_server_blocks(ns, ctx->cus) : 0;
+    const int nsrv = (gate && ctx->resident) ? fdf_server_blocks(ns, ctx->cus, ctx->srv_waves) : 0;
     if (nsrv > 0) {
       // the resident server runs every pass of this BFGS run: start it with the first one
       const long long nsup = ctx->nsup_local();
@@ -1115,7 +1116,8 @@ struct DeviceFunctor {
         ProfScope ps(ctx, kFamFdf);
         HIPCK(launch_fdf_server(c, ctx->cpos.p, ctx->chunk_base.p, ns, ctx->partial.p, ctx->spart.p,
                                 ctx->tickets.p, out, ctx->d_flag, seq, ctx->d_cmd, ctx->mail, ctx->gate_timeout,
-                                ctx->d_ptimes, 0, Ax, ctx->host_rows ? ctx->d_rows : nullptr, nsrv, ctx->stream));
+                                ctx->d_ptimes, 0, Ax, ctx->host_rows ? ctx->d_rows : nullptr, nsrv, ctx->srv_waves,
+                                ctx->stream));
         ctx->srv_live = true;
       }
       publish_cmd(ctx, seq, kPassRun, 0, &Ax);
@@ -1375,6 +1377,7 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
   if (const char* ga = std::getenv("MGICP_GATED")) ctx->gated = std::atoi(ga) != 0;
   if (const char* rs = std::getenv("MGICP_RESIDENT")) ctx->resident = std::atoi(rs) != 0;
   if (const char* hr = std::getenv("MGICP_HOST_ROWS")) ctx->host_rows = std::atoi(hr) != 0;
+  if (const char* sw = std::getenv("MGICP_SRV_WAVES")) ctx->srv_waves = std::atoi(sw) == 8 ? 8 : 4;
   ctx->knn_logged = knn_logged_enabled();
   if (const char* st = std::getenv("MGICP_SPLIT_TARGET_COV")) ctx->split_target_cov = std::atoi(st) != 0;
   if (const char* ps = std::getenv("MGICP_PROF_STRIDE")) ctx->prof_stride = std::max(1, std::atoi(ps));
@@ -2084,7 +2087,7 @@ int mgicp_debug_pass_bench(mgicp_ctx* ctx, const double x[6], int npasses, int m
   HIPCK(hipEventRecord(a, ctx->stream));
   hipError_t e = hipSuccess;
   if (mode == 0) {
-    const int nb = fdf_server_blocks(ns, ctx->cus);
+    const int nb = fdf_server_blocks(ns, ctx->cus, ctx->srv_waves);
     if (nb <= 0) {
       (void)hipEventDestroy(a);
       (void)hipEventDestroy(b);
@@ -2093,7 +2096,7 @@ int mgicp_debug_pass_bench(mgicp_ctx* ctx, const double x[6], int npasses, int m
     const unsigned long long seq0 = ++ctx->pass_seq;
     e = launch_fdf_server(c, ctx->cpos.p, ctx->chunk_base.p, ns, ctx->partial.p, ctx->spart.p, ctx->tickets.p,
                           ctx->d_h_red, ctx->d_flag, seq0, ctx->d_cmd, ctx->mail, ctx->gate_timeout, ctx->d_ptimes,
-                          npasses, A, nullptr, nb, ctx->stream);
+                          npasses, A, nullptr, nb, ctx->srv_waves, ctx->stream);
     ctx->pass_seq = seq0 + static_cast<unsigned long long>(npasses);  // the closing cancel's stamp too
   } else {
     const int nb = fdf_grid_blocks(ns, ctx->fdf_max_blocks);

@@ -156,14 +156,14 @@ int        fdf_grid_blocks(size_t ns, int max_blocks = 2048);
 // seq0, seq0 + 1, ... each run on the command with that stamp, until a cancel; bench_passes > 0
 // (timing): that many passes of A back to back without commands.  fdf_server_blocks: its grid for a
 // shard of ns positions on `cus` CUs (0: not servable, use the launched passes)
-int        fdf_server_blocks(size_t ns, int cus);
+int        fdf_server_blocks(size_t ns, int cus, int waves /*4 or 8 per CU*/);
 hipError_t launch_fdf_server(const CorrSoA& c, const uint32_t* pos, const uint32_t* base, size_t ns, double* partial,
                              double* spart, unsigned int* tickets, double* out, unsigned long long* done_flag,
                              unsigned long long seq0, const PassCmd* cmd, PassCmd* mail,
                              unsigned long long timeout_ticks, unsigned long long* ptimes /*nullable*/,
                              int bench_passes, Xf34 A,
                              unsigned long long* host_rows /*nullable: super rows to the host*/, int nb,
-                             hipStream_t s);
+                             int waves, hipStream_t s);
 
 // super partials of nch chunk partials of nv (kRedVals or kMomVals) values
 hipError_t launch_super_reduce(const double* chunk, int nch, int nv, double* sup, hipStream_t s);

@@ -1456,42 +1456,59 @@ __device__ __forceinline__ void fdf_soa_body(CorrSoA c, const uint32_t* __restri
 // because one wave per SIMD keeps few loads in flight; software-pipelining the streamed groups in
 // registers (2-3 resident groups, spills) or through an LDS-DMA ring (3 resident groups) measured
 // 67-77 us per pass against ~65 us for this form and ~66-70 us for launched passes.
-constexpr int kSrvRegGroups = 4;  // = one full chunk: kChunkPts / 4 / 64
-constexpr int kSrvLdsGroups = 2;
-constexpr int kSrvWaves = 4;
+// Two shapes (env MGICP_SRV_WAVES): 4 waves per CU (1 per SIMD, 512 VGPR+AGPR) holding a whole chunk
+// in registers + 2 groups in LDS (31 % of C4's bytes on chip), or 8 waves per CU (2 per SIMD, 256
+// registers) holding 1 group in registers + 1 in LDS each (21 %) with two waves per SIMD to
+// overlap the streamed loads.
+template <int kWaves>
+struct SrvShape;
+template <>
+struct SrvShape<4> {
+  static constexpr int kReg = 4, kLds = 2;  // kReg = 4: the LDS groups are chunk 1's first kLds
+};
+template <>
+struct SrvShape<8> {
+  static constexpr int kReg = 1, kLds = 1;  // kReg < 4: the LDS groups follow in chunk 0
+};
 
 // kBench: the timing instantiation (bench_passes > 0) -- a symbol of its own, so a rocprofv3 kernel
 // trace separates it from the servers of the aligns (its duration / bench_passes = one pass)
-template <bool kBench>
-__global__ __launch_bounds__(256, 1) void fdf_server_kernel(
+template <bool kBench, int kWaves>
+__global__ __launch_bounds__(64 * kWaves, 1) void fdf_server_kernel(
     CorrSoA c, const uint32_t* __restrict__ pos, const uint32_t* __restrict__ base, size_t ns, int nch,
     double* __restrict__ partial, double* __restrict__ spart, unsigned int* __restrict__ tickets,
     double* __restrict__ out, unsigned long long* done_flag, unsigned long long seq0, const PassCmd* cmd,
     PassCmd* mail, unsigned long long timeout, unsigned long long* ptimes, int bench_passes, Xf34 Abench,
     unsigned long long* host_rows) {
-  __shared__ float4 lf[kSrvWaves][kSrvLdsGroups][6][64];
-  __shared__ double2 ld[kSrvWaves][kSrvLdsGroups][12][64];
+  constexpr int kR = SrvShape<kWaves>::kReg, kL = SrvShape<kWaves>::kLds;
+  static_assert(kR <= 4 && (kR == 4 || kR + kL <= 4), "resident groups: chunk 0, then chunk 1 only after a full chunk 0");
+  __shared__ float4 lf[kWaves][kL][6][64];
+  __shared__ double2 ld[kWaves][kL][12][64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int nw = gridDim.x * kSrvWaves;
-  const int w0 = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x * kSrvWaves + wid));
-  // resident data: chunk w0 in registers, groups 0..kSrvLdsGroups-1 of chunk w0 + nw in LDS (each
-  // lane reads back only its own slots, so no barrier is needed)
-  CorrGroup R[kSrvRegGroups];
+  const int nw = gridDim.x * kWaves;
+  const int w0 = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x * kWaves + wid));
+  // resident data: groups [0, kR) of chunk w0 in registers; kLds groups in LDS -- chunk w1's first
+  // ones when chunk w0 is whole in registers, else chunk w0's next ones (each lane reads back only
+  // its own slots, so no barrier is needed)
+  const int w1 = w0 + nw;
+  CorrGroup R[kR];
   uint32_t rb = 0, re = 0, lb = 0, le = 0;
   if (w0 < nch) {
     rb = base[w0] >> 2;
     re = base[w0 + 1] >> 2;
   }
-#pragma unroll
-  for (int k = 0; k < kSrvRegGroups; ++k)
-    if (rb + lane + 64 * k < re) load_group(c, rb + lane + 64 * k, R[k]);
-  const int w1 = w0 + nw;
-  if (w1 < nch) {
+  if (kR == 4 && w1 < nch) {
     lb = base[w1] >> 2;
     le = base[w1 + 1] >> 2;
+  } else if (kR < 4) {
+    lb = rb + 64 * kR;
+    le = re;
   }
 #pragma unroll
-  for (int k = 0; k < kSrvLdsGroups; ++k) {
+  for (int k = 0; k < kR; ++k)
+    if (rb + lane + 64 * k < re) load_group(c, rb + lane + 64 * k, R[k]);
+#pragma unroll
+  for (int k = 0; k < kL; ++k) {
     if (lb + lane + 64 * k < le) {
       CorrGroup g;
       load_group(c, lb + lane + 64 * k, g);
@@ -1501,38 +1518,52 @@ __global__ __launch_bounds__(256, 1) void fdf_server_kernel(
       for (int q = 0; q < 12; ++q) ld[wid][k][q][lane] = g.d[q];
     }
   }
-  const int host_pollers = bench_passes > 0 ? 0 : 1;
+  auto lds_group = [&](int k, const Xf34& A, double (&acc)[kRedVals]) {
+    CorrGroup g;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) g.f[q] = lf[wid][k][q][lane];
+#pragma unroll
+    for (int q = 0; q < 12; ++q) g.d[q] = ld[wid][k][q][lane];
+    fdf_group(A, g, acc);
+  };
+  const int host_pollers = kBench ? 0 : 1;
   for (unsigned long long seq = seq0;; ++seq) {
     Xf34 A = Abench;
     int rev = 0;
-    if (!(bench_passes > 0 && seq == seq0) && !pass_gate(seq, cmd, mail, timeout, nullptr, host_pollers, A, rev))
-      return;
+    if (!(kBench && seq == seq0) && !pass_gate(seq, cmd, mail, timeout, nullptr, host_pollers, A, rev)) return;
     if (ptimes && blockIdx.x == 0 && threadIdx.x == 0) ptimes[2 * (seq & 1023)] = wall_clock64();
     if (w0 < nch) {
       double acc[kRedVals];
 #pragma unroll
       for (int v = 0; v < kRedVals; ++v) acc[v] = 0.0;
 #pragma unroll
-      for (int k = 0; k < kSrvRegGroups; ++k)
+      for (int k = 0; k < kR; ++k)
         if (rb + lane + 64 * k < re) fdf_group(A, R[k], acc);
+      if (kR < 4) {
+#pragma unroll
+        for (int k = 0; k < kL; ++k)
+          if (lb + lane + 64 * k < le) lds_group(k, A, acc);
+        for (uint32_t i = rb + lane + 64 * (kR + kL); i < re; i += 64) {
+          CorrGroup g;
+          load_group(c, i, g);
+          fdf_group(A, g, acc);
+        }
+      }
       chunk_store(w0, acc, pos, ns, partial, lane);
     }
     if (w1 < nch) {
       double acc[kRedVals];
 #pragma unroll
       for (int v = 0; v < kRedVals; ++v) acc[v] = 0.0;
+      uint32_t i0 = (base[w1] >> 2) + lane;
+      if (kR == 4) {
 #pragma unroll
-      for (int k = 0; k < kSrvLdsGroups; ++k) {
-        if (lb + lane + 64 * k < le) {
-          CorrGroup g;
-#pragma unroll
-          for (int q = 0; q < 6; ++q) g.f[q] = lf[wid][k][q][lane];
-#pragma unroll
-          for (int q = 0; q < 12; ++q) g.d[q] = ld[wid][k][q][lane];
-          fdf_group(A, g, acc);
-        }
+        for (int k = 0; k < kL; ++k)
+          if (lb + lane + 64 * k < le) lds_group(k, A, acc);
+        i0 = lb + lane + 64 * kL;
       }
-      for (uint32_t i = lb + lane + 64 * kSrvLdsGroups; i < le; i += 64) {
+      const uint32_t g1 = base[w1 + 1] >> 2;
+      for (uint32_t i = i0; i < g1; i += 64) {
         CorrGroup g;
         load_group(c, i, g);
         fdf_group(A, g, acc);
@@ -1553,10 +1584,10 @@ __global__ __launch_bounds__(256, 1) void fdf_server_kernel(
     }
     if (w0 >= nch) continue;
     const bool fin = wave_tickets(w0, nw, nch, 0, tickets, partial, spart, out, done_flag, seq, lane,
-                                  bench_passes > 0 ? nullptr : host_rows);
+                                  kBench ? nullptr : host_rows);
     if (fin && lane == 0) {
       if (ptimes) ptimes[2 * (seq & 1023) + 1] = wall_clock64();
-      if (bench_passes > 0) {
+      if (kBench) {
         // the next bench pass (or a cancel after the last), forwarded like block 0 forwards the host's
         unsigned long long v[16] = {};
         const bool more = seq + 1 < seq0 + static_cast<unsigned long long>(bench_passes);
@@ -2062,13 +2093,13 @@ hipError_t launch_fdf_soa_gated(const CorrSoA& c, const uint32_t* pos, const uin
   return hipGetLastError();
 }
 
-int fdf_server_blocks(size_t ns, int cus) {
-  // one 4-wave block per CU, fewer when the shard has fewer chunks; 0 when a wave would hold more
-  // than 64 chunks (its lanes draw the tickets of all its chunks at once)
+int fdf_server_blocks(size_t ns, int cus, int waves) {
+  // one block of `waves` waves per CU, fewer when the shard has fewer chunks; 0 when a wave would
+  // hold more than 64 chunks (its lanes draw the tickets of all its chunks at once)
   const int nch = chunk_count(ns);
-  if (nch == 0 || cus <= 0) return 0;
-  const int nb = std::min(cus, (nch + kSrvWaves - 1) / kSrvWaves);
-  if (nch > 64 * kSrvWaves * nb) return 0;
+  if (nch == 0 || cus <= 0 || (waves != 4 && waves != 8)) return 0;
+  const int nb = std::min(cus, (nch + waves - 1) / waves);
+  if (nch > 64 * waves * nb) return 0;
   return nb;
 }
 
@@ -2076,27 +2107,35 @@ hipError_t launch_fdf_server(const CorrSoA& c, const uint32_t* pos, const uint32
                              double* spart, unsigned int* tickets, double* out, unsigned long long* done_flag,
                              unsigned long long seq0, const PassCmd* cmd, PassCmd* mail,
                              unsigned long long timeout_ticks, unsigned long long* ptimes, int bench_passes,
-                             Xf34 A, unsigned long long* host_rows, int nb, hipStream_t s) {
+                             Xf34 A, unsigned long long* host_rows, int nb, int waves, hipStream_t s) {
   int nch = chunk_count(ns);
-  if (nch == 0 || nb <= 0) return hipErrorInvalidValue;
+  if (nch == 0 || nb <= 0 || (waves != 4 && waves != 8)) return hipErrorInvalidValue;
   // every block must be resident at once (the blocks wait on each other's commands): refuse a grid
   // the device cannot hold (one block per CU, at most one per CU by its LDS and registers).  A plain
   // launch after this check: a cooperative launch checks the same, but under rocprofv3 the process
   // then crashed in the runtime's teardown after the profiler had finalised (r02)
-  const void* fn = bench_passes > 0 ? reinterpret_cast<const void*>(fdf_server_kernel<true>)
-                                    : reinterpret_cast<const void*>(fdf_server_kernel<false>);
+  const bool b = bench_passes > 0;
+  const void* fn = waves == 4 ? (b ? reinterpret_cast<const void*>(fdf_server_kernel<true, 4>)
+                                   : reinterpret_cast<const void*>(fdf_server_kernel<false, 4>))
+                              : (b ? reinterpret_cast<const void*>(fdf_server_kernel<true, 8>)
+                                   : reinterpret_cast<const void*>(fdf_server_kernel<false, 8>));
   int per_cu = 0, dev = 0, cus = 0;
-  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, 0);
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * waves, 0);
   if (e == hipSuccess) e = hipGetDevice(&dev);
   if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   if (e != hipSuccess) return e;
   if (per_cu < 1 || static_cast<long long>(per_cu) * cus < nb) return hipErrorCooperativeLaunchTooLarge;
-  if (bench_passes > 0)
-    fdf_server_kernel<true><<<nb, 256, 0, s>>>(c, pos, base, ns, nch, partial, spart, tickets, out, done_flag, seq0,
-                                                cmd, mail, timeout_ticks, ptimes, bench_passes, A, host_rows);
-  else
-    fdf_server_kernel<false><<<nb, 256, 0, s>>>(c, pos, base, ns, nch, partial, spart, tickets, out, done_flag, seq0,
-                                                 cmd, mail, timeout_ticks, ptimes, bench_passes, A, host_rows);
+#define MGICP_SRV_LAUNCH(B, W)                                                                                  \
+  fdf_server_kernel<B, W><<<nb, 64 * (W), 0, s>>>(c, pos, base, ns, nch, partial, spart, tickets, out, done_flag, \
+                                                  seq0, cmd, mail, timeout_ticks, ptimes, bench_passes, A, host_rows)
+  if (waves == 4) {
+    if (b) MGICP_SRV_LAUNCH(true, 4);
+    else MGICP_SRV_LAUNCH(false, 4);
+  } else {
+    if (b) MGICP_SRV_LAUNCH(true, 8);
+    else MGICP_SRV_LAUNCH(false, 8);
+  }
+#undef MGICP_SRV_LAUNCH
   return hipGetLastError();
 }
 
@@ -2285,8 +2324,10 @@ hipError_t preload_kernels(void* pinned, size_t pinned_bytes, hipStream_t s) {
       reinterpret_cast<const void*>(&compact_kernel),
       reinterpret_cast<const void*>(&fdf_soa_kernel),
       reinterpret_cast<const void*>(&fdf_soa_gated_kernel),
-      reinterpret_cast<const void*>(&fdf_server_kernel<false>),
-      reinterpret_cast<const void*>(&fdf_server_kernel<true>),
+      reinterpret_cast<const void*>(&fdf_server_kernel<false, 4>),
+      reinterpret_cast<const void*>(&fdf_server_kernel<true, 4>),
+      reinterpret_cast<const void*>(&fdf_server_kernel<false, 8>),
+      reinterpret_cast<const void*>(&fdf_server_kernel<true, 8>),
       reinterpret_cast<const void*>(&fitness_kernel),
       reinterpret_cast<const void*>(&resolution_kernel),
       reinterpret_cast<const void*>(&radius_keep_kernel),
