@@ -324,6 +324,10 @@ struct mgicp_ctx {
   unsigned long long* d_rows = nullptr;
   size_t rows_cap = 0;                  // supers
   std::vector<double> row_sums;         // decoded super partials
+  // MGICP_PASS_TIMES: host view of the server passes -- command published -> rows complete
+  // (device pass + PCIe both ways) and rows complete -> next command (host BFGS step)
+  double ht_dev = 0, ht_host = 0, ht_last_rows = 0;
+  int ht_n = 0, ht_nh = 0;
   // build scratch
   DevBuf<uint32_t> counts, keys, keys_sorted, vals;
   DevBuf<unsigned char> scratch;
@@ -1120,10 +1124,20 @@ struct DeviceFunctor {
                                 ctx->stream));
         ctx->srv_live = true;
       }
+      const double t_pub = ctx->h_ptimes ? now_ms() : 0.0;
+      if (ctx->h_ptimes && ctx->ht_last_rows > 0 && t_pub - ctx->ht_last_rows < 1.0) {
+        ctx->ht_host += t_pub - ctx->ht_last_rows;
+        ++ctx->ht_nh;
+      }
       publish_cmd(ctx, seq, kPassRun, 0, &Ax);
       ctx->srv_next = seq + 1;
       if (ctx->host_rows) {
         if ((rc = wait_rows(ctx, seq, nsup, sums))) return rc;
+        if (ctx->h_ptimes) {
+          ctx->ht_last_rows = now_ms();
+          ctx->ht_dev += ctx->ht_last_rows - t_pub;
+          ++ctx->ht_n;
+        }
       } else {
         if ((rc = wait_pass(ctx, seq))) return rc;
         std::memcpy(sums, ctx->h_red, kRedVals * sizeof(double));
@@ -1617,6 +1631,11 @@ int mgicp_align(mgicp_ctx* ctx, const float guess_cm[16], float out_T_cm[16], mg
     if (na)
       std::fprintf(stderr, "[pass-times] passes %d | active %.2f us | finish -> next gate exit %.2f us (%d)\n", na,
                    act / na, ng ? gap / ng : 0.0, ng);
+    if (ctx->ht_n)
+      std::fprintf(stderr, "[pass-times] host view: %d passes | command -> rows complete %.2f us | rows -> next command %.2f us\n",
+                   ctx->ht_n, 1e3 * ctx->ht_dev / ctx->ht_n, ctx->ht_nh ? 1e3 * ctx->ht_host / ctx->ht_nh : 0.0);
+    ctx->ht_dev = ctx->ht_host = ctx->ht_last_rows = 0;
+    ctx->ht_n = ctx->ht_nh = 0;
     std::memset(ctx->h_ptimes, 0, 2 * 1024 * sizeof(unsigned long long));
   }
   // final_transformation_ = previous_transformation_ (3x3) * guess (3x3); t = prev t + guess t
