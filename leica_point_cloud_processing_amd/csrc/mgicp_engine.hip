@@ -209,6 +209,8 @@ struct Cloud {
   DevBuf<uint32_t> cell_start;
   DevBuf<uint8_t> empty_dist; // empty-space map (target only: 1-NN queries leave the surface)
   bool want_empty_map = false;
+  DevBuf<uint32_t> seed, seed_scratch;  // seed map (target: first-sweep 1-NN seeds; env MGICP_SEED_MAP)
+  bool want_seed_map = false;
   DevBuf<float4> boxes;       // per-cell point boxes (target only: the 1-NN sweeps prune by them)
   bool want_boxes = false;
   bool drop_nonfinite = false; // build the grid over the finite points only (KdTreeFLANN semantics)
@@ -298,6 +300,10 @@ struct mgicp_ctx {
   PassCmd* h_cmd = nullptr;             // pinned, mapped, coherent host memory
   PassCmd* d_cmd = nullptr;             // its device address
   PassCmd* mail = nullptr;              // device copy block 0 of a gated pass forwards to the others
+  // the server's command block in fine-grained device memory that the host stores into through the
+  // BAR (env MGICP_BAR_CMD): every server block polls it, no PCIe read and no mailbox hop
+  bool bar = true;
+  PassCmd* bar_cmd = nullptr;
   // blocks polling the host copy (env MGICP_GATE_POLLERS): 1 measured best (14.15 ms / C4 align;
   // 8 pollers 14.8 ms, all 256 blocks on host memory ~70 ms: PCIe read contention;
   // profiles/r02/ab_gate)
@@ -326,7 +332,7 @@ struct mgicp_ctx {
   std::vector<double> row_sums;         // decoded super partials
   // MGICP_PASS_TIMES: host view of the server passes -- command published -> rows complete
   // (device pass + PCIe both ways) and rows complete -> next command (host BFGS step)
-  double ht_dev = 0, ht_host = 0, ht_last_rows = 0;
+  double ht_dev = 0, ht_host = 0, ht_bfgs = 0, ht_last_rows = 0;
   int ht_n = 0, ht_nh = 0;
   // build scratch
   DevBuf<uint32_t> counts, keys, keys_sorted, vals;
@@ -443,6 +449,13 @@ void publish_cmd(mgicp_ctx* ctx, unsigned long long seq, unsigned int op, int re
   w[12] = op;
   w[13] = static_cast<unsigned int>(reverse);
   const unsigned long long stamp = static_cast<unsigned long long>(static_cast<unsigned int>(seq)) << 32;
+  if (ctx->bar_cmd) {
+    // device memory through the BAR: aligned 8-byte stores, then a store fence so they leave the
+    // core's write-combining buffers now
+    volatile unsigned long long* b = ctx->bar_cmd->h;
+    for (int i = 0; i < kCmdWords; ++i) b[i] = stamp | w[i];
+    __builtin_ia32_sfence();
+  }
   for (int i = 0; i < kCmdWords; ++i) __atomic_store_n(&ctx->h_cmd->h[i], stamp | w[i], __ATOMIC_RELEASE);
 }
 
@@ -680,13 +693,20 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
   g.cell_start = cl.cell_start.p;
   g.pts = cl.pts.p;
   g.empty_dist = nullptr;
+  g.seed = nullptr;
   if (cl.want_empty_map) {
     HIPCK(cl.empty_dist.reserve(nc));
     HIPCK(ctx->scratch.reserve(nc));
-    HIPCK(launch_empty_map(cl.cell_start.p, nd[0], nd[1], nd[2], cl.empty_dist.p, ctx->scratch.p, s));
+    if (cl.want_seed_map) {
+      HIPCK(cl.seed.reserve(nc));
+      HIPCK(cl.seed_scratch.reserve(nc));
+    }
+    HIPCK(launch_empty_map(cl.cell_start.p, nd[0], nd[1], nd[2], cl.empty_dist.p, ctx->scratch.p, s,
+                           cl.want_seed_map ? cl.seed.p : nullptr, cl.want_seed_map ? cl.seed_scratch.p : nullptr));
     if ((rc = sync(ctx))) return rc;
     MGICP_TRACE_AT("grid: empty map done");
     g.empty_dist = cl.empty_dist.p;
+    if (cl.want_seed_map) g.seed = cl.seed.p;
   }
   g.boxes = nullptr;
   if (cl.want_boxes && nc <= kMaxBoxCells) {
@@ -840,6 +860,13 @@ int ensure_host_red(mgicp_ctx* ctx) {
       if (const char* gp = std::getenv("MGICP_GATE_POLLERS")) ctx->gate_pollers = std::max(1, std::atoi(gp));
     }
     HIPCK(hipMemsetAsync(ctx->mail, 0, sizeof(PassCmd), ctx->stream));
+    if (ctx->bar && !ctx->bar_cmd) {
+      if (hipExtMallocWithFlags(reinterpret_cast<void**>(&ctx->bar_cmd), sizeof(PassCmd), hipDeviceMallocFinegrained) !=
+          hipSuccess)
+        ctx->bar_cmd = nullptr;  // no host-writable device memory: block 0 polls the pinned copy
+      else
+        HIPCK(hipMemset(ctx->bar_cmd, 0, sizeof(PassCmd)));  // complete before the host's first store
+    }
     if (const char* pt = std::getenv("MGICP_PASS_TIMES"); pt && std::atoi(pt)) {
       HIPCK(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_ptimes), 2 * 1024 * sizeof(unsigned long long),
                           hipHostMallocMapped | hipHostMallocCoherent));
@@ -1092,6 +1119,7 @@ struct DeviceFunctor {
   double m = 0;  // correspondences of this sweep (all ranks)
 
   int pass(const Vec6& x, double sums[kRedVals]) {
+    const double t_entry = ctx->h_ptimes ? now_ms() : 0.0;
     const Mat4 A = apply_state(x);
     const size_t ns = ctx->shard_p1() - ctx->shard_p0();
     const int nb = fdf_grid_blocks(ns, ctx->fdf_max_blocks);
@@ -1119,14 +1147,16 @@ struct DeviceFunctor {
         HIPCK(hipMemsetAsync(ctx->tickets.p, 0, ctx->tickets_n * sizeof(unsigned int), ctx->stream));
         ProfScope ps(ctx, kFamFdf);
         HIPCK(launch_fdf_server(c, ctx->cpos.p, ctx->chunk_base.p, ns, ctx->partial.p, ctx->spart.p,
-                                ctx->tickets.p, out, ctx->d_flag, seq, ctx->d_cmd, ctx->mail, ctx->gate_timeout,
+                                ctx->tickets.p, out, ctx->d_flag, seq, ctx->bar_cmd ? ctx->bar_cmd : ctx->d_cmd,
+                                ctx->mail, ctx->gate_timeout,
                                 ctx->d_ptimes, 0, Ax, ctx->host_rows ? ctx->d_rows : nullptr, nsrv, ctx->srv_waves,
-                                ctx->stream));
+                                ctx->bar_cmd ? nsrv : 1, ctx->stream));
         ctx->srv_live = true;
       }
       const double t_pub = ctx->h_ptimes ? now_ms() : 0.0;
       if (ctx->h_ptimes && ctx->ht_last_rows > 0 && t_pub - ctx->ht_last_rows < 1.0) {
         ctx->ht_host += t_pub - ctx->ht_last_rows;
+        ctx->ht_bfgs += t_entry - ctx->ht_last_rows;
         ++ctx->ht_nh;
       }
       publish_cmd(ctx, seq, kPassRun, 0, &Ax);
@@ -1392,6 +1422,7 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
   if (const char* rs = std::getenv("MGICP_RESIDENT")) ctx->resident = std::atoi(rs) != 0;
   if (const char* hr = std::getenv("MGICP_HOST_ROWS")) ctx->host_rows = std::atoi(hr) != 0;
   if (const char* sw = std::getenv("MGICP_SRV_WAVES")) ctx->srv_waves = std::atoi(sw) == 8 ? 8 : 4;
+  if (const char* bc = std::getenv("MGICP_BAR_CMD")) ctx->bar = std::atoi(bc) != 0;
   ctx->knn_logged = knn_logged_enabled();
   if (const char* st = std::getenv("MGICP_SPLIT_TARGET_COV")) ctx->split_target_cov = std::atoi(st) != 0;
   if (const char* ps = std::getenv("MGICP_PROF_STRIDE")) ctx->prof_stride = std::max(1, std::atoi(ps));
@@ -1438,6 +1469,8 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
     ctx->cus = 0;  // no resident server
   ctx->tgt.want_empty_map = true;  // correspondence / fitness queries start off the surface
   if (const char* em = std::getenv("MGICP_EMPTY_MAP")) ctx->tgt.want_empty_map = std::atoi(em) != 0;
+  ctx->tgt.want_seed_map = true;  // first 1-NN sweep seeded from a nearest non-empty cell
+  if (const char* sm = std::getenv("MGICP_SEED_MAP")) ctx->tgt.want_seed_map = std::atoi(sm) != 0;
   // per-cell point boxes in the 1-NN sweeps: exact and 1.75x fewer candidates in sweep 1, but the
   // per-cell box loads and tests cost more than they save (C4 correspondence 1.39 vs 1.11 ms,
   // profiles/r02/ab_boxes): off by default, knob MGICP_CELL_BOXES=1
@@ -1489,6 +1522,7 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   for (Cloud* c : {&ctx->src, &ctx->tgt, &ctx->aux, &ctx->qry}) {
     c->raw.release(); c->orig.release(); c->pts.release(); c->perm.release();
     c->cell_start.release(); c->cov.release(); c->empty_dist.release(); c->boxes.release();
+    c->seed.release(); c->seed_scratch.release();
   }
   ctx->src_out.release();
   ctx->qperm.release();
@@ -1508,6 +1542,7 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   if (ctx->h_gtrace) (void)hipHostFree(ctx->h_gtrace);
   if (ctx->h_ptimes) (void)hipHostFree(ctx->h_ptimes);
   if (ctx->h_rows) (void)hipHostFree(ctx->h_rows);
+  if (ctx->bar_cmd) (void)hipFree(ctx->bar_cmd);
   if (ctx->h_small) (void)hipHostFree(ctx->h_small);
   prof_resolve(ctx);
   for (hipEvent_t e : ctx->pool) (void)hipEventDestroy(e);
@@ -1632,9 +1667,10 @@ int mgicp_align(mgicp_ctx* ctx, const float guess_cm[16], float out_T_cm[16], mg
       std::fprintf(stderr, "[pass-times] passes %d | active %.2f us | finish -> next gate exit %.2f us (%d)\n", na,
                    act / na, ng ? gap / ng : 0.0, ng);
     if (ctx->ht_n)
-      std::fprintf(stderr, "[pass-times] host view: %d passes | command -> rows complete %.2f us | rows -> next command %.2f us\n",
-                   ctx->ht_n, 1e3 * ctx->ht_dev / ctx->ht_n, ctx->ht_nh ? 1e3 * ctx->ht_host / ctx->ht_nh : 0.0);
-    ctx->ht_dev = ctx->ht_host = ctx->ht_last_rows = 0;
+      std::fprintf(stderr, "[pass-times] host view: %d passes | command -> rows complete %.2f us | rows -> next command %.2f us (BFGS step until the next pass %.2f us)\n",
+                   ctx->ht_n, 1e3 * ctx->ht_dev / ctx->ht_n, ctx->ht_nh ? 1e3 * ctx->ht_host / ctx->ht_nh : 0.0,
+                   ctx->ht_nh ? 1e3 * ctx->ht_bfgs / ctx->ht_nh : 0.0);
+    ctx->ht_dev = ctx->ht_host = ctx->ht_bfgs = ctx->ht_last_rows = 0;
     ctx->ht_n = ctx->ht_nh = 0;
     std::memset(ctx->h_ptimes, 0, 2 * 1024 * sizeof(unsigned long long));
   }
@@ -2115,7 +2151,7 @@ int mgicp_debug_pass_bench(mgicp_ctx* ctx, const double x[6], int npasses, int m
     const unsigned long long seq0 = ++ctx->pass_seq;
     e = launch_fdf_server(c, ctx->cpos.p, ctx->chunk_base.p, ns, ctx->partial.p, ctx->spart.p, ctx->tickets.p,
                           ctx->d_h_red, ctx->d_flag, seq0, ctx->d_cmd, ctx->mail, ctx->gate_timeout, ctx->d_ptimes,
-                          npasses, A, nullptr, nb, ctx->srv_waves, ctx->stream);
+                          npasses, A, nullptr, nb, ctx->srv_waves, 1, ctx->stream);
     ctx->pass_seq = seq0 + static_cast<unsigned long long>(npasses);  // the closing cancel's stamp too
   } else {
     const int nb = fdf_grid_blocks(ns, ctx->fdf_max_blocks);

@@ -27,6 +27,9 @@ struct GridView {
   // optional empty-space map: per cell, the Chebyshev distance (in cells) to the nearest
   // non-empty cell, capped at kEmptyCap + 1; rings closer than it hold no point
   const uint8_t* empty_dist;
+  // optional seed map (with empty_dist): per cell within the cap, the sorted position of a point in
+  // a Chebyshev-nearest non-empty cell -- a real candidate that seeds an unseeded 1-NN search
+  const uint32_t* seed;
   // optional per-cell point boxes (2 float4 per cell: min xyz | bits(start), max xyz | bits(end));
   // 1-NN searches skip cells whose point box lies beyond their bound
   const float4* boxes;
@@ -163,7 +166,7 @@ hipError_t launch_fdf_server(const CorrSoA& c, const uint32_t* pos, const uint32
                              unsigned long long timeout_ticks, unsigned long long* ptimes /*nullable*/,
                              int bench_passes, Xf34 A,
                              unsigned long long* host_rows /*nullable: super rows to the host*/, int nb,
-                             int waves, hipStream_t s);
+                             int waves, int pollers /*blocks reading cmd themselves (1 or nb)*/, hipStream_t s);
 
 // super partials of nch chunk partials of nv (kRedVals or kMomVals) values
 hipError_t launch_super_reduce(const double* chunk, int nch, int nv, double* sup, hipStream_t s);
@@ -229,6 +232,7 @@ hipError_t launch_cell_boxes(const float4* pts, const uint32_t* cell_start, size
                              hipStream_t s);
 // empty-space distance map of a grid (3 separable capped min-max passes); scratch: nc bytes
 hipError_t launch_empty_map(const uint32_t* cell_start, int nx, int ny, int nz, uint8_t* out,
-                            uint8_t* scratch, hipStream_t s);
+                            uint8_t* scratch, hipStream_t s,
+                            uint32_t* seed = nullptr /*nullable: nc entries*/, uint32_t* seed_scratch = nullptr);
 
 }  // namespace mgicp

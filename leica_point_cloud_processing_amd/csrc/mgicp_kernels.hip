@@ -521,25 +521,41 @@ __global__ void xform_points_kernel(const float4* in, size_t n, Xf34 T, float4* 
   out[i] = make_float4(x, y, z, p.w);
 }
 
-// empty-space map, pass 0: 0 for non-empty cells, 255 for empty ones
-__global__ void empty_init_kernel(const uint32_t* __restrict__ cs, size_t nc, uint8_t* __restrict__ e) {
+// empty-space map, pass 0: 0 for non-empty cells, 255 for empty ones; with `seed`, a non-empty
+// cell's seed is its first sorted position (an empty cell's is undefined until a pass sets it)
+__global__ void empty_init_kernel(const uint32_t* __restrict__ cs, size_t nc, uint8_t* __restrict__ e,
+                                  uint32_t* __restrict__ seed) {
   const size_t c = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (c < nc) e[c] = cs[c + 1] > cs[c] ? 0 : 255;
+  if (c >= nc) return;
+  const bool full = cs[c + 1] > cs[c];
+  e[c] = full ? 0 : 255;
+  if (seed) seed[c] = full ? cs[c] : 0xffffffffu;
 }
 
 // one separable pass of the Chebyshev (L-inf) distance transform along an axis of extent n and
-// element stride `stride`: out(c) = min_{|d| <= cap} max(|d|, in(c + d*stride)), capped at cap+1
+// element stride `stride`: out(c) = min_{|d| <= cap} max(|d|, in(c + d*stride)), capped at cap+1.
+// With seeds, the seed of the winning cell travels along (first winner in |d|, minus side first),
+// so the final seed lies in a Chebyshev-nearest non-empty cell
 __global__ void empty_pass_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
-                                  size_t nc, int n, size_t stride, int cap) {
+                                  size_t nc, int n, size_t stride, int cap, const uint32_t* __restrict__ sin,
+                                  uint32_t* __restrict__ sout) {
   const size_t c = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (c >= nc) return;
   const int x = static_cast<int>((c / stride) % static_cast<size_t>(n));
   int best = min(static_cast<int>(in[c]), cap + 1);
+  size_t arg = c;
   for (int d = 1; d <= cap && d < best; ++d) {
-    if (x - d >= 0) best = min(best, max(d, static_cast<int>(in[c - d * stride])));
-    if (x + d < n) best = min(best, max(d, static_cast<int>(in[c + d * stride])));
+    if (x - d >= 0) {
+      const int v = max(d, static_cast<int>(in[c - d * stride]));
+      if (v < best) { best = v; arg = c - d * stride; }
+    }
+    if (x + d < n) {
+      const int v = max(d, static_cast<int>(in[c + d * stride]));
+      if (v < best) { best = v; arg = c + d * stride; }
+    }
   }
   out[c] = static_cast<uint8_t>(min(best, cap + 1));
+  if (sout) sout[c] = best <= cap ? sin[arg] : 0xffffffffu;
 }
 
 // per-cell point boxes: boxes[2c] = (min x, min y, min z, bits(start)), boxes[2c + 1] =
@@ -880,6 +896,15 @@ __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_kernel(GridV
     // and the ball-cell pruning starts from a near-final radius
     const uint32_t pp = nn_pos[p - p0];
     if (pp != 0xffffffffu) vis.range(tg, pp, pp + 1);
+  } else if (tg.seed) {
+    // first sweep: a point of a Chebyshev-nearest non-empty cell (seed map) -- any real candidate
+    // keeps the search exact and lets box_search prune from its first row
+    const int cx = qcell(qx, tg.ox, tg.inv_h), cy = qcell(qy, tg.oy, tg.inv_h), cz = qcell(qz, tg.oz, tg.inv_h);
+    if (cx >= 0 && cx < tg.nx && cy >= 0 && cy < tg.ny && cz >= 0 && cz < tg.nz) {
+      const uint32_t pp = tg.seed[static_cast<size_t>(cx) +
+                                  static_cast<size_t>(tg.nx) * (static_cast<size_t>(cy) + static_cast<size_t>(tg.ny) * cz)];
+      if (pp != 0xffffffffu) vis.range(tg, pp, pp + 1);
+    }
   }
   if (tg.boxes) ring_search_boxed(tg, qx, qy, qz, vis);
   else if (kSeedBox && vis.best != ~0ull) box_search(tg, qx, qy, qz, vis);
@@ -1479,7 +1504,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void fdf_server_kernel(
     double* __restrict__ partial, double* __restrict__ spart, unsigned int* __restrict__ tickets,
     double* __restrict__ out, unsigned long long* done_flag, unsigned long long seq0, const PassCmd* cmd,
     PassCmd* mail, unsigned long long timeout, unsigned long long* ptimes, int bench_passes, Xf34 Abench,
-    unsigned long long* host_rows) {
+    unsigned long long* host_rows, int pollers) {
   constexpr int kR = SrvShape<kWaves>::kReg, kL = SrvShape<kWaves>::kLds;
   static_assert(kR <= 4 && (kR == 4 || kR + kL <= 4), "resident groups: chunk 0, then chunk 1 only after a full chunk 0");
   __shared__ float4 lf[kWaves][kL][6][64];
@@ -1526,7 +1551,10 @@ __global__ __launch_bounds__(64 * kWaves, 1) void fdf_server_kernel(
     for (int q = 0; q < 12; ++q) g.d[q] = ld[wid][k][q][lane];
     fdf_group(A, g, acc);
   };
-  const int host_pollers = kBench ? 0 : 1;
+  // pollers: blocks [0, pollers) read the command block themselves (system-coherent loads); the
+  // others poll the mailbox block 0 forwards to.  1 = the host's pinned copy (PCIe reads by one
+  // block); gridDim = a command block the host stores straight into device memory (BAR)
+  const int host_pollers = kBench ? 0 : pollers;
   for (unsigned long long seq = seq0;; ++seq) {
     Xf34 A = Abench;
     int rev = 0;
@@ -1965,15 +1993,21 @@ hipError_t launch_xform_points(const float4* in, size_t n, Xf34 T, float4* out, 
 }
 
 hipError_t launch_empty_map(const uint32_t* cell_start, int nx, int ny, int nz, uint8_t* out,
-                            uint8_t* scratch, hipStream_t s) {
+                            uint8_t* scratch, hipStream_t s, uint32_t* seed, uint32_t* seed_scratch) {
   const size_t nc = static_cast<size_t>(nx) * ny * nz;
   if (!nc) return hipSuccess;
-  empty_init_kernel<<<nblk(nc), 256, 0, s>>>(cell_start, nc, out);
-  empty_pass_kernel<<<nblk(nc), 256, 0, s>>>(out, scratch, nc, nx, 1, kEmptyCap);
-  empty_pass_kernel<<<nblk(nc), 256, 0, s>>>(scratch, out, nc, ny, static_cast<size_t>(nx), kEmptyCap);
-  empty_pass_kernel<<<nblk(nc), 256, 0, s>>>(out, scratch, nc, nz, static_cast<size_t>(nx) * ny, kEmptyCap);
+  uint32_t* s2 = seed ? seed_scratch : nullptr;
+  empty_init_kernel<<<nblk(nc), 256, 0, s>>>(cell_start, nc, out, seed);
+  empty_pass_kernel<<<nblk(nc), 256, 0, s>>>(out, scratch, nc, nx, 1, kEmptyCap, seed, s2);
+  empty_pass_kernel<<<nblk(nc), 256, 0, s>>>(scratch, out, nc, ny, static_cast<size_t>(nx), kEmptyCap, s2, seed);
+  empty_pass_kernel<<<nblk(nc), 256, 0, s>>>(out, scratch, nc, nz, static_cast<size_t>(nx) * ny, kEmptyCap, seed,
+                                             s2);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+  if (seed) {
+    e = hipMemcpyAsync(seed, s2, nc * sizeof(uint32_t), hipMemcpyDeviceToDevice, s);
+    if (e != hipSuccess) return e;
+  }
   return hipMemcpyAsync(out, scratch, nc, hipMemcpyDeviceToDevice, s);
 }
 
@@ -2107,7 +2141,8 @@ hipError_t launch_fdf_server(const CorrSoA& c, const uint32_t* pos, const uint32
                              double* spart, unsigned int* tickets, double* out, unsigned long long* done_flag,
                              unsigned long long seq0, const PassCmd* cmd, PassCmd* mail,
                              unsigned long long timeout_ticks, unsigned long long* ptimes, int bench_passes,
-                             Xf34 A, unsigned long long* host_rows, int nb, int waves, hipStream_t s) {
+                             Xf34 A, unsigned long long* host_rows, int nb, int waves, int pollers,
+                             hipStream_t s) {
   int nch = chunk_count(ns);
   if (nch == 0 || nb <= 0 || (waves != 4 && waves != 8)) return hipErrorInvalidValue;
   // every block must be resident at once (the blocks wait on each other's commands): refuse a grid
@@ -2127,7 +2162,8 @@ hipError_t launch_fdf_server(const CorrSoA& c, const uint32_t* pos, const uint32
   if (per_cu < 1 || static_cast<long long>(per_cu) * cus < nb) return hipErrorCooperativeLaunchTooLarge;
 #define MGICP_SRV_LAUNCH(B, W)                                                                                  \
   fdf_server_kernel<B, W><<<nb, 64 * (W), 0, s>>>(c, pos, base, ns, nch, partial, spart, tickets, out, done_flag, \
-                                                  seq0, cmd, mail, timeout_ticks, ptimes, bench_passes, A, host_rows)
+                                                  seq0, cmd, mail, timeout_ticks, ptimes, bench_passes, A, host_rows, \
+                                                  pollers)
   if (waves == 4) {
     if (b) MGICP_SRV_LAUNCH(true, 4);
     else MGICP_SRV_LAUNCH(false, 4);
