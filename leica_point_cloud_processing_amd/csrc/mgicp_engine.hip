@@ -330,10 +330,11 @@ struct mgicp_ctx {
   unsigned long long* d_rows = nullptr;
   size_t rows_cap = 0;                  // supers
   std::vector<double> row_sums;         // decoded super partials
+  bool spin_pause = false;              // env MGICP_SPIN_PAUSE: pause instruction in the row spin
   // MGICP_PASS_TIMES: host view of the server passes -- command published -> rows complete
   // (device pass + PCIe both ways) and rows complete -> next command (host BFGS step)
-  double ht_dev = 0, ht_host = 0, ht_bfgs = 0, ht_last_rows = 0;
-  int ht_n = 0, ht_nh = 0;
+  double ht_dev = 0, ht_host = 0, ht_bfgs = 0, ht_eval = 0, ht_last_rows = 0;
+  int ht_n = 0, ht_nh = 0, ht_ne = 0;
   // build scratch
   DevBuf<uint32_t> counts, keys, keys_sorted, vals;
   DevBuf<unsigned char> scratch;
@@ -922,6 +923,7 @@ int wait_rows(mgicp_ctx* ctx, unsigned long long seq, long long nsup, double out
       bool all = true;
       for (int w = 0; w < 32 && all; ++w) all = static_cast<unsigned int>(__atomic_load_n(row + w, __ATOMIC_ACQUIRE) >> 32) == st;
       if (all) break;
+      if (ctx->spin_pause) __builtin_ia32_pause();
       if ((spins & 1023u) == 1023u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(500)) {
         int rc = sync(ctx);
         if (rc) return rc;
@@ -1144,6 +1146,7 @@ struct DeviceFunctor {
       if (!ctx->srv_live) {
         cancel_gated(ctx);
         if (ctx->host_rows && (rc = ensure_rows(ctx, nsup))) return rc;
+        ctx->ht_last_rows = 0;  // host-view diagnostics: a new BFGS run, not a host step
         HIPCK(hipMemsetAsync(ctx->tickets.p, 0, ctx->tickets_n * sizeof(unsigned int), ctx->stream));
         ProfScope ps(ctx, kFamFdf);
         HIPCK(launch_fdf_server(c, ctx->cpos.p, ctx->chunk_base.p, ns, ctx->partial.p, ctx->spart.p,
@@ -1238,6 +1241,10 @@ struct DeviceFunctor {
     memo_x = x;
     memo_f = f;
     memo_g = g;
+    if (ctx->h_ptimes && ctx->ht_last_rows > 0) {
+      ctx->ht_eval += now_ms() - ctx->ht_last_rows;
+      ++ctx->ht_ne;
+    }
     return 0;
   }
 };
@@ -1423,6 +1430,7 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
   if (const char* hr = std::getenv("MGICP_HOST_ROWS")) ctx->host_rows = std::atoi(hr) != 0;
   if (const char* sw = std::getenv("MGICP_SRV_WAVES")) ctx->srv_waves = std::atoi(sw) == 8 ? 8 : 4;
   if (const char* bc = std::getenv("MGICP_BAR_CMD")) ctx->bar = std::atoi(bc) != 0;
+  if (const char* sp = std::getenv("MGICP_SPIN_PAUSE")) ctx->spin_pause = std::atoi(sp) != 0;
   ctx->knn_logged = knn_logged_enabled();
   if (const char* st = std::getenv("MGICP_SPLIT_TARGET_COV")) ctx->split_target_cov = std::atoi(st) != 0;
   if (const char* ps = std::getenv("MGICP_PROF_STRIDE")) ctx->prof_stride = std::max(1, std::atoi(ps));
@@ -1670,8 +1678,11 @@ int mgicp_align(mgicp_ctx* ctx, const float guess_cm[16], float out_T_cm[16], mg
       std::fprintf(stderr, "[pass-times] host view: %d passes | command -> rows complete %.2f us | rows -> next command %.2f us (BFGS step until the next pass %.2f us)\n",
                    ctx->ht_n, 1e3 * ctx->ht_dev / ctx->ht_n, ctx->ht_nh ? 1e3 * ctx->ht_host / ctx->ht_nh : 0.0,
                    ctx->ht_nh ? 1e3 * ctx->ht_bfgs / ctx->ht_nh : 0.0);
-    ctx->ht_dev = ctx->ht_host = ctx->ht_bfgs = ctx->ht_last_rows = 0;
-    ctx->ht_n = ctx->ht_nh = 0;
+    if (ctx->ht_ne)
+      std::fprintf(stderr, "[pass-times] host view: rows complete -> f, g of the pass ready %.2f us (%d)\n",
+                   1e3 * ctx->ht_eval / ctx->ht_ne, ctx->ht_ne);
+    ctx->ht_dev = ctx->ht_host = ctx->ht_bfgs = ctx->ht_eval = ctx->ht_last_rows = 0;
+    ctx->ht_n = ctx->ht_nh = ctx->ht_ne = 0;
     std::memset(ctx->h_ptimes, 0, 2 * 1024 * sizeof(unsigned long long));
   }
   // final_transformation_ = previous_transformation_ (3x3) * guess (3x3); t = prev t + guess t
