@@ -2152,6 +2152,10 @@ int mgicp_debug_pass_bench(mgicp_ctx* ctx, const double x[6], int npasses, int m
   HIPCK(hipEventCreate(&b));
   HIPCK(hipEventRecord(a, ctx->stream));
   hipError_t e = hipSuccess;
+  const long long nsup = ctx->nsup_local();
+  const bool rows = mode == 0 && ctx->host_rows;
+  if (rows && (rc = ensure_rows(ctx, nsup))) return rc;
+  if (rows) HIPCK(hipMemsetAsync(ctx->tickets.p, 0, ctx->tickets_n * sizeof(unsigned int), ctx->stream));
   if (mode == 0) {
     const int nb = fdf_server_blocks(ns, ctx->cus, ctx->srv_waves);
     if (nb <= 0) {
@@ -2162,7 +2166,7 @@ int mgicp_debug_pass_bench(mgicp_ctx* ctx, const double x[6], int npasses, int m
     const unsigned long long seq0 = ++ctx->pass_seq;
     e = launch_fdf_server(c, ctx->cpos.p, ctx->chunk_base.p, ns, ctx->partial.p, ctx->spart.p, ctx->tickets.p,
                           ctx->d_h_red, ctx->d_flag, seq0, ctx->d_cmd, ctx->mail, ctx->gate_timeout, ctx->d_ptimes,
-                          npasses, A, nullptr, nb, ctx->srv_waves, 1, ctx->stream);
+                          npasses, A, rows ? ctx->d_rows : nullptr, nb, ctx->srv_waves, 1, ctx->stream);
     ctx->pass_seq = seq0 + static_cast<unsigned long long>(npasses);  // the closing cancel's stamp too
   } else {
     const int nb = fdf_grid_blocks(ns, ctx->fdf_max_blocks);
@@ -2177,10 +2181,19 @@ int mgicp_debug_pass_bench(mgicp_ctx* ctx, const double x[6], int npasses, int m
   (void)hipEventDestroy(a);
   (void)hipEventDestroy(b);
   HIPCK(e);
-  if (__atomic_load_n(ctx->h_flag, __ATOMIC_ACQUIRE) != ctx->pass_seq - (mode == 0 ? 1 : 0))
-    return fail(ctx, MGICP_E_HIP, "pass bench: the last pass did not publish its sums");
+  if (rows) {
+    // the host-row tickets are left as multiples of the supers' sizes: re-arm them
+    HIPCK(hipMemsetAsync(ctx->tickets.p, 0, ctx->tickets_n * sizeof(unsigned int), ctx->stream));
+    double tot[kRedVals];
+    if ((rc = wait_rows(ctx, ctx->pass_seq - 1, nsup, tot))) return rc;
+    if ((rc = sync(ctx))) return rc;
+    if (out16) std::memcpy(out16, tot, kRedVals * sizeof(double));
+  } else {
+    if (__atomic_load_n(ctx->h_flag, __ATOMIC_ACQUIRE) != ctx->pass_seq - (mode == 0 ? 1 : 0))
+      return fail(ctx, MGICP_E_HIP, "pass bench: the last pass did not publish its sums");
+    if (out16) std::memcpy(out16, ctx->h_red, kRedVals * sizeof(double));
+  }
   if (out_ms) *out_ms = static_cast<double>(ms) / npasses;
-  if (out16) std::memcpy(out16, ctx->h_red, kRedVals * sizeof(double));
   return MGICP_OK;
 }
 

@@ -1332,12 +1332,14 @@ __device__ __forceinline__ void chunk_store(int j, double (&acc)[kRedVals], cons
 // host_rows (nullable, mapped host memory, 32 words per super): each super partial goes straight to
 // the host as one 256-byte store of stamped halves ((seq << 32) | 32-bit half, value v in words 2v
 // (low) and 2v + 1 (high)); the host takes the total in wave_total's order, so there is no global
-// ticket, device total or completion flag on the pass's critical path (returns false).
+// ticket, device total or completion flag on the pass's critical path (returns false).  chain
+// (timing form only): after its row, each super wave also takes a global ticket (modulo the super
+// count) and the wave completing the last super returns true, to forward the next command.
 __device__ __forceinline__ bool wave_tickets(int w0, int nw, int nch, int reverse, unsigned int* __restrict__ tickets,
                                              const double* __restrict__ partial, double* __restrict__ spart,
                                              double* __restrict__ out, unsigned long long* done_flag,
                                              unsigned long long seq, int lane,
-                                             unsigned long long* host_rows = nullptr) {
+                                             unsigned long long* host_rows = nullptr, bool chain = false) {
   const int nsup = (nch + kSuperChunks - 1) / kSuperChunks;
   // tickets, once per wave after all of its chunks (a per-chunk drain + atomic round trip cost
   // ~60 us per pass at 256 blocks): lane k takes the super of the wave's k-th chunk
@@ -1387,6 +1389,13 @@ __device__ __forceinline__ bool wave_tickets(int w0, int nw, int nch, int revers
         asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1" ::"v"(host_rows + static_cast<size_t>(sj) * 32 + lane),
                      "v"(w)
                      : "memory");
+      }
+      if (chain) {
+        int lastc = 0;
+        if (lane == 0)
+          lastc = __hip_atomic_fetch_add(tickets + nsup, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) %
+                          static_cast<unsigned>(nsup) == static_cast<unsigned>(nsup - 1) ? 1 : 0;
+        if (__shfl(lastc, 0, 64)) fin = true;
       }
       continue;
     }
@@ -1611,8 +1620,10 @@ __global__ __launch_bounds__(64 * kWaves, 1) void fdf_server_kernel(
       chunk_store(w, acc, pos, ns, partial, lane);
     }
     if (w0 >= nch) continue;
-    const bool fin = wave_tickets(w0, nw, nch, 0, tickets, partial, spart, out, done_flag, seq, lane,
-                                  kBench ? nullptr : host_rows);
+    // the timing form writes host rows too when given them (chained on the device by a global
+    // ticket), so it times the pass the aligns run
+    const bool fin = wave_tickets(w0, nw, nch, 0, tickets, partial, spart, out, done_flag, seq, lane, host_rows,
+                                  kBench && host_rows);
     if (fin && lane == 0) {
       if (ptimes) ptimes[2 * (seq & 1023) + 1] = wall_clock64();
       if (kBench) {
