@@ -379,9 +379,11 @@ def main():
     roofline["launches"] = n_evals
     if srv is not None:
         roofline["timing"] = (f"HIP events on the engine stream around {srv['launches']} server launches of "
-                              f"{srv['passes_per_launch']} back-to-back passes each (mgicp_debug_pass_bench mode 0) "
-                              "over the last timed align's correspondences; ~31 % of the bytes are register / "
-                              "LDS resident, the rest stream from HBM / Infinity Cache")
+                              f"{srv['passes_per_launch']} back-to-back passes each (mgicp_debug_pass_bench mode 0: "
+                              "the aligns' pass -- super partials to host rows -- chained on the device by a "
+                              "global ticket instead of the host's next command) over the last timed align's "
+                              "correspondences; ~31 % of the bytes are register / LDS resident, the rest stream "
+                              "from HBM / Infinity Cache")
         roofline["server"] = srv
     else:
         roofline["timing"] = ("HIP events on the engine stream around every 8th objective pass of the timed region "

@@ -30,6 +30,9 @@
 #ifndef MGICP_CORR_STATS
 #define MGICP_CORR_STATS 0  // 1: count 1-NN work per sweep (diagnostic builds only)
 #endif
+#ifndef MGICP_PACKED_RESID
+#define MGICP_PACKED_RESID 0  // 1: objective-pass residuals two per packed fp32 instruction (A/B: no gain, more spills; profiles/r02/ab_server)
+#endif
 #ifndef MGICP_SEED_BOX
 #define MGICP_SEED_BOX 1  // seeded 1-NN queries search the cube of their seed's ball (box_search)
 #endif
@@ -1218,6 +1221,41 @@ __device__ __forceinline__ void fdf_point(const Xf34& A, float sx, float sy, flo
   acc[10] += dz * t0; acc[11] += dz * t1; acc[12] += dz * t2;
 }
 
+// the fp64 part of fdf_point for a residual r = fp32(A s - q) already widened to fp64
+__device__ __forceinline__ void fdf_point_r(double r0, double r1, double r2, float sx, float sy, float sz,
+                                            double m00, double m01, double m02, double m11, double m12,
+                                            double m22, double (&acc)[kRedVals]) {
+  double t0 = m00 * r0; t0 = t0 + m01 * r1; t0 = t0 + m02 * r2;
+  double t1 = m01 * r0; t1 = t1 + m11 * r1; t1 = t1 + m12 * r2;
+  double t2 = m02 * r0; t2 = t2 + m12 * r1; t2 = t2 + m22 * r2;
+  double d = r0 * t0; d = d + r1 * t1; d = d + r2 * t2;
+  const double dx = sx, dy = sy, dz = sz;
+  acc[0] += d;
+  acc[1] += t0; acc[2] += t1; acc[3] += t2;
+  acc[4] += dx * t0; acc[5] += dx * t1; acc[6] += dx * t2;
+  acc[7] += dy * t0; acc[8] += dy * t1; acc[9] += dy * t2;
+  acc[10] += dz * t0; acc[11] += dz * t1; acc[12] += dz * t2;
+}
+
+// Eigen's Matrix4f * Vector4f for two points at once (packed fp32, v_pk_mul_f32 / v_pk_add_f32):
+// element-wise the same roundings as xform, half the fp32 instructions
+typedef float pf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void resid2(const Xf34& T, pf2 x, pf2 y, pf2 z, pf2 qx, pf2 qy, pf2 qz, pf2& rx,
+                                       pf2& ry, pf2& rz) {
+  pf2 a = T.m[0] * x;
+  a = a + T.m[1] * y;
+  a = a + T.m[2] * z;
+  rx = (a + T.m[3]) - qx;
+  pf2 b = T.m[4] * x;
+  b = b + T.m[5] * y;
+  b = b + T.m[6] * z;
+  ry = (b + T.m[7]) - qy;
+  pf2 c = T.m[8] * x;
+  c = c + T.m[9] * y;
+  c = c + T.m[10] * z;
+  rz = (c + T.m[11]) - qz;
+}
+
 // 4 consecutive correspondences of the compacted streams (one 16-byte load per stream and lane):
 // f = sx sy sz qx qy qz (float4 of 4 coordinates), d = m00 m00' m01 m01' m02 m02' m11 m11' m12 m12'
 // m22 m22' (double2 of 2 matrix entries) -- 72 dwords
@@ -1243,8 +1281,23 @@ __device__ __forceinline__ void load_group(const CorrSoA& c, uint32_t i, CorrGro
   }
 }
 
-// the group's 4 correspondences in stream order
+// the group's 4 correspondences in stream order (residuals two at a time in packed fp32)
 __device__ __forceinline__ void fdf_group(const Xf34& A, const CorrGroup& g, double (&acc)[kRedVals]) {
+#if MGICP_PACKED_RESID
+  pf2 rx01, ry01, rz01, rx23, ry23, rz23;
+  resid2(A, pf2{g.f[0].x, g.f[0].y}, pf2{g.f[1].x, g.f[1].y}, pf2{g.f[2].x, g.f[2].y}, pf2{g.f[3].x, g.f[3].y},
+         pf2{g.f[4].x, g.f[4].y}, pf2{g.f[5].x, g.f[5].y}, rx01, ry01, rz01);
+  resid2(A, pf2{g.f[0].z, g.f[0].w}, pf2{g.f[1].z, g.f[1].w}, pf2{g.f[2].z, g.f[2].w}, pf2{g.f[3].z, g.f[3].w},
+         pf2{g.f[4].z, g.f[4].w}, pf2{g.f[5].z, g.f[5].w}, rx23, ry23, rz23);
+  fdf_point_r(rx01.x, ry01.x, rz01.x, g.f[0].x, g.f[1].x, g.f[2].x, g.d[0].x, g.d[2].x, g.d[4].x, g.d[6].x,
+              g.d[8].x, g.d[10].x, acc);
+  fdf_point_r(rx01.y, ry01.y, rz01.y, g.f[0].y, g.f[1].y, g.f[2].y, g.d[0].y, g.d[2].y, g.d[4].y, g.d[6].y,
+              g.d[8].y, g.d[10].y, acc);
+  fdf_point_r(rx23.x, ry23.x, rz23.x, g.f[0].z, g.f[1].z, g.f[2].z, g.d[1].x, g.d[3].x, g.d[5].x, g.d[7].x,
+              g.d[9].x, g.d[11].x, acc);
+  fdf_point_r(rx23.y, ry23.y, rz23.y, g.f[0].w, g.f[1].w, g.f[2].w, g.d[1].y, g.d[3].y, g.d[5].y, g.d[7].y,
+              g.d[9].y, g.d[11].y, acc);
+#else
   fdf_point(A, g.f[0].x, g.f[1].x, g.f[2].x, g.f[3].x, g.f[4].x, g.f[5].x, g.d[0].x, g.d[2].x, g.d[4].x,
             g.d[6].x, g.d[8].x, g.d[10].x, acc);
   fdf_point(A, g.f[0].y, g.f[1].y, g.f[2].y, g.f[3].y, g.f[4].y, g.f[5].y, g.d[0].y, g.d[2].y, g.d[4].y,
@@ -1253,6 +1306,7 @@ __device__ __forceinline__ void fdf_group(const Xf34& A, const CorrGroup& g, dou
             g.d[7].x, g.d[9].x, g.d[11].x, acc);
   fdf_point(A, g.f[0].w, g.f[1].w, g.f[2].w, g.f[3].w, g.f[4].w, g.f[5].w, g.d[1].y, g.d[3].y, g.d[5].y,
             g.d[7].y, g.d[9].y, g.d[11].y, acc);
+#endif
 }
 
 // The gate of a pass whose state is not known at launch (pre-launched gated passes and the
