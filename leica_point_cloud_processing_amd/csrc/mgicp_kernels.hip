@@ -30,6 +30,9 @@
 #ifndef MGICP_CORR_STATS
 #define MGICP_CORR_STATS 0  // 1: count 1-NN work per sweep (diagnostic builds only)
 #endif
+#ifndef MGICP_SEED_BOTH
+#define MGICP_SEED_BOTH 1  // seeded 1-NN sweeps also test the seed map's candidate (the nearer one wins)
+#endif
 #ifndef MGICP_PACKED_RESID
 #define MGICP_PACKED_RESID 0  // 1: objective-pass residuals two per packed fp32 instruction (A/B: no gain, more spills; profiles/r02/ab_server)
 #endif
@@ -899,9 +902,12 @@ __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_kernel(GridV
     // and the ball-cell pruning starts from a near-final radius
     const uint32_t pp = nn_pos[p - p0];
     if (pp != 0xffffffffu) vis.range(tg, pp, pp + 1);
-  } else if (tg.seed) {
-    // first sweep: a point of a Chebyshev-nearest non-empty cell (seed map) -- any real candidate
-    // keeps the search exact and lets box_search prune from its first row
+  }
+  if ((!seeded || MGICP_SEED_BOTH) && tg.seed) {
+    // a point of a Chebyshev-nearest non-empty cell (seed map): the first sweep's seed, and in later
+    // sweeps a second candidate beside the last match (queries move by up to centimetres after the
+    // first BFGS run) -- any real candidate keeps the search exact and lets box_search prune from
+    // its first row
     const int cx = qcell(qx, tg.ox, tg.inv_h), cy = qcell(qy, tg.oy, tg.inv_h), cz = qcell(qz, tg.oz, tg.inv_h);
     if (cx >= 0 && cx < tg.nx && cy >= 0 && cy < tg.ny && cz >= 0 && cz < tg.nz) {
       const uint32_t pp = tg.seed[static_cast<size_t>(cx) +
