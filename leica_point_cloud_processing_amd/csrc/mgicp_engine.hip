@@ -703,7 +703,8 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
       HIPCK(cl.seed_scratch.reserve(nc));
     }
     HIPCK(launch_empty_map(cl.cell_start.p, nd[0], nd[1], nd[2], cl.empty_dist.p, ctx->scratch.p, s,
-                           cl.want_seed_map ? cl.seed.p : nullptr, cl.want_seed_map ? cl.seed_scratch.p : nullptr));
+                           cl.want_seed_map ? cl.seed.p : nullptr, cl.want_seed_map ? cl.seed_scratch.p : nullptr,
+                           &g));
     if ((rc = sync(ctx))) return rc;
     MGICP_TRACE_AT("grid: empty map done");
     g.empty_dist = cl.empty_dist.p;

@@ -233,6 +233,7 @@ hipError_t launch_cell_boxes(const float4* pts, const uint32_t* cell_start, size
 // empty-space distance map of a grid (3 separable capped min-max passes); scratch: nc bytes
 hipError_t launch_empty_map(const uint32_t* cell_start, int nx, int ny, int nz, uint8_t* out,
                             uint8_t* scratch, hipStream_t s,
-                            uint32_t* seed = nullptr /*nullable: nc entries*/, uint32_t* seed_scratch = nullptr);
+                            uint32_t* seed = nullptr /*nullable: nc entries*/, uint32_t* seed_scratch = nullptr,
+                            const GridView* g = nullptr /*with seed: each cell's point nearest its centre*/);
 
 }  // namespace mgicp

@@ -30,6 +30,9 @@
 #ifndef MGICP_CORR_STATS
 #define MGICP_CORR_STATS 0  // 1: count 1-NN work per sweep (diagnostic builds only)
 #endif
+#ifndef MGICP_SEED_NEIGHBOURS
+#define MGICP_SEED_NEIGHBOURS 1  // the first 1-NN sweep tests the seeds of the query's cell and its 6 face neighbours
+#endif
 #ifndef MGICP_SEED_BOTH
 #define MGICP_SEED_BOTH 1  // seeded 1-NN sweeps also test the seed map's candidate (the nearer one wins)
 #endif
@@ -530,12 +533,30 @@ __global__ void xform_points_kernel(const float4* in, size_t n, Xf34 T, float4* 
 // empty-space map, pass 0: 0 for non-empty cells, 255 for empty ones; with `seed`, a non-empty
 // cell's seed is its first sorted position (an empty cell's is undefined until a pass sets it)
 __global__ void empty_init_kernel(const uint32_t* __restrict__ cs, size_t nc, uint8_t* __restrict__ e,
-                                  uint32_t* __restrict__ seed) {
+                                  uint32_t* __restrict__ seed, const float4* __restrict__ pts, int nx, int ny,
+                                  float ox, float oy, float oz, float h) {
   const size_t c = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (c >= nc) return;
-  const bool full = cs[c + 1] > cs[c];
+  const uint32_t a = cs[c], b = cs[c + 1];
+  const bool full = b > a;
   e[c] = full ? 0 : 255;
-  if (seed) seed[c] = full ? cs[c] : 0xffffffffu;
+  if (!seed) return;
+  uint32_t best = full ? a : 0xffffffffu;
+  if (full && pts) {
+    // the cell's point nearest to the cell centre: a better seed than an arbitrary one for every
+    // query that lands in or near the cell
+    const int x = static_cast<int>(c % static_cast<size_t>(nx));
+    const int y = static_cast<int>((c / static_cast<size_t>(nx)) % static_cast<size_t>(ny));
+    const int z = static_cast<int>(c / (static_cast<size_t>(nx) * ny));
+    const float cx = ox + (static_cast<float>(x) + 0.5f) * h, cy = oy + (static_cast<float>(y) + 0.5f) * h,
+                cz = oz + (static_cast<float>(z) + 0.5f) * h;
+    float bd = INFINITY;
+    for (uint32_t j = a; j < b; ++j) {
+      const float d = dist2(cx, cy, cz, pts[j]);
+      if (d < bd) { bd = d; best = j; }
+    }
+  }
+  seed[c] = best;
 }
 
 // one separable pass of the Chebyshev (L-inf) distance transform along an axis of extent n and
@@ -904,15 +925,33 @@ __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_kernel(GridV
     if (pp != 0xffffffffu) vis.range(tg, pp, pp + 1);
   }
   if ((!seeded || MGICP_SEED_BOTH) && tg.seed) {
-    // a point of a Chebyshev-nearest non-empty cell (seed map): the first sweep's seed, and in later
-    // sweeps a second candidate beside the last match (queries move by up to centimetres after the
-    // first BFGS run) -- any real candidate keeps the search exact and lets box_search prune from
-    // its first row
-    const int cx = qcell(qx, tg.ox, tg.inv_h), cy = qcell(qy, tg.oy, tg.inv_h), cz = qcell(qz, tg.oz, tg.inv_h);
-    if (cx >= 0 && cx < tg.nx && cy >= 0 && cy < tg.ny && cz >= 0 && cz < tg.nz) {
-      const uint32_t pp = tg.seed[static_cast<size_t>(cx) +
-                                  static_cast<size_t>(tg.nx) * (static_cast<size_t>(cy) + static_cast<size_t>(tg.ny) * cz)];
-      if (pp != 0xffffffffu) vis.range(tg, pp, pp + 1);
+#if MGICP_SEED_NEIGHBOURS
+    if (!seeded) {
+      // the first sweep: the seeds of the query's cell and its 6 face neighbours, the nearest wins
+      const int cx = qcell(qx, tg.ox, tg.inv_h), cy = qcell(qy, tg.oy, tg.inv_h), cz = qcell(qz, tg.oz, tg.inv_h);
+      const int dd[7][3] = {{0, 0, 0}, {-1, 0, 0}, {1, 0, 0}, {0, -1, 0}, {0, 1, 0}, {0, 0, -1}, {0, 0, 1}};
+#pragma unroll
+      for (int k = 0; k < 7; ++k) {
+        const int x = cx + dd[k][0], y = cy + dd[k][1], z = cz + dd[k][2];
+        if (x >= 0 && x < tg.nx && y >= 0 && y < tg.ny && z >= 0 && z < tg.nz) {
+          const uint32_t pp = tg.seed[static_cast<size_t>(x) +
+                                      static_cast<size_t>(tg.nx) * (static_cast<size_t>(y) + static_cast<size_t>(tg.ny) * z)];
+          if (pp != 0xffffffffu) vis.range(tg, pp, pp + 1);
+        }
+      }
+    } else
+#endif
+    {
+      // a point of a Chebyshev-nearest non-empty cell (seed map): the first sweep's seed, and in
+      // later sweeps a second candidate beside the last match (queries move by up to centimetres
+      // after the first BFGS run) -- any real candidate keeps the search exact and lets box_search
+      // prune from its first row
+      const int cx = qcell(qx, tg.ox, tg.inv_h), cy = qcell(qy, tg.oy, tg.inv_h), cz = qcell(qz, tg.oz, tg.inv_h);
+      if (cx >= 0 && cx < tg.nx && cy >= 0 && cy < tg.ny && cz >= 0 && cz < tg.nz) {
+        const uint32_t pp = tg.seed[static_cast<size_t>(cx) +
+                                    static_cast<size_t>(tg.nx) * (static_cast<size_t>(cy) + static_cast<size_t>(tg.ny) * cz)];
+        if (pp != 0xffffffffu) vis.range(tg, pp, pp + 1);
+      }
     }
   }
   if (tg.boxes) ring_search_boxed(tg, qx, qy, qz, vis);
@@ -2064,11 +2103,13 @@ hipError_t launch_xform_points(const float4* in, size_t n, Xf34 T, float4* out, 
 }
 
 hipError_t launch_empty_map(const uint32_t* cell_start, int nx, int ny, int nz, uint8_t* out,
-                            uint8_t* scratch, hipStream_t s, uint32_t* seed, uint32_t* seed_scratch) {
+                            uint8_t* scratch, hipStream_t s, uint32_t* seed, uint32_t* seed_scratch,
+                            const GridView* g) {
   const size_t nc = static_cast<size_t>(nx) * ny * nz;
   if (!nc) return hipSuccess;
   uint32_t* s2 = seed ? seed_scratch : nullptr;
-  empty_init_kernel<<<nblk(nc), 256, 0, s>>>(cell_start, nc, out, seed);
+  empty_init_kernel<<<nblk(nc), 256, 0, s>>>(cell_start, nc, out, seed, g ? g->pts : nullptr, nx, ny,
+                                             g ? g->ox : 0.f, g ? g->oy : 0.f, g ? g->oz : 0.f, g ? g->h : 0.f);
   empty_pass_kernel<<<nblk(nc), 256, 0, s>>>(out, scratch, nc, nx, 1, kEmptyCap, seed, s2);
   empty_pass_kernel<<<nblk(nc), 256, 0, s>>>(scratch, out, nc, ny, static_cast<size_t>(nx), kEmptyCap, s2, seed);
   empty_pass_kernel<<<nblk(nc), 256, 0, s>>>(out, scratch, nc, nz, static_cast<size_t>(nx) * ny, kEmptyCap, seed,
