@@ -68,7 +68,7 @@ def parse():
     ap.add_argument("--oracle-full", type=int, default=1,
                     help="1 = run the oracle on the full workload with all usable host cores "
                          "(all-core CPU baseline + full-size frob_vs_oracle; rank 0, N = 1 only)")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r02", "pmc_summary.json"))
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r02", "final", "pmc_summary.json"))
     ap.add_argument("--gn-steps", type=int, default=5,
                     help="timed aligns of the opt-in Gauss-Newton mode (MGICP_SOLVER_GN; 0 = skip)")
     ap.add_argument("--fod-cpu-sample", type=int, default=500_000,

@@ -5,7 +5,7 @@ Corrections follow /opt/skills/guides/MI355X_MICROARCH.md "HBM": FETCH_SIZE / WR
 KiB; on gfx950 FETCH_SIZE reports exactly HALF of the bytes of a wide (16 B/lane) coalesced
 STREAMING read, and "other access widths are uncalibrated".  So the x2 correction is applied per
 kernel only where the kernel's reads are all 16-byte-per-lane coalesced streams:
-  * fdf_soa_kernel and the resident server's streamed part (fdf_server_kernel<true>) -- every load
+  * fdf_soa_kernel and the resident server's streamed part (fdf_server_kernel<true, W>) -- every load
     is a float4 / double2 stream at consecutive addresses: x2;
   * correspond_kernel, knn_cov_kernel, fitness / segdiff (grid gathers), compact_kernel and
     gn_moments_kernel (coalesced 4 B index loads mixed with 16 B gathers): raw FETCH_SIZE,
@@ -20,12 +20,12 @@ import json
 import os
 import sys
 
-STREAMING = {"fdf_soa_kernel", "fdf_server_kernel<true>"}
-# the resident pass server's timing form runs PASSES passes per dispatch (bench.py
+STREAMING = {"fdf_soa_kernel", "fdf_server_kernel<true"}
+# the resident pass server's timing form (fdf_server_kernel<true, W>) runs PASSES passes per dispatch (bench.py
 # --pass-bench-passes): its figures are per pass (dispatch / PASSES, the one-time resident load
 # included pro rata)
-PASSES = {"fdf_server_kernel<true>": int(os.environ.get("PASS_BENCH_PASSES", "50"))}
-KERNELS = ("fdf_server_kernel<true>", "fdf_soa_kernel", "correspond_kernel", "compact_kernel", "chunk_base_kernel", "knn_cov2_kernel",
+PASSES = {"fdf_server_kernel<true": int(os.environ.get("PASS_BENCH_PASSES", "50"))}
+KERNELS = ("fdf_server_kernel<true", "fdf_soa_kernel", "correspond_kernel", "compact_kernel", "chunk_base_kernel", "knn_cov2_kernel",
            "knn_cov_kernel", "fitness_kernel", "gn_moments_kernel", "segdiff_kernel", "voxel_key_kernel",
            "voxel_centroid_kernel")
 
@@ -65,8 +65,8 @@ def main():
             kernels[k] = entry(fk, wk, k in STREAMING, PASSES.get(k, 1))
             if k in PASSES:
                 kernels[k]["per"] = f"pass (dispatch / {PASSES[k]})"
-    if "fdf_server_kernel<true>" in kernels:  # bench.py's key for the server's roofline traffic
-        kernels["fdf_server_kernel"] = kernels["fdf_server_kernel<true>"]
+    if "fdf_server_kernel<true" in kernels:  # bench.py's key for the server's roofline traffic
+        kernels["fdf_server_kernel"] = kernels.pop("fdf_server_kernel<true")
     if "correspond_kernel" in kernels and "compact_kernel" in kernels:
         a, b = kernels["correspond_kernel"], kernels["compact_kernel"]
         kernels["correspond_plus_compact"] = {
