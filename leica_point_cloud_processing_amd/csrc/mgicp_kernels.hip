@@ -31,7 +31,8 @@
 #define MGICP_CORR_STATS 0  // 1: count 1-NN work per sweep (diagnostic builds only)
 #endif
 #ifndef MGICP_SEED_NEIGHBOURS
-#define MGICP_SEED_NEIGHBOURS 1  // the first 1-NN sweep tests the seeds of the query's cell and its 6 face neighbours
+#define MGICP_SEED_NEIGHBOURS 1  // 1: the first 1-NN sweep tests the seeds of the query's cell and its 6 face
+                                 // neighbours (2: every sweep)
 #endif
 #ifndef MGICP_SEED_BOTH
 #define MGICP_SEED_BOTH 1  // seeded 1-NN sweeps also test the seed map's candidate (the nearer one wins)
@@ -926,7 +927,7 @@ __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_kernel(GridV
   }
   if ((!seeded || MGICP_SEED_BOTH) && tg.seed) {
 #if MGICP_SEED_NEIGHBOURS
-    if (!seeded) {
+    if (!seeded || MGICP_SEED_NEIGHBOURS > 1) {
       // the first sweep: the seeds of the query's cell and its 6 face neighbours, the nearest wins
       const int cx = qcell(qx, tg.ox, tg.inv_h), cy = qcell(qy, tg.oy, tg.inv_h), cz = qcell(qz, tg.oz, tg.inv_h);
       const int dd[7][3] = {{0, 0, 0}, {-1, 0, 0}, {1, 0, 0}, {0, -1, 0}, {0, 1, 0}, {0, 0, -1}, {0, 0, 1}};

@@ -330,6 +330,32 @@ def test_resident_server_matches_launched_passes(part_small, monkeypatch, n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("waves,bar,rows", [(4, 1, 1), (4, 0, 1), (4, 1, 0), (8, 1, 1)])
+def test_server_forms_align_identically(monkeypatch, waves, bar, rows):
+    """Every form of the resident server -- 4 or 8 waves per CU, commands through the BAR or the
+    pinned copy, super partials as host rows or the device total -- aligns 300k points to the same
+    T and iteration count as the launched passes, bit for bit."""
+    from leica_point_cloud_processing_amd import synth
+    from leica_point_cloud_processing_amd.engine import GICPEngine
+
+    scan, cad, _ = synth.scan_vs_cad(300_000, 300_000)
+    res = {}
+    for form in ("launched", "server"):
+        monkeypatch.setenv("MGICP_RESIDENT", "0" if form == "launched" else "1")
+        monkeypatch.setenv("MGICP_SRV_WAVES", str(waves))
+        monkeypatch.setenv("MGICP_BAR_CMD", str(bar))
+        monkeypatch.setenv("MGICP_HOST_ROWS", str(rows))
+        e = GICPEngine()
+        e.set_source_xyz(scan)
+        e.set_target_xyz(cad)
+        T = e.align()
+        res[form] = (T, e.last_result["iterations"], e.last_result["n_evals"])
+        e.close()
+    np.testing.assert_array_equal(res["server"][0], res["launched"][0])
+    assert res["server"][1:] == res["launched"][1:]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("solver", [0, 1])
 def test_single_rank_comm_matches_plain(part_small, solver):
     """The collective code path (RCCL all-reduce per BFGS pass / per GN iteration, publish kernel,
