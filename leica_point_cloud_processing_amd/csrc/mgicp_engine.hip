@@ -862,7 +862,11 @@ int ensure_host_red(mgicp_ctx* ctx) {
       if (const char* gp = std::getenv("MGICP_GATE_POLLERS")) ctx->gate_pollers = std::max(1, std::atoi(gp));
     }
     HIPCK(hipMemsetAsync(ctx->mail, 0, sizeof(PassCmd), ctx->stream));
-    if (ctx->bar && !ctx->bar_cmd) {
+    // host stores into device memory need the whole VRAM behind the PCIe BAR (large BAR); without
+    // it block 0 polls the pinned copy
+    hipDeviceProp_t prop;
+    const bool large_bar = hipGetDeviceProperties(&prop, ctx->device) == hipSuccess && prop.isLargeBar;
+    if (ctx->bar && large_bar && !ctx->bar_cmd) {
       if (hipExtMallocWithFlags(reinterpret_cast<void**>(&ctx->bar_cmd), sizeof(PassCmd), hipDeviceMallocFinegrained) !=
           hipSuccess)
         ctx->bar_cmd = nullptr;  // no host-writable device memory: block 0 polls the pinned copy
