@@ -30,6 +30,9 @@
 #ifndef MGICP_CORR_STATS
 #define MGICP_CORR_STATS 0  // 1: count 1-NN work per sweep (diagnostic builds only)
 #endif
+#ifndef MGICP_SRV_STAGGER
+#define MGICP_SRV_STAGGER 1  // resident pass server: odd waves stream first, even waves compute resident data first
+#endif
 #ifndef MGICP_SEED_NEIGHBOURS
 #define MGICP_SEED_NEIGHBOURS 1  // 1: the first 1-NN sweep tests the seeds of the query's cell and its 6 face
                                  // neighbours (2: every sweep)
@@ -1669,6 +1672,26 @@ __global__ __launch_bounds__(64 * kWaves, 1) void fdf_server_kernel(
     int rev = 0;
     if (!(kBench && seq == seq0) && !pass_gate(seq, cmd, mail, timeout, nullptr, host_pollers, A, rev)) return;
     if (ptimes && blockIdx.x == 0 && threadIdx.x == 0) ptimes[2 * (seq & 1023)] = wall_clock64();
+    // odd waves take their streamed chunks first and their resident ones last, even waves the
+    // reverse: the CU's memory pipe is never left idle while all its waves compute resident data
+    // (the order of a wave's chunks does not change any sum)
+    const bool resident_last = MGICP_SRV_STAGGER && (wid & 1);
+    // the streamed chunks, then the resident ones (odd waves)
+    auto stream_chunks = [&]() {
+      for (int w = w1 + nw; w < nch; w += nw) {
+        double acc[kRedVals];
+#pragma unroll
+        for (int v = 0; v < kRedVals; ++v) acc[v] = 0.0;
+        const uint32_t g1 = base[w + 1] >> 2;
+        for (uint32_t i = (base[w] >> 2) + lane; i < g1; i += 64) {
+          CorrGroup g;
+          load_group(c, i, g);
+          fdf_group(A, g, acc);
+        }
+        chunk_store(w, acc, pos, ns, partial, lane);
+      }
+    };
+    if (resident_last) stream_chunks();
     if (w0 < nch) {
       double acc[kRedVals];
 #pragma unroll
@@ -1707,18 +1730,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void fdf_server_kernel(
       }
       chunk_store(w1, acc, pos, ns, partial, lane);
     }
-    for (int w = w1 + nw; w < nch; w += nw) {
-      double acc[kRedVals];
-#pragma unroll
-      for (int v = 0; v < kRedVals; ++v) acc[v] = 0.0;
-      const uint32_t g1 = base[w + 1] >> 2;
-      for (uint32_t i = (base[w] >> 2) + lane; i < g1; i += 64) {
-        CorrGroup g;
-        load_group(c, i, g);
-        fdf_group(A, g, acc);
-      }
-      chunk_store(w, acc, pos, ns, partial, lane);
-    }
+    if (!resident_last) stream_chunks();
     if (w0 >= nch) continue;
     // the timing form writes host rows too when given them (chained on the device by a global
     // ticket), so it times the pass the aligns run
