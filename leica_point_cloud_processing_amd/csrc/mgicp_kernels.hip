@@ -31,7 +31,7 @@
 #define MGICP_CORR_STATS 0  // 1: count 1-NN work per sweep (diagnostic builds only)
 #endif
 #ifndef MGICP_SRV_STAGGER
-#define MGICP_SRV_STAGGER 1  // resident pass server: odd waves stream first, even waves compute resident data first
+#define MGICP_SRV_STAGGER 2  // resident pass server: 2 = wave wid computes its resident chunks after wid/4 of its streamed ones, 1 = odd waves last, 0 = all first
 #endif
 #ifndef MGICP_SEED_NEIGHBOURS
 #define MGICP_SEED_NEIGHBOURS 1  // 1: the first 1-NN sweep tests the seeds of the query's cell and its 6 face
@@ -1675,10 +1675,9 @@ __global__ __launch_bounds__(64 * kWaves, 1) void fdf_server_kernel(
     // odd waves take their streamed chunks first and their resident ones last, even waves the
     // reverse: the CU's memory pipe is never left idle while all its waves compute resident data
     // (the order of a wave's chunks does not change any sum)
-    const bool resident_last = MGICP_SRV_STAGGER && (wid & 1);
-    // the streamed chunks, then the resident ones (odd waves)
-    auto stream_chunks = [&]() {
-      for (int w = w1 + nw; w < nch; w += nw) {
+    // the wave's streamed chunks [c0, c1) (chunks w1 + nw, w1 + 2 nw, ...)
+    auto stream_chunks = [&](int c0, int c1) {
+      for (int w = w1 + nw * (1 + c0); w < nch && c0 < c1; w += nw, ++c0) {
         double acc[kRedVals];
 #pragma unroll
         for (int v = 0; v < kRedVals; ++v) acc[v] = 0.0;
@@ -1691,7 +1690,13 @@ __global__ __launch_bounds__(64 * kWaves, 1) void fdf_server_kernel(
         chunk_store(w, acc, pos, ns, partial, lane);
       }
     };
-    if (resident_last) stream_chunks();
+    // stagger: wave wid computes its resident chunks after split(wid) of its streamed ones, so the
+    // CU's memory pipe is never left idle while all its waves compute resident data (the order of
+    // a wave's chunks does not change any sum).  MGICP_SRV_STAGGER 1: odd waves last, 2: quarters
+    const int nst = w1 + nw < nch ? (nch - w1 - 1) / nw : 0;
+    const int split = MGICP_SRV_STAGGER == 2 ? (wid * nst + kWaves / 2) / kWaves
+                                             : (MGICP_SRV_STAGGER == 1 && (wid & 1) ? nst : 0);
+    stream_chunks(0, split);
     if (w0 < nch) {
       double acc[kRedVals];
 #pragma unroll
@@ -1730,7 +1735,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void fdf_server_kernel(
       }
       chunk_store(w1, acc, pos, ns, partial, lane);
     }
-    if (!resident_last) stream_chunks();
+    stream_chunks(split, nst);
     if (w0 >= nch) continue;
     // the timing form writes host rows too when given them (chained on the device by a global
     // ticket), so it times the pass the aligns run
