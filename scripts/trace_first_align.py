@@ -1,0 +1,10 @@
+import os, sys, time
+sys.path.insert(0, os.getcwd())
+import numpy as np
+from leica_point_cloud_processing_amd import synth
+from leica_point_cloud_processing_amd.engine import GICPEngine
+scan, cad, T = synth.scan_vs_cad(5_000_000, 5_000_000)
+e = GICPEngine(); e.set_target_xyz(cad); e.set_source_xyz(scan); e.align(); e.close()
+print("---- second context (warm process) ----", file=sys.stderr, flush=True)
+e = GICPEngine(); e.set_target_xyz(cad); e.set_source_xyz(scan); e.align(); print(e.last_result, file=sys.stderr)
+e.align(); print(e.last_result, file=sys.stderr)
