@@ -1,0 +1,15 @@
+# 8-wave server shape again, now with stagger, host rows and the spill-free code (env only)
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/r02/w8b; mkdir -p $O
+for W in 8 4 8 4; do
+  MGICP_SRV_WAVES=$W timeout -k 10 200 python -u scripts/srv_timing.py > $O/t_$W.json 2> $O/t_$W.err || { tail -20 $O/t_$W.err; exit 1; }
+  echo "waves $W $(cat $O/t_$W.json)"
+done
+B="bench.py --steps 10 --warmup 2 --cpu-sample 0 --oracle-full 0 --fod-cpu-sample 0 --gn-steps 0 --no-events --pass-bench 0"
+for W in 8 4 8 4; do
+  MGICP_SRV_WAVES=$W timeout -k 10 300 python -u $B > $O/b_$W.json 2> $O/b_$W.err || { tail -30 $O/b_$W.err; exit 1; }
+  python3 -c "
+import json
+d=json.load(open('$O/b_$W.json')); print('waves $W', d['value'], d['ms_per_step'])"
+done
