@@ -958,7 +958,11 @@ int wait_rows(mgicp_ctx* ctx, unsigned long long seq, long long nsup, double out
 
 int ensure_rows(mgicp_ctx* ctx, long long nsup) {
   if (ctx->h_rows && ctx->rows_cap >= static_cast<size_t>(nsup)) return MGICP_OK;
-  if (ctx->h_rows) HIPCK(hipHostFree(ctx->h_rows));
+  if (ctx->h_rows) {
+    int rc = sync(ctx);  // no server of an earlier run may still hold the old rows
+    if (rc) return rc;
+    HIPCK(hipHostFree(ctx->h_rows));
+  }
   ctx->h_rows = nullptr;
   const size_t cap = static_cast<size_t>(std::max<long long>(nsup, 64));
   HIPCK(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_rows), cap * 32 * sizeof(unsigned long long),

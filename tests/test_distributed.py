@@ -356,6 +356,33 @@ def test_server_forms_align_identically(monkeypatch, waves, bar, rows):
 
 
 @pytest.mark.gpu
+def test_server_context_reuse_across_cloud_sizes(part_small):
+    """One context aligning a 20k pair, then a 300k pair (the host rows grow), then the 20k pair
+    again gives each fresh context's T bit for bit."""
+    from leica_point_cloud_processing_amd import synth
+    from leica_point_cloud_processing_amd.engine import GICPEngine
+
+    small = part_small[:2]
+    big = synth.scan_vs_cad(300_000, 300_000)[:2]
+
+    def fresh(pair):
+        f = GICPEngine()
+        f.set_source_xyz(pair[0])
+        f.set_target_xyz(pair[1])
+        T = f.align()
+        f.close()
+        return T
+
+    ref = {"small": fresh(small), "big": fresh(big)}
+    e = GICPEngine()
+    for name, pair in (("small", small), ("big", big), ("small", small)):
+        e.set_source_xyz(pair[0])
+        e.set_target_xyz(pair[1])
+        np.testing.assert_array_equal(e.align(), ref[name])
+    e.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("solver", [0, 1])
 def test_single_rank_comm_matches_plain(part_small, solver):
     """The collective code path (RCCL all-reduce per BFGS pass / per GN iteration, publish kernel,
