@@ -267,7 +267,6 @@ struct mgicp_ctx {
   DevBuf<double> corr_d;   // 6 streams
   DevBuf<unsigned char> cscratch;
   size_t corr_cap = 0;     // elements per stream (multiple of 4)
-  size_t m_local = 0;      // accepted correspondences of this rank
   bool seed_valid = false;
   // query order of the 1-NN sweeps (Morton order of the shard; env MGICP_QUERY_ORDER)
   bool query_order = true;
@@ -1110,12 +1109,8 @@ int correspond(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
                          rot_of(T, G), ctx->prev_pos.p, ctx->flags.p, ctx->cpos.p, ctx->chunk_base.p, p0, p1,
                          corr_soa(ctx), s));
   }
-  HIPCK(hipMemcpyAsync(ctx->h_small, ctx->cpos.p + ns, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-  int rc = sync(ctx);
-  if (rc) return rc;
-  uint32_t m = 0;
-  std::memcpy(&m, ctx->h_small, sizeof(m));
-  ctx->m_local = m;
+  // no host round trip here: the correspondence count arrives with the first objective pass (its
+  // count lane) and every consumer of the streams runs on the same stream
   ctx->have_corr = true;
   return MGICP_OK;
 }
