@@ -9,10 +9,12 @@ GICPAlignment::iterate(), /root/reference/src/GICPAlignment.cpp:111-121) over cl
 in HBM whose grids and covariances are cached (the first align, in warmup, builds them and is
 reported separately as ms_to_converge_first).  value = outer GICP iterations of all timed
 steps / timed seconds.  With N GPUs the same 5M <-> 5M problem is sharded by source point
-ranges (strong scaling); the per-pass 16-double all-reduce runs over RCCL inside libmgicp.so.
+ranges (strong scaling); every rank runs the resident pass server and the per-pass sums travel
+through a node-wide shared-memory segment of super rows (--transport shm, default) or one RCCL
+all-gather per pass (--transport rccl).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--n-source S] [--n-target T]
-       (N > 1 is launched by torch.distributed.run, one rank per GPU)
+       (N > 1: this script starts its own N ranks, or runs under torch.distributed.run)
 """
 from __future__ import annotations
 
@@ -81,6 +83,11 @@ def parse():
     ap.add_argument("--pass-bench-passes", type=int, default=50)
     ap.add_argument("--prof-steps", type=int, default=3,
                     help="aligns of the kernel-time leg (HIP events around every kernel family)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch + rendezvous of every rank only (no GPU, libmgicp.so not loaded)")
+    ap.add_argument("--transport", default="shm", choices=["shm", "rccl"],
+                    help="N > 1: per-pass sums through the node-wide shared row segment (resident pass "
+                         "server on every rank, no collective per pass) or one RCCL all-gather per pass")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
     args.n_source = args.n_source or cfg["n_source"]
@@ -90,18 +97,86 @@ def parse():
 
 
 def dist_setup(args):
-    """RANK / WORLD_SIZE / MASTER_* come from torch.distributed.run; the control plane is
-    leica_point_cloud_processing_amd.parallel.Rendezvous (torch is never imported in a process
-    that uses libmgicp.so: see parallel.py for the two-HIP-runtime hazard)."""
+    """RANK / WORLD_SIZE / MASTER_* come from torch.distributed.run or from launch_ranks below; the
+    control plane is leica_point_cloud_processing_amd.parallel.Rendezvous (torch is never imported
+    in a process that uses libmgicp.so: see parallel.py for the two-HIP-runtime hazard)."""
     from leica_point_cloud_processing_amd.parallel import Rendezvous
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
-    if world == 1 and args.gpus > 1:
-        raise SystemExit("--gpus > 1 must be launched with torch.distributed.run (one rank per GPU)")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     return world, rank, local, Rendezvous(rank, world)
+
+
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int) -> int:
+    """`python bench.py --gpus N` without torchrun: this parent starts N fresh
+    child processes of this script -- one rank per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in
+    their environment -- relays rank 0's stdout (the JSON line) and exits non-zero if any child
+    does.  The parent itself never loads libmgicp.so or touches HIP: it only spawns and waits
+    (children are separate programs, not an exec of this process)."""
+    import subprocess
+    import threading
+
+    port, ctrl = _free_port(), _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
+                    "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "MGICP_CTRL_PORT": str(ctrl)})
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno(),
+                                      text=True, start_new_session=False))
+    lines = []
+
+    def relay():
+        for line in procs[0].stdout:
+            lines.append(line)
+            sys.stdout.write(line)
+            sys.stdout.flush()
+
+    t = threading.Thread(target=relay, daemon=True)
+    t.start()
+    rc = 0
+    alive = set(range(n))
+    while alive:
+        for r in sorted(alive):
+            code = procs[r].poll()
+            if code is None:
+                continue
+            alive.discard(r)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                sys.stderr.write(f"bench.py: rank {r} exited with {code}; stopping the other ranks\n")
+                for o in alive:
+                    procs[o].terminate()  # the exact children this parent started
+        time.sleep(0.05)
+    t.join(timeout=10)
+    return rc
+
+
+def dry_run(args, world, rank, pg):
+    """--dry-run: the launch and rendezvous of every rank (the shared-segment name and a 128-byte id
+    broadcast, barrier, max-over-ranks timer) without loading libmgicp.so -- the CPU test of the
+    N > 1 launch path."""
+    name = pg.broadcast(f"/mgicp_dry_{os.getpid()}".encode() if rank == 0 else None)
+    uid = pg.broadcast(bytes(range(128)) if rank == 0 else None)
+    pg.barrier()
+    joined = pg.allreduce_max(float(rank)) + 1
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_joined": int(joined),
+                          "uid_ok": uid == bytes(range(128)), "shm_name": name.decode(),
+                          "local_rank": int(os.environ.get("LOCAL_RANK", "0"))}))
 
 
 def cpu_baseline(n, threads, occlusion=0.0):
@@ -209,7 +284,12 @@ def fod_rows(eng, scan, cad, T_final, n_cpu):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     world, rank, local, pg = dist_setup(args)
+    if args.dry_run:
+        dry_run(args, world, rank, pg)
+        return
     from leica_point_cloud_processing_amd import synth
     from leica_point_cloud_processing_amd.engine import GICPEngine
 
@@ -220,9 +300,29 @@ def main():
     t_c = time.perf_counter()
     eng = GICPEngine(device=local, max_iter=args.max_iter, fixed_iterations=int(args.fixed))
     ms_create = 1e3 * (time.perf_counter() - t_c)
+    transport = "local"
     if world > 1:
         uid = pg.broadcast(GICPEngine.unique_id() if rank == 0 else None)
         eng.comm_init(world, rank, uid)
+        transport = "rccl"
+        if args.transport == "shm":
+            # the node-wide row segment: every rank's resident server writes its supers there, every
+            # host takes the fixed-order total (no collective per pass); RCCL keeps the one-time
+            # target-covariance all-gather.  Any rank failing to attach -> every rank stays on RCCL.
+            import secrets
+
+            name = pg.broadcast(f"/mgicp_{os.getpid()}_{secrets.token_hex(6)}".encode() if rank == 0 else None)
+            err = None
+            try:
+                eng.attach_shm(name.decode(), args.n_source)
+            except Exception as exc:  # noqa: BLE001 -- reported in the JSON line, RCCL path kept
+                err = str(exc)
+            if pg.allreduce_max(1.0 if err else 0.0) > 0:
+                if not err:
+                    eng.detach_shm()
+                transport = f"rccl (shared segment unavailable: {err or 'on another rank'})"
+            else:
+                transport = "shm rows + rccl (target covariances)"
     eng.set_source_xyz(scan)
     eng.set_target_xyz(cad)
 
@@ -260,7 +360,7 @@ def main():
             eng.align()
         kt = eng.kernel_times()
         eng.set_profiling(False)
-    # roofline leg of the pass the aligns run on one GPU: the resident pass server (one cooperative
+    # roofline leg of the pass the aligns run on one GPU: the resident pass server (one
     # launch holding part of the streams on chip across passes) in its timing form -- P passes of
     # one state back to back, chained on the device -- bracketed by HIP events on the engine's
     # stream; rocprofv3 lists it as fdf_server_kernel<true> (duration / P = one pass).  Beside it the
@@ -521,7 +621,8 @@ def main():
             "name": args.config,
             "n_source": args.n_source,
             "n_target": args.n_target,
-            "parallelism": f"source point-range shards x{world}, target replicated, RCCL all-reduce per pass",
+            "parallelism": f"source point-range shards x{world}, target replicated",
+            "transport": transport,
         },
         "iterations_per_align": iters_per_align,
         "objective_passes_per_align": result["n_evals"],

@@ -14,7 +14,9 @@
  * (32 for pcl::PointXYZRGB, 16 for pcl::PointXYZ, 12 for packed xyz).
  *
  * Threading: one context per host thread; every call blocks until its result is on the
- * host.  Status codes: 0 = OK, negative = error (mgicp_last_error() has the message).
+ * host.  Several contexts may align on one device at once: one of them at a time runs the
+ * resident pass server (it needs every CU), the others run launched passes.  Status codes: 0 = OK,
+ * negative = error (mgicp_last_error() has the message).
  */
 #ifndef MI355X_GICP_H
 #define MI355X_GICP_H
@@ -157,9 +159,21 @@ int mgicp_voxel_grid(mgicp_ctx* ctx, const float* in, size_t n, size_t stride, i
  * and sums them in a fixed order, so every N gives the single-GPU result bit for bit (see
  * mgicp_debug_supers); the target covariances are computed in N slices and all-gathered.  nranks = 1 with an id builds a
  * one-rank communicator (the collective path on a single device); id = NULL makes a "detached"
- * shard for the debug entry points. */
+ * shard for the debug entry points (or an RCCL-free rank, once mgicp_comm_attach_shm succeeds). */
 int mgicp_get_unique_id(unsigned char id[128]);
 int mgicp_comm_init(mgicp_ctx* ctx, int nranks, int rank, const unsigned char id[128]);
+/* Node-local transport of the per-pass sums (all ranks on one node), called by EVERY rank after
+ * mgicp_comm_init with the same POSIX shared-memory name ("/..."; unique per job, e.g. chosen by
+ * rank 0 and broadcast) and the same max_source_points (0 = 32M; the largest source cloud any
+ * later set_source may hold).  It blocks until every rank has mapped the segment, then unlinks the
+ * name.  From then on every objective pass writes each rank's super partials straight from its GPU
+ * into the segment (resident pass server on every rank, no collective per pass) and every rank's
+ * host takes the same fixed-order total; GN moments and fitness gather through it too.  Results
+ * stay bitwise those of one GPU.  RCCL (if initialised) is then used only for the one-time
+ * all-gather of the target covariances; without it every rank computes them all.  Every rank must
+ * run the same sequence of align / fitness calls.  MGICP_E_COMM: segment or peers unavailable (the
+ * context keeps its previous transport).  name = NULL detaches (back to RCCL / local). */
+int mgicp_comm_attach_shm(mgicp_ctx* ctx, const char* name, size_t max_source_points);
 
 /* ---- introspection for parity tests (original point order) ---- */
 /* covariances of the source (which = 0) or target (which = 1): n x {c00,c01,c02,c11,c12,c22} */
@@ -179,7 +193,7 @@ int mgicp_debug_fdf(mgicp_ctx* ctx, const double x[6], double* f, double g6[6]);
 int mgicp_debug_fdf_sums(mgicp_ctx* ctx, const double x[6], double out16[16]);
 /* Objective-pass timing (bench.py's roofline leg): npasses passes at state x over the last
  * correspondence sweep, back to back on the device, bracketed by HIP events on the context's
- * stream.  mode 0: the resident pass server (one cooperative launch running all passes; the pass
+ * stream.  mode 0: the resident pass server (one launch running all passes; the pass
  * the aligns use on one GPU), mode 1: one fdf_soa_kernel launch per pass.  out_ms: average per
  * pass; out16: the sums of the last pass (as mgicp_debug_fdf_sums).  Single-rank contexts only. */
 int mgicp_debug_pass_bench(mgicp_ctx* ctx, const double x[6], int npasses, int mode, double* out_ms,
@@ -211,6 +225,14 @@ int mgicp_debug_trace(mgicp_ctx* ctx, float* out, int max_iters);
 #define MGICP_KERNEL_FAMILIES 6
 int mgicp_debug_kernel_times(mgicp_ctx* ctx, double out_ms[MGICP_KERNEL_FAMILIES],
                              int out_counts[MGICP_KERNEL_FAMILIES]);
+/* objective-pass path counters since mgicp_create: [0] resident servers launched, [1] passes run
+ * by a server, [2] passes run by launched kernels, [3] server passes that missed their deadline
+ * (env MGICP_ROW_DEADLINE_MS, default 500) and were taken over by a launched pass (bitwise the
+ * same sums; the rest of that align runs launched passes), [4] 1 if the server reads its commands
+ * from device memory the host writes through the BAR, [5] private host-row buffer allocations,
+ * [6] transport (0 local, 1 RCCL, 2 shared segment, 3 shared segment + RCCL), [7] server launches
+ * refused because another context of this process ran a server on the same device */
+int mgicp_debug_pass_stats(mgicp_ctx* ctx, long long out[8]);
 /* enable (1) / disable (0) per-launch HIP event timing (off by default); objective passes
  * ([2]) are sampled every 8th launch (env MGICP_PROF_STRIDE), every other family is timed on
  * every launch */

@@ -6,13 +6,16 @@
 // sweep on the GPU, then estimateRigidTransformationBFGS whose objective passes run on the
 // GPU and whose 6-DoF BFGS logic runs here (pcl_bfgs.hpp), then PCL's delta test.
 // Multi-GPU: one process per GPU, contiguous ranges of the grid-sorted source cloud per rank,
-// target replicated; every objective pass all-reduces 16 doubles over RCCL (xGMI).
+// target replicated; the per-pass sums travel through a node-wide shared-memory segment of super
+// rows (shm_rows.hpp: every rank's GPU writes its rows, every host takes the same fixed-order
+// total), or -- without that segment -- one RCCL all-gather of super partials per pass (xGMI).
 #pragma clang fp contract(off)
 
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -28,6 +31,7 @@
 #include "mgicp_internal.hpp"
 #include "gn_solver.hpp"
 #include "pcl_bfgs.hpp"
+#include "shm_rows.hpp"
 
 using namespace mgicp;
 
@@ -226,6 +230,24 @@ struct Cloud {
 
 enum { kFamCov = 0, kFamCorr = 1, kFamFdf = 2, kFamRed = 3, kFamCompact = 4, kFamMoments = 5, kFams = 6 };
 
+// pass-path counters (mgicp_debug_pass_stats)
+enum {
+  kStSrvLaunch = 0,  // resident servers launched
+  kStSrvPass,        // objective passes run by a server
+  kStLaunchedPass,   // objective passes run by a launched kernel (gated, plain, or taking over)
+  kStTakeover,       // server passes that missed their deadline and were re-run as launched passes
+  kStBar,            // 1: the server reads its commands from device memory written through the BAR
+  kStRowsAlloc,      // private host-row buffer allocations
+  kStTransport,      // 0 local, 1 RCCL, 2 shared segment, 3 shared segment + RCCL (bulk all-gathers)
+  kStSrvDenied,      // server launches refused because another context of this process held the device
+  kStCount
+};
+
+// One resident server per device and process: its blocks need every CU of the device (one block
+// per CU, 512 registers per lane), so a second context aligning on the same device at the same
+// time runs launched passes instead of a second server.
+std::atomic<int> g_srv_busy[64];
+
 }  // namespace
 
 struct mgicp_ctx {
@@ -314,21 +336,36 @@ struct mgicp_ctx {
   std::vector<double> host_gt;             // 2 x 1024
   unsigned long long gated_seq = 0;     // sequence number of the queued gated pass (0 = none)
   unsigned long long gate_timeout = 0;  // wall_clock64 ticks a gated pass waits before giving up
-  // the resident pass server (env MGICP_RESIDENT, single-GPU polled mode): one cooperative launch per
-  // BFGS run keeps part of the compacted streams in registers / LDS across all its passes
+  // the resident pass server (env MGICP_RESIDENT; single GPU polled mode, or any rank count with the
+  // shared row segment): one launch per BFGS run keeps part of the compacted streams in registers /
+  // LDS across all its passes
   bool resident = true;
   bool srv_live = false;                // a server is running and waits for pass srv_next
+  bool srv_locked = false;              // this context holds g_srv_busy[device]
+  bool srv_degraded = false;            // a server pass was taken over: launched passes until the align ends
   unsigned long long srv_next = 0;
   int cus = 0;                          // compute units (the server's grid)
+  int srv_cus = 0;                      // env MGICP_SRV_CUS: cap on the server's blocks (0 = every CU)
   int srv_waves = 4;                    // server shape: 4 or 8 waves per CU (env MGICP_SRV_WAVES)
+  int stall_pass = -1;                  // env MGICP_SRV_STALL_PASS (tests): a server block withholds this pass
+  double row_deadline_ms = 500.0;       // env MGICP_ROW_DEADLINE_MS: own rows missing this long -> take over
+  double remote_deadline_s = 120.0;     // env MGICP_REMOTE_DEADLINE_S: other ranks' rows / gathers
   unsigned long long* h_ptimes = nullptr;  // MGICP_PASS_TIMES=1: per pass gate exit / finish (wall clock)
   unsigned long long* d_ptimes = nullptr;
-  // the server's super partials as stamped host rows (32 words per super; env MGICP_HOST_ROWS)
+  // the passes' super partials as stamped host rows (32 words per super, two parity buffers; env
+  // MGICP_HOST_ROWS): private pinned memory, or the node-wide shared segment
   bool host_rows = true;
   unsigned long long* h_rows = nullptr;
   unsigned long long* d_rows = nullptr;
-  size_t rows_cap = 0;                  // supers
+  size_t rows_cap = 0;                  // supers per parity buffer
   std::vector<double> row_sums;         // decoded super partials
+  unsigned int pass_idx = 0;            // objective passes so far: the row stamp (identical on every rank)
+  unsigned long long gather_idx = 0;    // generic gathers through the shared segment so far
+  // node-wide transport (mgicp_comm_attach_shm)
+  bool have_shm = false;
+  shm::Segment shm;
+  unsigned char* shm_d = nullptr;       // device view of the segment (hipHostRegister'ed)
+  long long st[kStCount] = {};          // pass-path counters
   bool spin_pause = false;              // env MGICP_SPIN_PAUSE: pause instruction in the row spin
   // MGICP_PASS_TIMES: host view of the server passes -- command published -> rows complete
   // (device pass + PCIe both ways) and rows complete -> next command (host BFGS step)
@@ -442,12 +479,14 @@ void prof_resolve(mgicp_ctx* ctx) {
 }
 
 // command block of the queued gated pass: op / reverse / A first, then the sequence number
-void publish_cmd(mgicp_ctx* ctx, unsigned long long seq, unsigned int op, int reverse, const Xf34* A) {
+void publish_cmd(mgicp_ctx* ctx, unsigned long long seq, unsigned int op, int reverse, const Xf34* A,
+                 unsigned int rstamp = 0) {
   // every 8-byte half: (stamp << 32) | word, one aligned 8-byte store each (single-copy atomic)
   unsigned int w[kCmdWords] = {};
   if (A) std::memcpy(w, A->m, 12 * sizeof(unsigned int));
   w[12] = op;
   w[13] = static_cast<unsigned int>(reverse);
+  w[14] = rstamp;
   const unsigned long long stamp = static_cast<unsigned long long>(static_cast<unsigned int>(seq)) << 32;
   if (ctx->bar_cmd) {
     // device memory through the BAR: aligned 8-byte stores, then a store fence so they leave the
@@ -469,6 +508,10 @@ void cancel_gated(mgicp_ctx* ctx) {
     // host-row passes leave the tickets as multiples of their supers' sizes: re-arm them for the
     // launched passes (stream order: after the server has exited)
     (void)hipMemsetAsync(ctx->tickets.p, 0, ctx->tickets_n * sizeof(unsigned int), ctx->stream);
+    if (ctx->srv_locked) {  // the device's server slot is free for the next BFGS run (any context)
+      g_srv_busy[ctx->device & 63].store(0, std::memory_order_release);
+      ctx->srv_locked = false;
+    }
   }
   if (!ctx->gated_seq) return;
   publish_cmd(ctx, ctx->gated_seq, kPassCancel, 0, nullptr);
@@ -914,48 +957,49 @@ int wait_pass(mgicp_ctx* ctx, unsigned long long seq) {
   return MGICP_OK;
 }
 
-// Wait for the host rows of pass `seq` (every super's 32 stamped words), then take the total exactly
-// as wave_total / wave_sum would on one wave: lane l sums supers l, l + 64, ... in order from 0.0,
-// then the shuffle tree v[i] += v[i + off] for off = 32 ... 1 (lane 0's value)
-int wait_rows(mgicp_ctx* ctx, unsigned long long seq, long long nsup, double out[kRedVals]) {
-  const unsigned int st = static_cast<unsigned int>(seq);
-  ctx->row_sums.resize(static_cast<size_t>(nsup) * kRedVals);
-  const auto t0 = std::chrono::steady_clock::now();
-  for (long long r = 0; r < nsup; ++r) {
-    const unsigned long long* row = ctx->h_rows + 32 * r;
-    for (unsigned spins = 0;; ++spins) {
-      bool all = true;
-      for (int w = 0; w < 32 && all; ++w) all = static_cast<unsigned int>(__atomic_load_n(row + w, __ATOMIC_ACQUIRE) >> 32) == st;
-      if (all) break;
-      if (ctx->spin_pause) __builtin_ia32_pause();
-      if ((spins & 1023u) == 1023u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(500)) {
-        int rc = sync(ctx);
-        if (rc) return rc;
-        return fail(ctx, MGICP_E_HIP, "objective pass finished without publishing its super rows");
-      }
-    }
-    for (int v = 0; v < kRedVals; ++v) {
-      const unsigned long long lo = __atomic_load_n(row + 2 * v, __ATOMIC_ACQUIRE) & 0xffffffffull;
-      const unsigned long long hi = __atomic_load_n(row + 2 * v + 1, __ATOMIC_ACQUIRE) & 0xffffffffull;
-      const unsigned long long bits = (hi << 32) | lo;
-      std::memcpy(&ctx->row_sums[static_cast<size_t>(r) * kRedVals + v], &bits, sizeof(double));
-    }
+CorrSoA corr_soa(mgicp_ctx* ctx);
+
+// Where the host rows of the passes live: this context's private pinned buffers (single rank), or
+// the node-wide shared segment (every rank's rows at their global super index).  Parity buffer p
+// starts stride words after parity 0; this rank's rows start at super `first`.
+struct RowView {
+  unsigned long long* h0 = nullptr;  // host view, parity 0, super 0
+  unsigned long long* d0 = nullptr;  // device view, parity 0, super 0
+  size_t stride = 0;                 // words between the parity buffers
+  long long first = 0, nloc = 0, ntot = 0;
+  unsigned long long* dev_rows(unsigned int rstamp) const {  // this rank's rows of the pass stamped rstamp
+    return d0 + (rstamp & 1u) * stride + static_cast<size_t>(first) * shm::kRowWords;
   }
-  for (int v = 0; v < kRedVals; ++v) {
-    double lanes[64];
-    for (int l = 0; l < 64; ++l) {
-      double a = 0.0;
-      for (long long sg = l; sg < nsup; sg += 64) a += ctx->row_sums[static_cast<size_t>(sg) * kRedVals + v];
-      lanes[l] = a;
-    }
-    for (int off = 32; off > 0; off >>= 1)
-      for (int i = 0; i < off; ++i) lanes[i] = lanes[i] + lanes[i + off];
-    out[v] = lanes[0];
+};
+
+RowView row_view(const mgicp_ctx* ctx) {
+  RowView v;
+  if (ctx->have_shm) {
+    v.h0 = reinterpret_cast<unsigned long long*>(ctx->shm.rows(0));
+    v.d0 = reinterpret_cast<unsigned long long*>(ctx->shm_d + ctx->shm.rows_offset_bytes());
+    v.stride = ctx->shm.rows_stride_words();
+    v.ntot = ctx->nsup_total();
+    v.first = super_first(ctx->rank, v.ntot, ctx->nranks);
+    v.nloc = ctx->nsup_local();
+  } else {
+    v.h0 = ctx->h_rows;
+    v.d0 = ctx->d_rows;
+    v.stride = ctx->rows_cap * shm::kRowWords;
+    v.ntot = v.nloc = ctx->nsup_local();
   }
-  return MGICP_OK;
+  return v;
 }
 
-int ensure_rows(mgicp_ctx* ctx, long long nsup) {
+// Host rows for the current source cloud: the private buffers grow as needed (two parity buffers);
+// the shared segment was sized at attach time.
+int ensure_rows(mgicp_ctx* ctx) {
+  const long long nsup = ctx->nsup_total();
+  if (ctx->have_shm) {
+    if (nsup > ctx->shm.max_sup)
+      return fail(ctx, MGICP_E_INVALID, "source cloud larger than the shared row segment (mgicp_comm_attach_shm "
+                                        "max_source_points)");
+    return MGICP_OK;
+  }
   if (ctx->h_rows && ctx->rows_cap >= static_cast<size_t>(nsup)) return MGICP_OK;
   if (ctx->h_rows) {
     int rc = sync(ctx);  // no server of an earlier run may still hold the old rows
@@ -964,11 +1008,83 @@ int ensure_rows(mgicp_ctx* ctx, long long nsup) {
   }
   ctx->h_rows = nullptr;
   const size_t cap = static_cast<size_t>(std::max<long long>(nsup, 64));
-  HIPCK(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_rows), cap * 32 * sizeof(unsigned long long),
-                      hipHostMallocMapped | hipHostMallocCoherent));
+  const size_t bytes = 2 * cap * shm::kRowWords * sizeof(unsigned long long);
+  HIPCK(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_rows), bytes, hipHostMallocMapped | hipHostMallocCoherent));
   HIPCK(hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->d_rows), ctx->h_rows, 0));
-  std::memset(ctx->h_rows, 0, cap * 32 * sizeof(unsigned long long));
+  std::memset(ctx->h_rows, 0, bytes);  // stamp 0 is never a pass's stamp
   ctx->rows_cap = cap;
+  ctx->st[kStRowsAlloc]++;
+  return MGICP_OK;
+}
+
+// A server pass missed its deadline (its blocks could not all run: other work on the device, a
+// profiler, a withheld block in the tests): cancel the server -- blocks still waiting see the later
+// command and exit, blocks that start late exit at their first gate -- and re-run the pass as a
+// launched kernel that writes the same rows with the same stamp (the sums are bitwise those of the
+// server: same chunks, lane order and tree).  The rest of the align runs launched passes.
+int take_over(mgicp_ctx* ctx, unsigned int rstamp, const Xf34& A) {
+  cancel_gated(ctx);  // tickets re-armed on the stream after the server has exited
+  ctx->srv_degraded = true;
+  ctx->st[kStTakeover]++;
+  ctx->st[kStLaunchedPass]++;
+  const size_t ns = ctx->shard_p1() - ctx->shard_p0();
+  HIPCK(launch_fdf_soa(corr_soa(ctx), ctx->cpos.p, ctx->chunk_base.p, ns, A, ctx->partial.p, ctx->spart.p,
+                       fdf_grid_blocks(ns, ctx->fdf_max_blocks), ctx->tickets.p, nullptr, 0, nullptr, 0, ctx->stream,
+                       row_view(ctx).dev_rows(rstamp), rstamp));
+  // host-row passes leave the tickets as multiples of their supers' sizes: re-arm them for whatever
+  // form the next pass takes
+  HIPCK(hipMemsetAsync(ctx->tickets.p, 0, ctx->tickets_n * sizeof(unsigned int), ctx->stream));
+  return MGICP_OK;
+}
+
+// Wait for every host row of the pass stamped rstamp (32 stamped words per super: this rank's own
+// rows first, then the other ranks'), then take the total exactly as wave_total / wave_sum would on
+// one wave (shm::fixed_total).  Own rows missing after row_deadline_ms: the pass is taken over
+// (take_over, when allowed) and waited for again; after a stream drain every row is checked once
+// more before an error is returned.  Other ranks' rows: remote_deadline_s.
+int wait_rows(mgicp_ctx* ctx, unsigned int rstamp, const Xf34& A, double out[kRedVals], bool allow_takeover) {
+  const RowView rv = row_view(ctx);
+  const unsigned long long* buf = rv.h0 + (rstamp & 1u) * rv.stride;
+  ctx->row_sums.resize(static_cast<size_t>(std::max<long long>(rv.ntot, 1)) * kRedVals);
+  auto t0 = std::chrono::steady_clock::now();
+  bool taken = false;
+  const double dl_own = ctx->row_deadline_ms * 1e-3;
+  auto wait_row = [&](long long r, bool own) -> int {
+    const unsigned long long* row = buf + shm::kRowWords * static_cast<size_t>(r);
+    for (unsigned spins = 0; !shm::row_complete(reinterpret_cast<const uint64_t*>(row), rstamp); ++spins) {
+      if (ctx->spin_pause) __builtin_ia32_pause();
+      if ((spins & 1023u) != 1023u) continue;
+      const double el = shm::elapsed_s(t0);
+      if (own && !taken && allow_takeover && el > dl_own) {
+        int rc = take_over(ctx, rstamp, A);
+        if (rc) return rc;
+        taken = true;
+        t0 = std::chrono::steady_clock::now();
+        continue;
+      }
+      if (own && el > (taken ? ctx->remote_deadline_s : dl_own)) {
+        int rc = sync(ctx);  // drains the stream (and cancels a live server): the rows are final now
+        if (rc) return rc;
+        if (shm::row_complete(reinterpret_cast<const uint64_t*>(row), rstamp)) break;
+        return fail(ctx, MGICP_E_HIP, "objective pass finished without publishing its super rows");
+      }
+      if (!own && el > ctx->remote_deadline_s)
+        return fail(ctx, MGICP_E_COMM, "another rank did not publish its super rows (shared row segment)");
+    }
+    shm::row_decode(reinterpret_cast<const uint64_t*>(row), &ctx->row_sums[static_cast<size_t>(r) * kRedVals]);
+    return MGICP_OK;
+  };
+  for (long long r = rv.first; r < rv.first + rv.nloc; ++r) {
+    int rc = wait_row(r, true);
+    if (rc) return rc;
+  }
+  t0 = std::chrono::steady_clock::now();
+  for (long long r = 0; r < rv.ntot; ++r) {
+    if (r >= rv.first && r < rv.first + rv.nloc) continue;
+    int rc = wait_row(r, false);
+    if (rc) return rc;
+  }
+  shm::fixed_total(ctx->row_sums.data(), rv.ntot, kRedVals, out);
   return MGICP_OK;
 }
 
@@ -1014,6 +1130,37 @@ int combine_supers(mgicp_ctx* ctx, int nv, const double* sup, double* out) {
     const long long ns = ctx->nsup_local();
     HIPCK(launch_finish_supers(sup, ns, ns, 1, nv, out, ctx->stream));
   }
+  return MGICP_OK;
+}
+
+// The same totals delivered to the host (GN moments once per outer iteration, fitness once per
+// call).  With the shared segment: a generic gather -- this rank copies its supers to their global
+// rows of the gather's parity buffer, publishes the gather index and waits for every rank's, and
+// every host takes the fixed-order total itself (no collective).  Otherwise combine_supers + D2H.
+int combine_to_host(mgicp_ctx* ctx, int nv, const double* sup, double* out) {
+  if (ctx->have_shm) {
+    const unsigned long long g = ++ctx->gather_idx;
+    double* buf = ctx->shm.gath(static_cast<int>(g & 1));
+    const long long ntot = ctx->nsup_total();
+    const long long first = super_first(ctx->rank, ntot, ctx->nranks), nloc = ctx->nsup_local();
+    if (nloc > 0)
+      HIPCK(hipMemcpyAsync(buf + static_cast<size_t>(first) * nv, sup, static_cast<size_t>(nloc) * nv * sizeof(double),
+                           hipMemcpyDeviceToHost, ctx->stream));
+    int rc = sync(ctx);
+    if (rc) return rc;
+    if (!shm::gather_publish_wait(ctx->shm, g, ctx->remote_deadline_s))
+      return fail(ctx, MGICP_E_COMM, "another rank did not publish its supers (shared segment gather)");
+    // the gather rows are packed nv per super: fixed_total reads rows[s * nv + v]
+    shm::fixed_total(buf, ntot, nv, out);
+    return MGICP_OK;
+  }
+  double* dst = nv == kRedVals ? ctx->red.p : ctx->mred.p;
+  int rc = combine_supers(ctx, nv, sup, dst);
+  if (rc) return rc;
+  HIPCK(hipMemcpyAsync(ctx->h_small, dst, static_cast<size_t>(nv) * sizeof(double), hipMemcpyDeviceToHost,
+                       ctx->stream));
+  if ((rc = sync(ctx))) return rc;
+  std::memcpy(out, ctx->h_small, static_cast<size_t>(nv) * sizeof(double));
   return MGICP_OK;
 }
 
@@ -1135,30 +1282,56 @@ struct DeviceFunctor {
     const int reverse = (ctx->alt_sweep ? (ctx->n_evals & 1) : 0) | ctx->fdf_diag;
     const bool poll = ctx->poll && !ctx->fdf_diag;
     const unsigned long long seq = ++ctx->pass_seq;
+    // the pass's row stamp: the objective-pass index, identical on every rank
+    // (0 is never a stamp; stamps >= 2^31 belong to mgicp_debug_pass_bench's timing form)
+    if (++ctx->pass_idx >= 0x80000000u) ctx->pass_idx = 1;
+    const unsigned int rstamp = ctx->pass_idx;
     // single GPU: the finishing wave writes the totals straight into mapped pinned host memory.
-    // Otherwise the pass leaves its super partials, then combine_supers (RCCL all-gather + the
-    // fixed-order total) and a one-wave kernel publishes the totals plus the completion word.
-    const bool inlaunch = ctx->fused_finish && !ctx->comm && ctx->nranks == 1;
+    // Shared row segment (any rank count): every pass -- server or launched -- writes its super rows
+    // there and every host takes the total.  Otherwise (RCCL only) the pass leaves its super
+    // partials, then combine_supers (RCCL all-gather + the fixed-order total) and a one-wave kernel
+    // publishes the totals plus the completion word.
+    const bool shm_rows = ctx->have_shm;
+    const bool inlaunch = ctx->fused_finish && !ctx->comm && ctx->nranks == 1 && !shm_rows;
     double* out = inlaunch ? ctx->d_h_red : nullptr;
     const bool gate = ctx->gated && poll && inlaunch && !ctx->profiling;
     const Xf34 Ax = A.xf();
     const CorrSoA c = corr_soa(ctx);
-    const int nsrv = (gate && ctx->resident) ? fdf_server_blocks(ns, ctx->cus, ctx->srv_waves) : 0;
+    const bool want_srv = ctx->resident && !ctx->srv_degraded && !ctx->profiling && !ctx->fdf_diag &&
+                          (gate || (shm_rows && ctx->poll));
+    const int cap = ctx->srv_cus > 0 ? std::min(ctx->srv_cus, ctx->cus) : ctx->cus;
+    int nsrv = want_srv ? fdf_server_blocks(ns, cap, ctx->srv_waves) : 0;
+    if (nsrv > 0 && !ctx->srv_live) {
+      int idle = 0;  // one server per device and process (g_srv_busy)
+      ctx->srv_locked = g_srv_busy[ctx->device & 63].compare_exchange_strong(idle, 1, std::memory_order_acq_rel);
+      if (!ctx->srv_locked) {
+        nsrv = 0;
+        ctx->st[kStSrvDenied]++;
+      }
+    }
+    const bool rows = shm_rows || (nsrv > 0 && ctx->host_rows);
+    if (rows && !ctx->srv_live && (rc = ensure_rows(ctx))) return rc;
     if (nsrv > 0) {
       // the resident server runs every pass of this BFGS run: start it with the first one
-      const long long nsup = ctx->nsup_local();
       if (!ctx->srv_live) {
         cancel_gated(ctx);
-        if (ctx->host_rows && (rc = ensure_rows(ctx, nsup))) return rc;
         ctx->ht_last_rows = 0;  // host-view diagnostics: a new BFGS run, not a host step
         HIPCK(hipMemsetAsync(ctx->tickets.p, 0, ctx->tickets_n * sizeof(unsigned int), ctx->stream));
+        const RowView rv = row_view(ctx);
         ProfScope ps(ctx, kFamFdf);
-        HIPCK(launch_fdf_server(c, ctx->cpos.p, ctx->chunk_base.p, ns, ctx->partial.p, ctx->spart.p,
-                                ctx->tickets.p, out, ctx->d_flag, seq, ctx->bar_cmd ? ctx->bar_cmd : ctx->d_cmd,
-                                ctx->mail, ctx->gate_timeout,
-                                ctx->d_ptimes, 0, Ax, ctx->host_rows ? ctx->d_rows : nullptr, nsrv, ctx->srv_waves,
-                                ctx->bar_cmd ? nsrv : 1, ctx->stream));
+        const hipError_t e = launch_fdf_server(
+            c, ctx->cpos.p, ctx->chunk_base.p, ns, ctx->partial.p, ctx->spart.p, ctx->tickets.p, out, ctx->d_flag, seq,
+            ctx->bar_cmd ? ctx->bar_cmd : ctx->d_cmd, ctx->mail, ctx->gate_timeout, ctx->d_ptimes, 0, Ax,
+            rows ? rv.dev_rows(0) : nullptr, rv.stride, nsrv, ctx->srv_waves, ctx->bar_cmd ? nsrv : 1,
+            ctx->stall_pass, ctx->stream);
+        if (e != hipSuccess) {
+          g_srv_busy[ctx->device & 63].store(0, std::memory_order_release);
+          ctx->srv_locked = false;
+          HIPCK(e);
+        }
         ctx->srv_live = true;
+        ctx->st[kStSrvLaunch]++;
+        ctx->st[kStBar] = ctx->bar_cmd ? 1 : 0;
       }
       const double t_pub = ctx->h_ptimes ? now_ms() : 0.0;
       if (ctx->h_ptimes && ctx->ht_last_rows > 0 && t_pub - ctx->ht_last_rows < 1.0) {
@@ -1166,10 +1339,11 @@ struct DeviceFunctor {
         ctx->ht_bfgs += t_entry - ctx->ht_last_rows;
         ++ctx->ht_nh;
       }
-      publish_cmd(ctx, seq, kPassRun, 0, &Ax);
+      publish_cmd(ctx, seq, kPassRun, 0, &Ax, rstamp);
       ctx->srv_next = seq + 1;
-      if (ctx->host_rows) {
-        if ((rc = wait_rows(ctx, seq, nsup, sums))) return rc;
+      ctx->st[kStSrvPass]++;
+      if (rows) {
+        if ((rc = wait_rows(ctx, rstamp, Ax, sums, true))) return rc;
         if (ctx->h_ptimes) {
           ctx->ht_last_rows = now_ms();
           ctx->ht_dev += ctx->ht_last_rows - t_pub;
@@ -1179,6 +1353,20 @@ struct DeviceFunctor {
         if ((rc = wait_pass(ctx, seq))) return rc;
         std::memcpy(sums, ctx->h_red, kRedVals * sizeof(double));
       }
+      ctx->n_evals++;
+      return MGICP_OK;
+    }
+    ctx->st[kStLaunchedPass]++;
+    if (shm_rows) {
+      // a launched pass into the shared rows (profiling, a degraded align, an unservable shard)
+      cancel_gated(ctx);
+      {
+        ProfScope ps(ctx, kFamFdf);
+        HIPCK(launch_fdf_soa(c, ctx->cpos.p, ctx->chunk_base.p, ns, Ax, ctx->partial.p, ctx->spart.p, nb,
+                             ctx->tickets.p, nullptr, reverse, nullptr, seq, ctx->stream,
+                             row_view(ctx).dev_rows(rstamp), rstamp));
+      }
+      if ((rc = wait_rows(ctx, rstamp, Ax, sums, false))) return rc;
       ctx->n_evals++;
       return MGICP_OK;
     }
@@ -1331,12 +1519,8 @@ int moments_pass(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool supers_only 
     }
   }
   if (supers_only) return sync(ctx);
-  int rc0 = combine_supers(ctx, kMomVals, ctx->msuper.p, ctx->mred.p);
-  if (rc0) return rc0;
-  HIPCK(hipMemcpyAsync(ctx->h_small, ctx->mred.p, kMomVals * sizeof(double), hipMemcpyDeviceToHost, s));
-  int rc = sync(ctx);
+  int rc = combine_to_host(ctx, kMomVals, ctx->msuper.p, ctx->mom);
   if (rc) return rc;
-  std::memcpy(ctx->mom, ctx->h_small, kMomVals * sizeof(double));
   ctx->n_evals++;
   return MGICP_OK;
 }
@@ -1435,6 +1619,16 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
   if (const char* sw = std::getenv("MGICP_SRV_WAVES")) ctx->srv_waves = std::atoi(sw) == 8 ? 8 : 4;
   if (const char* bc = std::getenv("MGICP_BAR_CMD")) ctx->bar = std::atoi(bc) != 0;
   if (const char* sp = std::getenv("MGICP_SPIN_PAUSE")) ctx->spin_pause = std::atoi(sp) != 0;
+  if (const char* sc = std::getenv("MGICP_SRV_CUS")) ctx->srv_cus = std::max(0, std::atoi(sc));
+  if (const char* sp = std::getenv("MGICP_SRV_STALL_PASS")) ctx->stall_pass = std::atoi(sp);
+  if (const char* dl = std::getenv("MGICP_ROW_DEADLINE_MS")) {
+    const double v = std::atof(dl);
+    if (v > 0) ctx->row_deadline_ms = v;
+  }
+  if (const char* rd = std::getenv("MGICP_REMOTE_DEADLINE_S")) {
+    const double v = std::atof(rd);
+    if (v > 0) ctx->remote_deadline_s = v;
+  }
   ctx->knn_logged = knn_logged_enabled();
   if (const char* st = std::getenv("MGICP_SPLIT_TARGET_COV")) ctx->split_target_cov = std::atoi(st) != 0;
   if (const char* ps = std::getenv("MGICP_PROF_STRIDE")) ctx->prof_stride = std::max(1, std::atoi(ps));
@@ -1554,6 +1748,11 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   if (ctx->h_gtrace) (void)hipHostFree(ctx->h_gtrace);
   if (ctx->h_ptimes) (void)hipHostFree(ctx->h_ptimes);
   if (ctx->h_rows) (void)hipHostFree(ctx->h_rows);
+  if (ctx->have_shm) {
+    (void)hipHostUnregister(ctx->shm.base);
+    shm::detach(ctx->shm);
+    ctx->have_shm = false;
+  }
   if (ctx->bar_cmd) (void)hipFree(ctx->bar_cmd);
   if (ctx->h_small) (void)hipHostFree(ctx->h_small);
   prof_resolve(ctx);
@@ -1586,7 +1785,7 @@ int mgicp_set_source_device(mgicp_ctx* ctx, const float* d_xyz, size_t n, size_t
 
 int mgicp_align(mgicp_ctx* ctx, const float guess_cm[16], float out_T_cm[16], mgicp_result* res) {
   if (!ctx || !out_T_cm) return MGICP_E_INVALID;
-  if (ctx->nranks > 1 && !ctx->comm)
+  if (ctx->nranks > 1 && !ctx->comm && !ctx->have_shm)
     return fail(ctx, MGICP_E_INVALID, "detached shard context: only the debug entry points are available");
   HIPCK(hipSetDevice(ctx->device));
   mgicp_result r;
@@ -1606,6 +1805,7 @@ int mgicp_align(mgicp_ctx* ctx, const float guess_cm[16], float out_T_cm[16], mg
   Mat4 T = Mat4::identity(), prev = Mat4::identity();
   ctx->trace.clear();
   ctx->n_evals = 0;
+  ctx->srv_degraded = false;  // a take-over degrades the rest of one align only
   int nr_iterations = 0;
   bool converged = false;
   int solver_rc = MGICP_OK;
@@ -1727,7 +1927,7 @@ static int fitness_supers(mgicp_ctx* ctx, const Mat4& T, double max_range) {
 
 int mgicp_fitness(mgicp_ctx* ctx, const float T_cm[16], double max_range, double* out) {
   if (!ctx || !T_cm || !out) return MGICP_E_INVALID;
-  if (ctx->nranks > 1 && !ctx->comm)
+  if (ctx->nranks > 1 && !ctx->comm && !ctx->have_shm)
     return fail(ctx, MGICP_E_INVALID, "detached shard context: only the debug entry points are available");
   HIPCK(hipSetDevice(ctx->device));
   int rc = prepare(ctx, false);
@@ -1736,11 +1936,10 @@ int mgicp_fitness(mgicp_ctx* ctx, const float T_cm[16], double max_range, double
   if (!(max_range > 0)) max_range = 1.7976931348623157e308;
   const Mat4 T = Mat4::from_cm(T_cm);
   if ((rc = fitness_supers(ctx, T, max_range))) return rc;
-  if ((rc = combine_supers(ctx, kRedVals, ctx->spart.p, ctx->red.p))) return rc;
-  HIPCK(hipMemcpyAsync(ctx->h_red, ctx->red.p, kRedVals * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
-  if ((rc = sync(ctx))) return rc;
-  const double nr = ctx->h_red[13];
-  *out = nr > 0 ? ctx->h_red[0] / nr : 1.7976931348623157e308;
+  double tot[kRedVals];
+  if ((rc = combine_to_host(ctx, kRedVals, ctx->spart.p, tot))) return rc;
+  const double nr = tot[13];
+  *out = nr > 0 ? tot[0] / nr : 1.7976931348623157e308;
   return MGICP_OK;
 }
 
@@ -2024,18 +2223,72 @@ int mgicp_comm_init(mgicp_ctx* ctx, int nranks, int rank, const unsigned char id
     (void)ncclCommDestroy(ctx->comm);
     ctx->comm = nullptr;
   }
+  if (ctx->have_shm) {  // the segment's geometry belongs to the old rank layout
+    int rc = sync(ctx);
+    if (rc) return rc;
+    (void)hipHostUnregister(ctx->shm.base);
+    shm::detach(ctx->shm);
+    ctx->have_shm = false;
+  }
   ctx->nranks = nranks;
   ctx->rank = rank;
   ctx->qperm_valid = false;
   ctx->src.have_cov = false;
   ctx->have_corr = false;
   ctx->seed_valid = false;  // the shard (and its per-point match buffers) changes
-  // id == NULL: detached shard (debug entry points only).  nranks == 1 with an id builds a real
-  // one-rank communicator, so the collective code path can be exercised on a single device.
+  ctx->st[kStTransport] = 0;
+  // id == NULL: detached shard (debug entry points only, until mgicp_comm_attach_shm).  nranks == 1
+  // with an id builds a real one-rank communicator, so the collective code path can be exercised on
+  // a single device.
   if (!id) return MGICP_OK;
   ncclUniqueId uid;
   std::memcpy(&uid, id, 128);
   NCCLCK(ncclCommInitRank(&ctx->comm, nranks, uid, rank));
+  ctx->st[kStTransport] = 1;
+  return MGICP_OK;
+}
+
+int mgicp_comm_attach_shm(mgicp_ctx* ctx, const char* name, size_t max_source_points) {
+  if (!ctx) return MGICP_E_INVALID;
+  HIPCK(hipSetDevice(ctx->device));
+  int rc = sync(ctx);
+  if (rc) return rc;
+  if (ctx->have_shm) {
+    (void)hipHostUnregister(ctx->shm.base);
+    shm::detach(ctx->shm);
+    ctx->have_shm = false;
+    ctx->st[kStTransport] = ctx->comm ? 1 : 0;
+  }
+  if (!name) return MGICP_OK;  // detach only
+  if (max_source_points == 0) max_source_points = size_t(32) << 20;
+  if (max_source_points >= (size_t(1) << 31))
+    return fail(ctx, MGICP_E_INVALID, "max_source_points: at most 2^31 - 2 points per cloud");
+  const long long max_sup = static_cast<long long>((max_source_points + kSuperPts - 1) / kSuperPts);
+  std::string err;
+  shm::Segment seg;
+  if (!shm::attach(seg, name, ctx->nranks, ctx->rank, max_sup, ctx->remote_deadline_s, err))
+    return fail(ctx, MGICP_E_COMM, err);
+  // the GPU writes its rows straight into the segment: map it into the device's address space
+  hipError_t e = hipHostRegister(seg.base, seg.bytes, hipHostRegisterMapped);
+  void* d = nullptr;
+  if (e == hipSuccess) e = hipHostGetDevicePointer(&d, seg.base, 0);
+  if (e != hipSuccess) {
+    (void)hipHostUnregister(seg.base);
+    shm::detach(seg);
+    return fail(ctx, MGICP_E_HIP, std::string("hipHostRegister of the shared row segment: ") + hipGetErrorString(e));
+  }
+  ctx->shm = seg;
+  ctx->shm_d = static_cast<unsigned char*>(d);
+  ctx->have_shm = true;
+  ctx->pass_idx = 0;    // row stamps and gather indices count from the attach on every rank
+  ctx->gather_idx = 0;
+  ctx->st[kStTransport] = ctx->comm ? 3 : 2;
+  return MGICP_OK;
+}
+
+int mgicp_debug_pass_stats(mgicp_ctx* ctx, long long out[8]) {
+  if (!ctx || !out) return MGICP_E_INVALID;
+  for (int i = 0; i < kStCount; ++i) out[i] = ctx->st[i];
   return MGICP_OK;
 }
 
@@ -2140,7 +2393,7 @@ int mgicp_debug_pass_bench(mgicp_ctx* ctx, const double x[6], int npasses, int m
                            double out16[16]) {
   if (!ctx || !x || npasses < 1 || npasses > 100000 || (mode != 0 && mode != 1) || !ctx->have_corr)
     return MGICP_E_INVALID;
-  if (ctx->comm || ctx->nranks != 1)
+  if (ctx->comm || ctx->nranks != 1 || ctx->have_shm)
     return fail(ctx, MGICP_E_INVALID, "pass bench: single-rank contexts only");
   HIPCK(hipSetDevice(ctx->device));
   int rc = sync(ctx);  // cancels any queued pass / live server
@@ -2156,21 +2409,23 @@ int mgicp_debug_pass_bench(mgicp_ctx* ctx, const double x[6], int npasses, int m
   HIPCK(hipEventCreate(&b));
   HIPCK(hipEventRecord(a, ctx->stream));
   hipError_t e = hipSuccess;
-  const long long nsup = ctx->nsup_local();
   const bool rows = mode == 0 && ctx->host_rows;
-  if (rows && (rc = ensure_rows(ctx, nsup))) return rc;
+  if (rows && (rc = ensure_rows(ctx))) return rc;
   if (rows) HIPCK(hipMemsetAsync(ctx->tickets.p, 0, ctx->tickets_n * sizeof(unsigned int), ctx->stream));
   if (mode == 0) {
-    const int nb = fdf_server_blocks(ns, ctx->cus, ctx->srv_waves);
+    const int cap = ctx->srv_cus > 0 ? std::min(ctx->srv_cus, ctx->cus) : ctx->cus;
+    const int nb = fdf_server_blocks(ns, cap, ctx->srv_waves);
     if (nb <= 0) {
       (void)hipEventDestroy(a);
       (void)hipEventDestroy(b);
       return fail(ctx, MGICP_E_INVALID, "pass bench: shard not servable by the resident server");
     }
     const unsigned long long seq0 = ++ctx->pass_seq;
+    const RowView rv = row_view(ctx);
     e = launch_fdf_server(c, ctx->cpos.p, ctx->chunk_base.p, ns, ctx->partial.p, ctx->spart.p, ctx->tickets.p,
                           ctx->d_h_red, ctx->d_flag, seq0, ctx->d_cmd, ctx->mail, ctx->gate_timeout, ctx->d_ptimes,
-                          npasses, A, rows ? ctx->d_rows : nullptr, nb, ctx->srv_waves, 1, ctx->stream);
+                          npasses, A, rows ? rv.dev_rows(0) : nullptr, rv.stride, nb, ctx->srv_waves, 1, -1,
+                          ctx->stream);
     ctx->pass_seq = seq0 + static_cast<unsigned long long>(npasses);  // the closing cancel's stamp too
   } else {
     const int nb = fdf_grid_blocks(ns, ctx->fdf_max_blocks);
@@ -2189,7 +2444,9 @@ int mgicp_debug_pass_bench(mgicp_ctx* ctx, const double x[6], int npasses, int m
     // the host-row tickets are left as multiples of the supers' sizes: re-arm them
     HIPCK(hipMemsetAsync(ctx->tickets.p, 0, ctx->tickets_n * sizeof(unsigned int), ctx->stream));
     double tot[kRedVals];
-    if ((rc = wait_rows(ctx, ctx->pass_seq - 1, nsup, tot))) return rc;
+    // the timing form stamps each pass's rows with its sequence number | 2^31
+    const Xf34 unused{};
+    if ((rc = wait_rows(ctx, static_cast<unsigned int>(ctx->pass_seq - 1) | 0x80000000u, unused, tot, false))) return rc;
     if ((rc = sync(ctx))) return rc;
     if (out16) std::memcpy(out16, tot, kRedVals * sizeof(double));
   } else {
@@ -2226,6 +2483,8 @@ int mgicp_debug_supers(mgicp_ctx* ctx, int kind, const double* arg, double* out,
     Vec6 x;
     for (int i = 0; i < 6; ++i) x[i] = arg[i];
     const size_t ns = ctx->shard_p1() - ctx->shard_p0();
+    // host-row passes leave the tickets as multiples of their supers' sizes
+    HIPCK(hipMemsetAsync(ctx->tickets.p, 0, ctx->tickets_n * sizeof(unsigned int), ctx->stream));
     HIPCK(launch_fdf_soa(corr_soa(ctx), ctx->cpos.p, ctx->chunk_base.p, ns, apply_state(x).xf(), ctx->partial.p,
                          ctx->spart.p, fdf_grid_blocks(ns, ctx->fdf_max_blocks), ctx->tickets.p, nullptr, 0,
                          nullptr, 0, ctx->stream));

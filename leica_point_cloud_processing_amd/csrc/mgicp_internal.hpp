@@ -90,10 +90,13 @@ struct Xf34 { float m[12]; };
 // word (low 32 bits) and the low 32 bits of the pass's sequence number (high 32 bits); aligned
 // 8-byte stores and loads are single-copy atomic on both sides, so a reader that finds the stamp
 // in all kCmdWords halves holds a complete command of that pass -- in the same PCIe round trip
-// that detects it.  Words: [0..11] A (Xf34 bit patterns), [12] op, [13] sweep direction.
+// that detects it.  Words: [0..11] A (Xf34 bit patterns), [12] op, [13] sweep direction, [14] the
+// pass's row stamp (host-row passes: the objective-pass index, identical on every rank, that stamps
+// the super rows and selects their parity buffer).  A waiting block that finds a complete command
+// with a LATER sequence number was left behind by a cancel and exits.
 constexpr unsigned int kPassRun = 1;
 constexpr unsigned int kPassCancel = 2;
-constexpr int kCmdWords = 14;
+constexpr int kCmdWords = 15;
 struct alignas(128) PassCmd {
   unsigned long long h[16];
 };
@@ -142,9 +145,12 @@ hipError_t launch_compact(const float4* src, const float4* tpts, const Cov3& cov
 // tickets: one per super + one, zero between passes.  done_flag (nullable, mapped host memory):
 // the finishing wave stores `seq` there with a system-scope release after `out`, so the host can
 // poll instead of synchronising the stream
+// host_rows (nullable): super partials as stamped host rows (stamp rstamp, this pass's parity buffer
+// at the rank's first super; tickets counted modulo the supers' sizes) instead of spart / out
 hipError_t launch_fdf_soa(const CorrSoA& c, const uint32_t* pos, const uint32_t* base, size_t ns, Xf34 A,
                           double* partial, double* spart, int nb, unsigned int* tickets, double* out, int reverse,
-                          unsigned long long* done_flag, unsigned long long seq, hipStream_t s);
+                          unsigned long long* done_flag, unsigned long long seq, hipStream_t s,
+                          unsigned long long* host_rows = nullptr, unsigned int rstamp = 0);
 // the same pass pre-launched before its state is known: block 0 waits for cmd->seq == seq (or for
 // `timeout_ticks` of wall_clock64) and forwards the command to `mail` (device memory) for the other
 // blocks; then every block runs with its A / reverse, or exits on a cancel
@@ -155,8 +161,8 @@ hipError_t launch_fdf_soa_gated(const CorrSoA& c, const uint32_t* pos, const uin
                                 unsigned long long* gtrace /*nullable: diagnostics*/,
                                 int host_pollers /*blocks [0, host_pollers) poll the host copy*/, hipStream_t s);
 int        fdf_grid_blocks(size_t ns, int max_blocks = 2048);
-// the resident pass server (one cooperative launch per BFGS run, see mgicp_kernels.hip): passes
-// seq0, seq0 + 1, ... each run on the command with that stamp, until a cancel; bench_passes > 0
+// the resident pass server (one launch per BFGS run, see mgicp_kernels.hip): passes seq0, seq0 + 1,
+// ... each run on the command with that stamp, until a cancel (or a later command); bench_passes > 0
 // (timing): that many passes of A back to back without commands.  fdf_server_blocks: its grid for a
 // shard of ns positions on `cus` CUs (0: not servable, use the launched passes)
 int        fdf_server_blocks(size_t ns, int cus, int waves /*4 or 8 per CU*/);
@@ -165,8 +171,10 @@ hipError_t launch_fdf_server(const CorrSoA& c, const uint32_t* pos, const uint32
                              unsigned long long seq0, const PassCmd* cmd, PassCmd* mail,
                              unsigned long long timeout_ticks, unsigned long long* ptimes /*nullable*/,
                              int bench_passes, Xf34 A,
-                             unsigned long long* host_rows /*nullable: super rows to the host*/, int nb,
-                             int waves, int pollers /*blocks reading cmd themselves (1 or nb)*/, hipStream_t s);
+                             unsigned long long* host_rows /*nullable: super rows to the host, parity 0*/,
+                             size_t rows_stride /*words from the parity-0 to the parity-1 row buffer*/, int nb,
+                             int waves, int pollers /*blocks reading cmd themselves (1 or nb)*/,
+                             int stall_pass /*tests: -1, or the pass the last block withholds*/, hipStream_t s);
 
 // super partials of nch chunk partials of nv (kRedVals or kMomVals) values
 hipError_t launch_super_reduce(const double* chunk, int nch, int nv, double* sup, hipStream_t s);

@@ -1361,11 +1361,14 @@ __device__ __forceinline__ void fdf_group(const Xf34& A, const CorrGroup& g, dou
 // The gate of a pass whose state is not known at launch (pre-launched gated passes and the
 // resident pass server).  Every block's thread 0 polls a command block until it carries this
 // pass's sequence number: blocks [0, host_pollers) the host-written copy (pinned, mapped,
-// system-coherent loads), the others the device mailbox block 0 forwards it to.  Returns false on a
-// cancel command or after `timeout` wall-clock ticks (every wave reaches an exit).
+// system-coherent loads, or device memory the host stores into through the BAR), the others the
+// device mailbox block 0 forwards it to.  Returns false on a cancel command, on a complete command
+// with a LATER sequence number (this block was left behind by a cancel: a server whose blocks could
+// not all be resident when the host gave up on a pass), or after `timeout` wall-clock ticks -- every
+// wave reaches an exit.  rstamp: the command's row stamp (word 14).
 __device__ __forceinline__ bool pass_gate(unsigned long long seq, const PassCmd* cmd, PassCmd* mail,
                                           unsigned long long timeout, unsigned long long* gtrace,
-                                          int host_pollers, Xf34& A, int& reverse) {
+                                          int host_pollers, Xf34& A, int& reverse, unsigned int& rstamp) {
   __shared__ unsigned int sw[kCmdWords];
   __shared__ int sok;
   __syncthreads();  // sw / sok of the previous gate of this block are consumed
@@ -1377,14 +1380,17 @@ __device__ __forceinline__ bool pass_gate(unsigned long long seq, const PassCmd*
     const unsigned int stamp = static_cast<unsigned int>(seq);
     const unsigned long long t0 = wall_clock64();
     unsigned long long v[16];
-    bool got = false;
+    bool got = false, later = false;
     for (;;) {
       if (host_poller) read_cmd<true>(cmd, v);
       else read_cmd<false>(mail, v);
-      bool all = true;
+      const unsigned int st0 = static_cast<unsigned int>(v[0] >> 32);
+      bool same = true;
 #pragma unroll
-      for (int i = 0; i < kCmdWords; ++i) all = all && static_cast<unsigned int>(v[i] >> 32) == stamp;
-      if (all) { got = true; break; }
+      for (int i = 1; i < kCmdWords; ++i) same = same && static_cast<unsigned int>(v[i] >> 32) == st0;
+      if (same && st0 == stamp) { got = true; break; }
+      // a complete, newer command: the host has moved past this pass (signed 32-bit distance)
+      if (same && static_cast<int>(st0 - stamp) > 0) { later = true; break; }
       if (wall_clock64() - t0 > timeout) break;  // no command: give up as if cancelled
       __builtin_amdgcn_s_sleep(1);
     }
@@ -1392,9 +1398,12 @@ __device__ __forceinline__ bool pass_gate(unsigned long long seq, const PassCmd*
       gtrace[4 * (seq & 1023)] = t0;
       gtrace[4 * (seq & 1023) + 1] = wall_clock64();
     }
-    if (!got) {  // a timeout forwards a cancel, so every block exits promptly
+    if (!got) {
+      // a timeout or a later command forwards a cancel (stamped with the later sequence number
+      // when there is one), so every block still waiting for this pass exits promptly
+      const unsigned long long st = later ? (v[0] >> 32) : static_cast<unsigned long long>(stamp);
 #pragma unroll
-      for (int i = 0; i < kCmdWords; ++i) v[i] = (static_cast<unsigned long long>(stamp) << 32) | (i == 12 ? kPassCancel : 0u);
+      for (int i = 0; i < kCmdWords; ++i) v[i] = (st << 32) | (i == 12 ? kPassCancel : 0u);
     }
 #pragma unroll
     for (int i = 0; i < kCmdWords; ++i) sw[i] = static_cast<unsigned int>(v[i]);
@@ -1408,6 +1417,7 @@ __device__ __forceinline__ bool pass_gate(unsigned long long seq, const PassCmd*
 #pragma unroll
   for (int i = 0; i < 12; ++i) A.m[i] = __uint_as_float(sw[i]);
   reverse = static_cast<int>(sw[13]);
+  rstamp = sw[14];
   return true;
 }
 
@@ -1432,17 +1442,20 @@ __device__ __forceinline__ void chunk_store(int j, double (&acc)[kRedVals], cons
 // After a wave stored all its chunk partials (chunks w0, w0 + nw, ...; reverse & 1: counted from
 // the back): tickets, the supers it completes, and -- for the wave completing the last super -- the
 // total into `out` and `seq` into done_flag.  Returns true on that finishing wave.
-// host_rows (nullable, mapped host memory, 32 words per super): each super partial goes straight to
-// the host as one 256-byte store of stamped halves ((seq << 32) | 32-bit half, value v in words 2v
-// (low) and 2v + 1 (high)); the host takes the total in wave_total's order, so there is no global
-// ticket, device total or completion flag on the pass's critical path (returns false).  chain
-// (timing form only): after its row, each super wave also takes a global ticket (modulo the super
-// count) and the wave completing the last super returns true, to forward the next command.
+// host_rows (nullable, mapped host memory -- private, or a node-wide shared segment at this rank's
+// first super -- 32 words per super, already offset to this pass's parity buffer): each super
+// partial goes straight to the host as one 256-byte store of stamped halves ((rstamp << 32) |
+// 32-bit half, value v in words 2v (low) and 2v + 1 (high)); the host takes the total in
+// wave_total's order, so there is no global ticket, device total or completion flag on the pass's
+// critical path (returns false).  chain (timing form only): after its row, each super wave also
+// takes a global ticket (modulo the super count) and the wave completing the last super returns
+// true, to forward the next command.
 __device__ __forceinline__ bool wave_tickets(int w0, int nw, int nch, int reverse, unsigned int* __restrict__ tickets,
                                              const double* __restrict__ partial, double* __restrict__ spart,
                                              double* __restrict__ out, unsigned long long* done_flag,
                                              unsigned long long seq, int lane,
-                                             unsigned long long* host_rows = nullptr, bool chain = false) {
+                                             unsigned long long* host_rows = nullptr, bool chain = false,
+                                             unsigned int rstamp = 0) {
   const int nsup = (nch + kSuperChunks - 1) / kSuperChunks;
   // tickets, once per wave after all of its chunks (a per-chunk drain + atomic round trip cost
   // ~60 us per pass at 256 blocks): lane k takes the super of the wave's k-th chunk
@@ -1488,7 +1501,7 @@ __device__ __forceinline__ bool wave_tickets(int w0, int nw, int nch, int revers
       // system-coherent write-through (sc0 sc1): a plain store to mapped host memory may sit in the
       // L2 until something releases it; the 32 lanes' 8-byte words leave as one 256-byte burst
       if (lane < 32) {
-        const unsigned long long w = (static_cast<unsigned long long>(static_cast<unsigned int>(seq)) << 32) | half;
+        const unsigned long long w = (static_cast<unsigned long long>(rstamp) << 32) | half;
         asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1" ::"v"(host_rows + static_cast<size_t>(sj) * 32 + lane),
                      "v"(w)
                      : "memory");
@@ -1533,6 +1546,9 @@ __device__ __forceinline__ bool wave_tickets(int w0, int nw, int nch, int revers
 // returns at once on a cancel command (or after `timeout` wall-clock ticks: every wave reaches
 // an exit).  The host pre-launches pass k + 1 while pass k runs, so the next pass is resident
 // when the host's BFGS step publishes x_{k+1}: no launch latency between consecutive passes.
+// host_rows (nullable): the launched pass writes its super partials as stamped host rows (stamp
+// rstamp, tickets counted modulo the supers' sizes) instead of a device total -- the form of the
+// server's passes, used when a server pass is taken over (missed deadline) or cannot run.
 template <bool kGated>
 __device__ __forceinline__ void fdf_soa_body(CorrSoA c, const uint32_t* __restrict__ pos,
                                              const uint32_t* __restrict__ base, size_t ns, int nch, Xf34 A,
@@ -1541,9 +1557,9 @@ __device__ __forceinline__ void fdf_soa_body(CorrSoA c, const uint32_t* __restri
                                              int reverse, unsigned long long* done_flag,
                                              unsigned long long seq, const PassCmd* cmd, PassCmd* mail,
                                              unsigned long long timeout, unsigned long long* gtrace,
-                                             int host_pollers) {
+                                             int host_pollers, unsigned long long* host_rows, unsigned int rstamp) {
   if constexpr (kGated) {
-    if (!pass_gate(seq, cmd, mail, timeout, gtrace, host_pollers, A, reverse)) return;
+    if (!pass_gate(seq, cmd, mail, timeout, gtrace, host_pollers, A, reverse, rstamp)) return;
   }
   // persistent waves over the shard's chunks (reverse: back to front, so the tail of the previous
   // pass, still in the 256 MiB Infinity Cache, is consumed first)
@@ -1575,13 +1591,15 @@ __device__ __forceinline__ void fdf_soa_body(CorrSoA c, const uint32_t* __restri
     chunk_store(j, acc, pos, ns, partial, lane);
   }
   if (w0 >= nch || (reverse & 6)) return;
-  wave_tickets(w0, nw, nch, reverse, tickets, partial, spart, out, done_flag, seq, lane);
+  wave_tickets(w0, nw, nch, reverse, tickets, partial, spart, out, done_flag, seq, lane, host_rows, false, rstamp);
 }
 
 // ---- the resident pass server --------------------------------------------------------------
 // All objective passes of one BFGS run read the SAME compacted streams (72 B per correspondence,
-// 360 MB at C4).  The server is ONE cooperative launch per BFGS run with one 4-wave block per CU
-// (1 wave per SIMD, up to 512 VGPR+AGPR per lane): each wave keeps its first chunk (4 groups per
+// 360 MB at C4).  The server is ONE launch per BFGS run with one 4-wave block per CU (1 wave per
+// SIMD, up to 512 VGPR+AGPR per lane; a plain launch after an occupancy check -- its blocks wait on
+// the host's commands, not on each other, and a block that is not resident when the host gives up
+// on a pass exits at its first gate, see pass_gate): each wave keeps its first chunk (4 groups per
 // lane, 288 dwords) in registers and half of its second chunk (2 groups per lane, 36 KiB per wave,
 // 144 KiB per CU) in LDS for the whole run, and streams only the rest from HBM / Infinity Cache.
 // Between passes every block waits at the gate for the host's next command (pass_gate); the
@@ -1610,13 +1628,16 @@ struct SrvShape<8> {
 
 // kBench: the timing instantiation (bench_passes > 0) -- a symbol of its own, so a rocprofv3 kernel
 // trace separates it from the servers of the aligns (its duration / bench_passes = one pass)
+// host_rows: parity-0 row buffer at this rank's first super, rows_stride words to the parity-1
+// buffer (a pass writes into buffer rstamp & 1).  stall_pass >= 0 (tests only): the last block skips
+// that pass (relative to seq0) entirely, so the host must take it over.
 template <bool kBench, int kWaves>
 __global__ __launch_bounds__(64 * kWaves, 1) void fdf_server_kernel(
     CorrSoA c, const uint32_t* __restrict__ pos, const uint32_t* __restrict__ base, size_t ns, int nch,
     double* __restrict__ partial, double* __restrict__ spart, unsigned int* __restrict__ tickets,
     double* __restrict__ out, unsigned long long* done_flag, unsigned long long seq0, const PassCmd* cmd,
     PassCmd* mail, unsigned long long timeout, unsigned long long* ptimes, int bench_passes, Xf34 Abench,
-    unsigned long long* host_rows, int pollers) {
+    unsigned long long* host_rows, size_t rows_stride, int pollers, int stall_pass) {
   constexpr int kR = SrvShape<kWaves>::kReg, kL = SrvShape<kWaves>::kLds;
   static_assert(kR <= 4 && (kR == 4 || kR + kL <= 4), "resident groups: chunk 0, then chunk 1 only after a full chunk 0");
   __shared__ float4 lf[kWaves][kL][6][64];
@@ -1670,7 +1691,14 @@ __global__ __launch_bounds__(64 * kWaves, 1) void fdf_server_kernel(
   for (unsigned long long seq = seq0;; ++seq) {
     Xf34 A = Abench;
     int rev = 0;
-    if (!(kBench && seq == seq0) && !pass_gate(seq, cmd, mail, timeout, nullptr, host_pollers, A, rev)) return;
+    // the timing form stamps rows with seq | 2^31 (align passes stamp their pass index, < 2^31)
+    unsigned int rstamp = static_cast<unsigned int>(seq) | 0x80000000u;
+    if (!(kBench && seq == seq0) && !pass_gate(seq, cmd, mail, timeout, nullptr, host_pollers, A, rev, rstamp))
+      return;
+    if (stall_pass >= 0 && seq - seq0 == static_cast<unsigned long long>(stall_pass) &&
+        blockIdx.x == gridDim.x - 1)
+      continue;  // tests: withhold this block's share of the pass
+    unsigned long long* rows = host_rows ? host_rows + (rstamp & 1u) * rows_stride : nullptr;
     if (ptimes && blockIdx.x == 0 && threadIdx.x == 0) ptimes[2 * (seq & 1023)] = wall_clock64();
     // odd waves take their streamed chunks first and their resident ones last, even waves the
     // reverse: the CU's memory pipe is never left idle while all its waves compute resident data
@@ -1739,18 +1767,20 @@ __global__ __launch_bounds__(64 * kWaves, 1) void fdf_server_kernel(
     if (w0 >= nch) continue;
     // the timing form writes host rows too when given them (chained on the device by a global
     // ticket), so it times the pass the aligns run
-    const bool fin = wave_tickets(w0, nw, nch, 0, tickets, partial, spart, out, done_flag, seq, lane, host_rows,
-                                  kBench && host_rows);
+    const bool fin = wave_tickets(w0, nw, nch, 0, tickets, partial, spart, out, done_flag, seq, lane, rows,
+                                  kBench && rows, rstamp);
     if (fin && lane == 0) {
       if (ptimes) ptimes[2 * (seq & 1023) + 1] = wall_clock64();
       if (kBench) {
         // the next bench pass (or a cancel after the last), forwarded like block 0 forwards the host's
         unsigned long long v[16] = {};
         const bool more = seq + 1 < seq0 + static_cast<unsigned long long>(bench_passes);
-        const unsigned long long st = static_cast<unsigned long long>(static_cast<unsigned int>(seq + 1)) << 32;
+        const unsigned int s1 = static_cast<unsigned int>(seq + 1);
+        const unsigned long long st = static_cast<unsigned long long>(s1) << 32;
 #pragma unroll
         for (int i = 0; i < kCmdWords; ++i)
-          v[i] = st | (i < 12 ? (more ? __float_as_uint(Abench.m[i]) : 0u) : (i == 12 ? (more ? kPassRun : kPassCancel) : 0u));
+          v[i] = st | (i < 12 ? (more ? __float_as_uint(Abench.m[i]) : 0u)
+                              : (i == 12 ? (more ? kPassRun : kPassCancel) : (i == 14 ? (s1 | 0x80000000u) : 0u)));
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         write_mail(mail, v);
       }
@@ -1763,9 +1793,10 @@ __global__ __launch_bounds__(256) void fdf_soa_kernel(CorrSoA c, const uint32_t*
                                                       double* __restrict__ partial, double* __restrict__ spart,
                                                       unsigned int* __restrict__ tickets, double* __restrict__ out,
                                                       int reverse, unsigned long long* done_flag,
-                                                      unsigned long long seq) {
+                                                      unsigned long long seq, unsigned long long* host_rows,
+                                                      unsigned int rstamp) {
   fdf_soa_body<false>(c, pos, base, ns, nch, A, partial, spart, tickets, out, reverse, done_flag, seq, nullptr,
-                      nullptr, 0, nullptr, 0);
+                      nullptr, 0, nullptr, 0, host_rows, rstamp);
 }
 
 __global__ __launch_bounds__(256) void fdf_soa_gated_kernel(CorrSoA c, const uint32_t* __restrict__ pos,
@@ -1777,7 +1808,7 @@ __global__ __launch_bounds__(256) void fdf_soa_gated_kernel(CorrSoA c, const uin
                                                             PassCmd* mail, unsigned long long timeout,
                                                             unsigned long long* gtrace, int host_pollers) {
   fdf_soa_body<true>(c, pos, base, ns, nch, Xf34{}, partial, spart, tickets, out, 0, done_flag, seq, cmd, mail,
-                     timeout, gtrace, host_pollers);
+                     timeout, gtrace, host_pollers, nullptr, 0);
 }
 
 // ------------------------------------------------------------------------------------
@@ -2237,11 +2268,12 @@ hipError_t launch_compact(const float4* src, const float4* tpts, const Cov3& cov
 
 hipError_t launch_fdf_soa(const CorrSoA& c, const uint32_t* pos, const uint32_t* base, size_t ns, Xf34 A,
                           double* partial, double* spart, int nb, unsigned int* tickets, double* out, int reverse,
-                          unsigned long long* done_flag, unsigned long long seq, hipStream_t s) {
+                          unsigned long long* done_flag, unsigned long long seq, hipStream_t s,
+                          unsigned long long* host_rows, unsigned int rstamp) {
   const int nch = chunk_count(ns);
   if (nch == 0) return hipSuccess;
   fdf_soa_kernel<<<nb, 256, 0, s>>>(c, pos, base, ns, nch, A, partial, spart, tickets, out, reverse, done_flag,
-                                    seq);
+                                    seq, host_rows, rstamp);
   return hipGetLastError();
 }
 
@@ -2271,14 +2303,16 @@ hipError_t launch_fdf_server(const CorrSoA& c, const uint32_t* pos, const uint32
                              double* spart, unsigned int* tickets, double* out, unsigned long long* done_flag,
                              unsigned long long seq0, const PassCmd* cmd, PassCmd* mail,
                              unsigned long long timeout_ticks, unsigned long long* ptimes, int bench_passes,
-                             Xf34 A, unsigned long long* host_rows, int nb, int waves, int pollers,
-                             hipStream_t s) {
+                             Xf34 A, unsigned long long* host_rows, size_t rows_stride, int nb, int waves,
+                             int pollers, int stall_pass, hipStream_t s) {
   int nch = chunk_count(ns);
   if (nch == 0 || nb <= 0 || (waves != 4 && waves != 8)) return hipErrorInvalidValue;
-  // every block must be resident at once (the blocks wait on each other's commands): refuse a grid
-  // the device cannot hold (one block per CU, at most one per CU by its LDS and registers).  A plain
-  // launch after this check: a cooperative launch checks the same, but under rocprofv3 the process
-  // then crashed in the runtime's teardown after the profiler had finalised (r02)
+  // a pass completes only when every block has run it, so refuse a grid the device cannot hold at
+  // once (one block per CU, at most one per CU by its LDS and registers).  That check is all a
+  // cooperative launch adds; the blocks do not synchronise with each other (only with the host's
+  // commands), and a server whose blocks cannot all be resident (other work on the device) is
+  // cancelled by the host after its deadline -- blocks that start late see the later command at
+  // their first gate and exit (pass_gate) -- and the pass re-runs as a launched pass.
   const bool b = bench_passes > 0;
   const void* fn = waves == 4 ? (b ? reinterpret_cast<const void*>(fdf_server_kernel<true, 4>)
                                    : reinterpret_cast<const void*>(fdf_server_kernel<false, 4>))
@@ -2293,7 +2327,7 @@ hipError_t launch_fdf_server(const CorrSoA& c, const uint32_t* pos, const uint32
 #define MGICP_SRV_LAUNCH(B, W)                                                                                  \
   fdf_server_kernel<B, W><<<nb, 64 * (W), 0, s>>>(c, pos, base, ns, nch, partial, spart, tickets, out, done_flag, \
                                                   seq0, cmd, mail, timeout_ticks, ptimes, bench_passes, A, host_rows, \
-                                                  pollers)
+                                                  rows_stride, pollers, stall_pass)
   if (waves == 4) {
     if (b) MGICP_SRV_LAUNCH(true, 4);
     else MGICP_SRV_LAUNCH(false, 4);

@@ -267,6 +267,25 @@ class GICPEngine:
         buf = ctypes.create_string_buffer(uid, 128) if uid is not None else None
         self._check(self._lib.mgicp_comm_init(self._h, nranks, rank, buf), "comm_init")
 
+    def attach_shm(self, name: str, max_source_points: int = 0):
+        """Node-local transport of the per-pass sums (every rank, same name): the GPUs write their
+        super rows into one shared-memory segment, every host takes the same fixed-order total."""
+        self._check(self._lib.mgicp_comm_attach_shm(self._h, name.encode(), int(max_source_points)),
+                    "comm_attach_shm")
+
+    def detach_shm(self):
+        """Back to the previous transport (RCCL or local)."""
+        self._check(self._lib.mgicp_comm_attach_shm(self._h, None, 0), "comm_attach_shm(detach)")
+
+    PASS_STATS = ("server_launches", "server_passes", "launched_passes", "takeovers", "bar_commands",
+                  "row_allocs", "transport", "server_denied")
+
+    def pass_stats(self) -> dict:
+        """Objective-pass path counters (mgicp_debug_pass_stats)."""
+        out = (ctypes.c_longlong * 8)()
+        self._check(self._lib.mgicp_debug_pass_stats(self._h, out), "pass_stats")
+        return {k: int(out[i]) for i, k in enumerate(self.PASS_STATS)}
+
     # -- introspection (parity tests, profiling) ----------------------------------------------
     def debug_covariances(self, which: str, n: int) -> np.ndarray:
         out = np.zeros((n, 6), np.float64)

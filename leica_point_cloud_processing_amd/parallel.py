@@ -51,6 +51,25 @@ def shard_range(n: int, world: int, rank: int) -> tuple[int, int]:
             min(n, super_first(rank + 1, nsup, world) * SUPER_PTS))
 
 
+def fixed_total(rows):
+    """Host mirror of the device's total over supers (wave_total in mgicp_kernels.hip, and the
+    host-row total of shm_rows.hpp): lane l sums supers l, l + 64, ... sequentially from 0.0, then
+    the 64-lane shuffle tree lanes[i] += lanes[i + off] for off = 32 ... 1; lane 0 is the total.
+    rows: sequence of equal-length float64 vectors in global super order."""
+    import numpy as np
+
+    rows = [np.asarray(r, np.float64) for r in rows]
+    lanes = [np.zeros_like(rows[0]) for _ in range(64)]
+    for sg, r in enumerate(rows):
+        lanes[sg % 64] = lanes[sg % 64] + r
+    off = 32
+    while off:
+        for i in range(off):
+            lanes[i] = lanes[i] + lanes[i + off]
+        off >>= 1
+    return lanes[0]
+
+
 def combine_supers(rows, nsup: int, world: int):
     """Host mirror of the multi-GPU finish's indexing: the supers of every rank (rows[r] = rank r's
     supers, padded to a common length) in global order."""

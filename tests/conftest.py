@@ -34,5 +34,33 @@ def part_small():
     return scan, cad, T
 
 
+class heartbeat:
+    """Context manager: a line on the real stderr every `every` seconds while a long step (the
+    full-size CPU oracle) runs, so a supervisor watching the output does not take it for a hang."""
+
+    def __init__(self, what: str, every: float = 30.0):
+        self.what, self.every = what, every
+
+    def __enter__(self):
+        import threading
+        import time
+
+        self._stop = threading.Event()
+        t0 = time.time()
+
+        def beat():
+            while not self._stop.wait(self.every):
+                sys.__stderr__.write(f"[heartbeat] {self.what}: {time.time() - t0:.0f} s\n")
+                sys.__stderr__.flush()
+
+        self._t = threading.Thread(target=beat, daemon=True)
+        self._t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._stop.set()
+        self._t.join(timeout=5)
+
+
 def frob(a, b) -> float:
     return float(np.linalg.norm(np.asarray(a, np.float64) - np.asarray(b, np.float64)))
