@@ -1066,7 +1066,13 @@ int wait_rows(mgicp_ctx* ctx, unsigned int rstamp, const Xf34& A, double out[kRe
         int rc = sync(ctx);  // drains the stream (and cancels a live server): the rows are final now
         if (rc) return rc;
         if (shm::row_complete(reinterpret_cast<const uint64_t*>(row), rstamp)) break;
-        return fail(ctx, MGICP_E_HIP, "objective pass finished without publishing its super rows");
+        char msg[192];
+        std::snprintf(msg, sizeof(msg),
+                      "objective pass finished without publishing its super rows (row %lld of %lld: stamp %08x "
+                      "expected, words 0 / 31 carry %08x / %08x)",
+                      r, rv.nloc, rstamp, static_cast<unsigned int>(row[0] >> 32),
+                      static_cast<unsigned int>(row[31] >> 32));
+        return fail(ctx, MGICP_E_HIP, msg);
       }
       if (!own && el > ctx->remote_deadline_s)
         return fail(ctx, MGICP_E_COMM, "another rank did not publish its super rows (shared row segment)");
@@ -2440,6 +2446,18 @@ int mgicp_debug_pass_bench(mgicp_ctx* ctx, const double x[6], int npasses, int m
   (void)hipEventDestroy(a);
   (void)hipEventDestroy(b);
   HIPCK(e);
+  if (std::getenv("MGICP_SRV_DEBUG") && mode == 0) {
+    PassCmd m{};
+    HIPCK(hipMemcpy(&m, ctx->mail, sizeof(PassCmd), hipMemcpyDeviceToHost));
+    std::fprintf(stderr, "[srv-debug] seq0 %llu npasses %d ms %.3f | mail:", ctx->pass_seq - npasses, npasses, ms);
+    for (int i = 0; i < 16; ++i)
+      std::fprintf(stderr, " %x:%x", static_cast<unsigned>(m.h[i] >> 32), static_cast<unsigned>(m.h[i]));
+    std::fprintf(stderr, "\n");
+    if (ctx->h_ptimes)
+      for (unsigned long long q = ctx->pass_seq - npasses; q < ctx->pass_seq + 1; ++q)
+        std::fprintf(stderr, "[srv-debug] pass %llu: gate exit %llu finish %llu\n", q, ctx->h_ptimes[2 * (q & 1023)],
+                     ctx->h_ptimes[2 * (q & 1023) + 1]);
+  }
   if (rows) {
     // the host-row tickets are left as multiples of the supers' sizes: re-arm them
     HIPCK(hipMemsetAsync(ctx->tickets.p, 0, ctx->tickets_n * sizeof(unsigned int), ctx->stream));

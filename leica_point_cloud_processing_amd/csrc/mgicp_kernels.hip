@@ -1227,7 +1227,14 @@ __device__ __forceinline__ void read_cmd(const PassCmd* c, unsigned long long (&
     if (kHost) asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1" : "=v"(r[i]) : "v"(p + i) : "memory");
     else asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(r[i]) : "v"(p + i) : "memory");
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // the wait names the loads' destination registers as operands: the compiler does not know that an
+  // asm load's output is only valid after s_waitcnt, and a wait with no operands let it move the
+  // stamp compares above it (they then read the address registers -- r03: a server that never saw
+  // its next command)
+  asm volatile("s_waitcnt vmcnt(0)"
+               : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), "+v"(r[6]), "+v"(r[7])
+               :
+               : "memory");
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     v[2 * i] = (static_cast<unsigned long long>(r[i].y) << 32) | r[i].x;
