@@ -68,8 +68,9 @@ def parse():
                     help="points per cloud of the bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=1)
     ap.add_argument("--oracle-full", type=int, default=1,
-                    help="1 = run the oracle on the full workload with all usable host cores "
-                         "(all-core CPU baseline + full-size frob_vs_oracle; rank 0, N = 1 only)")
+                    help="1 = run the oracle on the full workload on the box's granted CPU share "
+                         "(min(OMP_NUM_THREADS, affinity) threads: the thread-share CPU baseline + full-size "
+                         "frob_vs_oracle; rank 0, N = 1 only)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r02", "final", "pmc_summary.json"))
     ap.add_argument("--gn-steps", type=int, default=5,
                     help="timed aligns of the opt-in Gauss-Newton mode (MGICP_SOLVER_GN; 0 = skip)")
@@ -213,11 +214,12 @@ def host_info():
     # the box grants a CPU share (OMP_NUM_THREADS) smaller than the machine (nproc)
     usable = min(share, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else share
     return {"lscpu_model": model, "nproc": os.cpu_count(), "sched_affinity": share,
-            "OMP_NUM_THREADS": omp, "threads_used_all_core": usable}
+            "OMP_NUM_THREADS": omp, "threads_used": usable,
+            "thread_share": f"{usable} of {os.cpu_count()} hardware threads (the box's granted share)"}
 
 
 def oracle_full(scan, cad, threads, max_iter, fixed, guess=None):
-    """The oracle on the FULL workload with every usable host core (OpenMP): the all-core CPU
+    """The oracle on the FULL workload with the box's granted thread share (OpenMP): the CPU
     baseline at the config's own size (no scaling) and the full-size final-transform parity."""
     from oracle import ref
 
@@ -570,9 +572,9 @@ def main():
         host = host_info()
         cpu["host"] = host
         if args.oracle_full:
-            # all usable host cores, the FULL workload: the stronger baseline (no scaling) and the
-            # full-size final-transform parity of BASELINE.json's metric
-            nt = host["threads_used_all_core"]
+            # the granted thread share (OMP_NUM_THREADS of the box's nproc), the FULL workload: the
+            # stronger baseline (no scaling) and the full-size final-transform parity of the metric
+            nt = host["threads_used"]
             T_o, oinfo = oracle_full(scan, cad, nt, args.max_iter, args.fixed)
             trace_err = (max(float(np.linalg.norm(a.astype(np.float64) - b.astype(np.float64)))
                              for a, b in zip(trace_final, oinfo["trace"]))
@@ -590,14 +592,14 @@ def main():
                 "unit": "iterations/s",
                 "cores": nt,
                 "kind": "port",
-                "sample": (f"oracle/gicp_ref.c with OpenMP on {nt} threads over the FULL {args.n_source}<->"
+                "sample": (f"oracle/gicp_ref.c with OpenMP on {nt} threads ({host['thread_share']}) over the FULL {args.n_source}<->"
                            f"{args.n_target} workload (no scaling): {oinfo['iterations']} iterations in "
                            f"{oinfo['t_loop_s']:.2f} s loop, covariances + kd-trees {oinfo['t_cov_s']:.2f} s, "
                            f"ms-to-converge {1e3 * oinfo['t_total_s']:.0f} ms"),
                 "ms_to_converge": 1e3 * oinfo["t_total_s"],
                 "host": host,
                 "single_thread": single,
-                "gpu_over_all_core": value / all_rate,
+                "gpu_over_thread_share": value / all_rate,
                 "gpu_over_single_thread": value / single["value"],
             }
 

@@ -289,6 +289,22 @@ def cube_fixture(ply_path: str, n: int = 5000, yaw: float = 0.175):
     return src, transform_points(T, src), T
 
 
+def cube_ply_vs_obj(ply_path: str, obj_path: str, n: int = 5000, yaw: float = 0.175):
+    """BASELINE.json configs[0] ("test/cube.ply vs test/cube.obj-sampled"): source =
+    CADToPointCloud(cube.ply, n) with glibc rand() from its default seed (as test_gicp_alignment.cpp:
+    32-47), target = CADToPointCloud(cube.obj, n) drawn from the SAME generator afterwards (one
+    process sampling both files, CADToPointCloud.cpp:35-62; vtkOBJReader -> vtkTriangleFilter),
+    rotated by Utils::rotateCloud(0, 0, yaw).  Two independent samplings of the same cube: no point
+    of the source has an exact partner in the target, unlike the ply-only fixture."""
+    rng = GlibcRand(1)
+    v, t = read_ply(ply_path)
+    src = cad_sample_reference(v, t, n, rng)
+    v2, t2 = read_obj(obj_path)
+    tgt0 = cad_sample_reference(v2, t2, n, rng)
+    T = rotate_cloud_matrix(0.0, 0.0, yaw)
+    return src, transform_points(T, tgt0), T
+
+
 # ---------------------------------------------------------------------------------------
 # synthetic aero part (SURVEY.md 8d)
 # ---------------------------------------------------------------------------------------
