@@ -217,6 +217,8 @@ struct Cloud {
   bool want_seed_map = false;
   DevBuf<float4> boxes;       // per-cell point boxes (target only: the 1-NN sweeps prune by them)
   bool want_boxes = false;
+  DevBuf<float4> pairs;       // pair-interleaved points (target only: the wave-uniform 1-NN scan)
+  bool want_pairs = false;
   bool drop_nonfinite = false; // build the grid over the finite points only (KdTreeFLANN semantics)
   double occupancy = 0;        // grid sizing target (points per non-empty cell); 0 = context default
   size_t n_built = 0;          // points of the last grid built in this slot (cell-size hint)
@@ -348,6 +350,13 @@ struct mgicp_ctx {
   int srv_cus = 0;                      // env MGICP_SRV_CUS: cap on the server's blocks (0 = every CU)
   int srv_waves = 4;                    // server shape: 4 or 8 waves per CU (env MGICP_SRV_WAVES)
   int stall_pass = -1;                  // env MGICP_SRV_STALL_PASS (tests): a server block withholds this pass
+  bool corr_wave = true;                // wave-uniform 1-NN sweeps (env MGICP_CORR_WAVE)
+  float corr_rcap = 5.f;                // cells: lanes with a larger seed bound search alone (MGICP_CORR_RCAP)
+  // r03 A/B (profiles/r03/corrsweep): union boxes of <= 96 rows and 16 cells along x, for waves whose
+  // mean seed bound is >= 1.25 cells (the first sweep mostly): 2455 -> 2300 us per C4 align's sweeps
+  int corr_max_rows = 96;               // union boxes with more rows / x cells: per-lane search
+  int corr_max_x = 16;
+  float corr_union_min_r = 1.25f;       // cells: waves whose mean seed bound is smaller search per lane
   double row_deadline_ms = 500.0;       // env MGICP_ROW_DEADLINE_MS: own rows missing this long -> take over
   double remote_deadline_s = 120.0;     // env MGICP_REMOTE_DEADLINE_S: other ranks' rows / gathers
   unsigned long long* h_ptimes = nullptr;  // MGICP_PASS_TIMES=1: per pass gate exit / finish (wall clock)
@@ -757,6 +766,12 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
     HIPCK(cl.boxes.reserve(2 * nc));
     HIPCK(launch_cell_boxes(cl.pts.p, cl.cell_start.p, nc, cl.boxes.p, s));
     g.boxes = cl.boxes.p;
+  }
+  g.pairs = nullptr;
+  if (cl.want_pairs) {
+    HIPCK(cl.pairs.reserve(2 * pair_count(n)));
+    HIPCK(launch_pairs(cl.pts.p, n, cl.pairs.p, s));
+    g.pairs = cl.pairs.p;
   }
   cl.ncells = nc;
   cl.n_built = n;
@@ -1225,6 +1240,21 @@ CorrSoA corr_soa(mgicp_ctx* ctx) {
                  d, d + c, d + 2 * c, d + 3 * c, d + 4 * c, d + 5 * c};
 }
 
+// The 1-NN sweep kernel of one correspondence phase: the wave-uniform scan when the target has its
+// pair copy (default), else the per-lane search (env MGICP_CORR_WAVE=0); both exact, same results.
+hipError_t launch_sweep(mgicp_ctx* ctx, const Mat4& T, double thr, bool seeded, const uint32_t* qp) {
+  const size_t p0 = ctx->shard_p0(), p1 = ctx->shard_p1();
+  const GridView& g = ctx->tgt.view;
+  if (ctx->corr_wave && g.pairs) {
+    const float rc = ctx->corr_rcap * g.h;
+    return launch_correspond_wave(g, ctx->d_out, p0, p1, T.xf(), thr, seeded ? 1 : 0, ctx->prev_pos.p,
+                                  ctx->flags.p, qp, rc * rc, ctx->corr_max_rows, ctx->corr_max_x, ctx->corr_union_min_r,
+                                  ctx->stream);
+  }
+  return launch_correspond(g, ctx->d_out, p0, p1, T.xf(), thr, seeded ? 1 : 0, ctx->prev_pos.p, ctx->flags.p, qp,
+                           ctx->stream);
+}
+
 // One correspondence sweep (the loop body of computeTransformation before the BFGS call):
 // exact 1-NN per source point, then a deterministic compaction of the accepted ones (exclusive
 // scan of the flags, scatter in grid-sorted order) that computes their Mahalanobis matrices
@@ -1239,8 +1269,7 @@ int correspond(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
   const uint32_t* qp = query_perm(ctx);
   {
     ProfScope ps(ctx, kFamCorr);
-    HIPCK(launch_correspond(ctx->tgt.view, ctx->d_out, p0, p1, T.xf(), thr, seeded ? 1 : 0,
-                            ctx->prev_pos.p, ctx->flags.p, qp, s));
+    HIPCK(launch_sweep(ctx, T, thr, seeded, qp));
   }
   ctx->seed_valid = true;
 #if MGICP_CORR_STATS
@@ -1248,9 +1277,16 @@ int correspond(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
     unsigned long long st[8];
     HIPCK(hipStreamSynchronize(s));
     HIPCK(corr_stats_take(st));
-    std::fprintf(stderr, "[corr-stats] queries %llu accepted %llu rejected %llu | tests/query acc %.1f rej %.1f | ranges/query acc %.1f rej %.1f\n",
-                 st[0], st[1], st[2], st[1] ? double(st[3]) / st[1] : 0.0, st[2] ? double(st[4]) / st[2] : 0.0,
-                 st[1] ? double(st[5]) / st[1] : 0.0, st[2] ? double(st[6]) / st[2] : 0.0);
+    if (ctx->corr_wave && ctx->tgt.view.pairs)
+      std::fprintf(stderr, "[corr-stats] wave scan: queries %llu accepted %llu rejected %llu | per-lane tests/query %.1f "
+                   "ranges/query %.1f | lanes left to the per-lane search %llu | union-scan waves %llu of %llu, "
+                   "candidates per union wave %.1f\n",
+                   st[0], st[1], st[2], st[0] ? double(st[3]) / st[0] : 0.0, st[0] ? double(st[4]) / st[0] : 0.0, st[5],
+                   st[7], (st[0] + 63) / 64, st[7] ? double(st[6]) / st[7] : 0.0);
+    else
+      std::fprintf(stderr, "[corr-stats] queries %llu accepted %llu rejected %llu | tests/query acc %.1f rej %.1f | ranges/query acc %.1f rej %.1f\n",
+                   st[0], st[1], st[2], st[1] ? double(st[3]) / st[1] : 0.0, st[2] ? double(st[4]) / st[2] : 0.0,
+                   st[1] ? double(st[5]) / st[1] : 0.0, st[2] ? double(st[6]) / st[2] : 0.0);
   }
 #endif
   const size_t sb = scan_scratch_bytes(ns + 1);
@@ -1535,13 +1571,11 @@ int moments_pass(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool supers_only 
 // then the moment pass; no scan / compaction (the moment pass reads the flags directly)
 int correspond_gn(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
   const double thr = ctx->prm.max_corr_dist * ctx->prm.max_corr_dist;
-  const size_t p0 = ctx->shard_p0(), p1 = ctx->shard_p1();
   const bool seeded = seed && ctx->seed_valid;
   const uint32_t* qp = query_perm(ctx);
   {
     ProfScope ps(ctx, kFamCorr);
-    HIPCK(launch_correspond(ctx->tgt.view, ctx->d_out, p0, p1, T.xf(), thr, seeded ? 1 : 0,
-                            ctx->prev_pos.p, ctx->flags.p, qp, ctx->stream));
+    HIPCK(launch_sweep(ctx, T, thr, seeded, qp));
   }
   ctx->seed_valid = true;
   ctx->have_corr = false;  // the SoA streams of the BFGS mode are not refreshed
@@ -1687,6 +1721,13 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
   // per-cell box loads and tests cost more than they save (C4 correspondence 1.39 vs 1.11 ms,
   // profiles/r02/ab_boxes): off by default, knob MGICP_CELL_BOXES=1
   ctx->tgt.want_boxes = false;
+  // the wave-uniform 1-NN scan (r03) and the target's pair copy it reads
+  if (const char* cw = std::getenv("MGICP_CORR_WAVE")) ctx->corr_wave = std::atoi(cw) != 0;
+  if (const char* rc = std::getenv("MGICP_CORR_RCAP")) ctx->corr_rcap = static_cast<float>(std::atof(rc));
+  if (const char* mr = std::getenv("MGICP_CORR_MAX_ROWS")) ctx->corr_max_rows = std::max(1, std::atoi(mr));
+  if (const char* mx = std::getenv("MGICP_CORR_MAX_X")) ctx->corr_max_x = std::max(1, std::atoi(mx));
+  if (const char* um = std::getenv("MGICP_CORR_UNION_MIN_R")) ctx->corr_union_min_r = static_cast<float>(std::atof(um));
+  ctx->tgt.want_pairs = ctx->corr_wave;
   if (const char* cb = std::getenv("MGICP_CELL_BOXES")) ctx->tgt.want_boxes = std::atoi(cb) != 0;
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
@@ -1733,7 +1774,7 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   ctx->f_count.release();
   for (Cloud* c : {&ctx->src, &ctx->tgt, &ctx->aux, &ctx->qry}) {
     c->raw.release(); c->orig.release(); c->pts.release(); c->perm.release();
-    c->cell_start.release(); c->cov.release(); c->empty_dist.release(); c->boxes.release();
+    c->cell_start.release(); c->cov.release(); c->empty_dist.release(); c->boxes.release(); c->pairs.release();
     c->seed.release(); c->seed_scratch.release();
   }
   ctx->src_out.release();

@@ -33,6 +33,9 @@ struct GridView {
   // optional per-cell point boxes (2 float4 per cell: min xyz | bits(start), max xyz | bits(end));
   // 1-NN searches skip cells whose point box lies beyond their bound
   const float4* boxes;
+  // optional pair-interleaved copy of pts for the wave-uniform 1-NN scan (2 float4 per pair of
+  // points: x0 x1 y0 y1 | z0 z1 w0 w1; pair_count(n) pairs, far sentinels past n)
+  const float4* pairs;
 };
 
 #ifndef MGICP_EMPTY_CAP
@@ -128,6 +131,14 @@ bool knn_logged_enabled();  // env MGICP_KNN2 (default on)
 hipError_t launch_correspond(const GridView& tgt, const float4* src, size_t p0, size_t p1, Xf34 T,
                              double thr, int seeded, uint32_t* nn_pos, uint32_t* flags,
                              const uint32_t* qperm /*nullable: query order*/, hipStream_t s);
+// the wave-uniform form (needs tgt.pairs): lanes whose seed bound exceeds sqrt(rcap2), or waves whose
+// union box exceeds max_rows rows or max_xcells cells along x, or whose mean seed bound is below
+// union_min_r cells, finish with the per-lane search
+hipError_t launch_correspond_wave(const GridView& tgt, const float4* src, size_t p0, size_t p1, Xf34 T,
+                                  double thr, int seeded, uint32_t* nn_pos, uint32_t* flags, const uint32_t* qperm,
+                                  float rcap2, int max_rows, int max_xcells, float union_min_r, hipStream_t s);
+size_t     pair_count(size_t n);
+hipError_t launch_pairs(const float4* pts, size_t n, float4* out, hipStream_t s);
 // Morton keys (30 bit, bbox lo, 1024 / extent = inv) of points [p0, p0 + n) and values 0..n-1
 hipError_t launch_morton_keys(const float4* pts, size_t p0, size_t n, const float lo[3], float inv,
                               uint32_t* keys, uint32_t* vals, hipStream_t s);

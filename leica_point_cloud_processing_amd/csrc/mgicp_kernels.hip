@@ -909,6 +909,274 @@ __device__ __forceinline__ void load_cov(const Cov3& c, size_t i, double M[3][3]
 // small register footprint (occupancy) and leaves the fp64 Mahalanobis work to the compaction.
 // `qperm` (optional): the shard's query order -- thread t handles shard point qperm[t], a
 // Morton order of the source, so that a wave's queries form a compact 3-D patch.
+// The starting candidates of a 1-NN query (real points, so any of them keeps the search exact):
+// last sweep's match, and the seed map's points of the query's cell (and, in the first sweep, of
+// its 6 face neighbours)
+__device__ __forceinline__ void seed_query(const GridView& tg, int seeded, uint32_t prev, float qx, float qy, float qz,
+                                           NnVisitor& vis) {
+  if (seeded) {
+    // seed with last iteration's match: a real candidate, so the exact search only tightens it,
+    // and the ball-cell pruning starts from a near-final radius
+    if (prev != 0xffffffffu) vis.range(tg, prev, prev + 1);
+  }
+  if ((!seeded || MGICP_SEED_BOTH) && tg.seed) {
+#if MGICP_SEED_NEIGHBOURS
+    if (!seeded || MGICP_SEED_NEIGHBOURS > 1) {
+      const int cx = qcell(qx, tg.ox, tg.inv_h), cy = qcell(qy, tg.oy, tg.inv_h), cz = qcell(qz, tg.oz, tg.inv_h);
+      const int dd[7][3] = {{0, 0, 0}, {-1, 0, 0}, {1, 0, 0}, {0, -1, 0}, {0, 1, 0}, {0, 0, -1}, {0, 0, 1}};
+#pragma unroll
+      for (int k = 0; k < 7; ++k) {
+        const int x = cx + dd[k][0], y = cy + dd[k][1], z = cz + dd[k][2];
+        if (x >= 0 && x < tg.nx && y >= 0 && y < tg.ny && z >= 0 && z < tg.nz) {
+          const uint32_t pp = tg.seed[static_cast<size_t>(x) +
+                                      static_cast<size_t>(tg.nx) * (static_cast<size_t>(y) + static_cast<size_t>(tg.ny) * z)];
+          if (pp != 0xffffffffu) vis.range(tg, pp, pp + 1);
+        }
+      }
+      return;
+    }
+#endif
+    const int cx = qcell(qx, tg.ox, tg.inv_h), cy = qcell(qy, tg.oy, tg.inv_h), cz = qcell(qz, tg.oz, tg.inv_h);
+    if (cx >= 0 && cx < tg.nx && cy >= 0 && cy < tg.ny && cz >= 0 && cz < tg.nz) {
+      const uint32_t pp = tg.seed[static_cast<size_t>(cx) +
+                                  static_cast<size_t>(tg.nx) * (static_cast<size_t>(cy) + static_cast<size_t>(tg.ny) * cz)];
+      if (pp != 0xffffffffu) vis.range(tg, pp, pp + 1);
+    }
+  }
+}
+
+// ---- wave-uniform 1-NN sweep (r03) ----------------------------------------------------------
+// The per-lane search (correspond_kernel) issues one 16-byte gather per candidate and lane; its 64
+// lanes touch ~18 cache lines per load, and the texture addresser was busy 87-88 % of every sweep
+// (TA_TA_BUSY, profiles/r03/corrdiag): the sweeps were bound by vector-memory ADDRESS throughput,
+// not by bytes or arithmetic.  Here the 64 Morton-ordered queries of a wave scan the rows of their
+// UNION box together: every row and candidate is wave-uniform, so cell bounds and points arrive
+// through the scalar cache (s_load, one 64-byte load per 4 candidates for the whole wave) and
+// every lane tests every candidate with packed fp32 arithmetic on a pair-interleaved copy of the
+// target (GridView::pairs: x0 x1 y0 y1 z0 z1 w0 w1 per pair) -- bit-identical distances (the FLANN
+// order, no contraction).  A 4-candidate block costs 8 packed + 3 VALU per lane; the exact
+// (d2, index) key compare runs only when some lane's block minimum reaches its bound.
+// Exactness: every lane starts from real seed candidates (bound R); the union box covers every
+// included lane's ball; a row is skipped only when no lane's CURRENT bound reaches it; testing
+// points outside a lane's ball never changes its exact minimum.  Lanes whose bound exceeds rcap
+// (no seed nearby, rejected queries), or waves whose union box is too large, finish with the
+// per-lane search from their best.
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int wave_min_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+  return __builtin_amdgcn_readfirstlane(v);
+}
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+  return __builtin_amdgcn_readfirstlane(v);
+}
+
+// squared distances (FLANN L2_Simple per element: ((dx^2) + dy^2) + dz^2, dx = query - point) of this
+// lane's query to the 4 candidates of two staged pairs (a0 a1 | b0 b1)
+__device__ __forceinline__ void pair_d2(float qx, float qy, float qz, const f4v& a0, const f4v& a1, const f4v& b0,
+                                        const f4v& b1, f2v& ra, f2v& rb) {
+  const f2v qx2 = {qx, qx}, qy2 = {qy, qy}, qz2 = {qz, qz};
+  f2v dx = qx2 - f2v{a0.x, a0.y}, dy = qy2 - f2v{a0.z, a0.w}, dz = qz2 - f2v{a1.x, a1.y};
+  ra = dx * dx;
+  ra = ra + dy * dy;
+  ra = ra + dz * dz;
+  dx = qx2 - f2v{b0.x, b0.y};
+  dy = qy2 - f2v{b0.z, b0.w};
+  dz = qz2 - f2v{b1.x, b1.y};
+  rb = dx * dx;
+  rb = rb + dy * dy;
+  rb = rb + dz * dz;
+}
+
+constexpr int kStagePairs = 64;     // pairs staged per wave and chunk (128 candidates, 2 KiB of LDS)
+constexpr int kCorrRowSlots = 256;  // union-box rows whose cell bounds a wave keeps in registers (4 per lane)
+
+__global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_wave_kernel(
+    GridView tg, const float4* __restrict__ src, size_t p0, size_t p1, Xf34 T, double thr, int seeded,
+    uint32_t* __restrict__ nn_pos, uint32_t* __restrict__ flags, const uint32_t* __restrict__ qperm, float rcap2,
+    int max_rows, int max_xcells, float union_min_r) {
+  __shared__ f4v stage[4][2 * kStagePairs];
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const size_t t = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const bool live = t < p1 - p0;  // no early exit: every lane of the wave takes part in the union scan
+  const size_t p = p0 + (live ? (qperm ? qperm[t] : t) : 0);
+  float qx = 0.f, qy = 0.f, qz = 0.f;
+  NnVisitor vis;
+  if (live) {
+    const float4 s = src[p];
+    xform(T, s.x, s.y, s.z, qx, qy, qz);
+  }
+  vis.init(qx, qy, qz, thr);
+  if (live) seed_query(tg, seeded, seeded ? nn_pos[p - p0] : 0xffffffffu, qx, qy, qz, vis);
+  // ---- the union box of the included lanes' seed balls
+  const float bd0 = vis.prune2();
+  bool incl = live && bd0 <= rcap2;
+  int zl = INT_MAX, zh = INT_MIN, yl = INT_MAX, yh = INT_MIN, xl = INT_MAX, xh = INT_MIN;
+  float rsum = 0.f;
+  if (incl) {
+    const float R = sqrtf(bd0 * 1.00001f) + tg.slop;
+    rsum = R;
+    zl = max(qcell(qz - R, tg.oz, tg.inv_h), 0);
+    zh = min(qcell(qz + R, tg.oz, tg.inv_h), tg.nz - 1);
+    yl = max(qcell(qy - R, tg.oy, tg.inv_h), 0);
+    yh = min(qcell(qy + R, tg.oy, tg.inv_h), tg.ny - 1);
+    xl = max(qcell(qx - R, tg.ox, tg.inv_h), 0);
+    xh = min(qcell(qx + R, tg.ox, tg.inv_h), tg.nx - 1);
+  }
+  const int Z0 = wave_min_i(zl), Z1 = wave_max_i(zh), Y0 = wave_min_i(yl), Y1 = wave_max_i(yh);
+  const int X0 = wave_min_i(xl), X1 = wave_max_i(xh);
+  // small balls (later sweeps: queries near their match) are cheaper per lane: mean bound in cells
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) rsum += __shfl_xor(rsum, o, 64);
+  const float nincl = static_cast<float>(__builtin_popcountll(__builtin_amdgcn_ballot_w64(incl)));
+  const bool box_ok = Z0 <= Z1 && Y0 <= Y1 && X0 <= X1 &&
+                      static_cast<long long>(Z1 - Z0 + 1) * (Y1 - Y0 + 1) <= min(max_rows, kCorrRowSlots) &&
+                      X1 - X0 + 1 <= max_xcells &&
+                      __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(rsum))) >= union_min_r * tg.h * nincl;
+  if (!box_ok) incl = false;
+  bool tie = false;
+  if (box_ok) {
+    const f4v* pairs = reinterpret_cast<const f4v*>(tg.pairs);
+    f4v* st = stage[wid];
+#if MGICP_CORR_STATS
+    unsigned long long ncand = 0;
+#endif
+    // the box's row table: cell bounds [cell_start(row, X0), cell_start(row, X1 + 1)) of slot
+    // s = (z - Z0) * nyb + (y - Y0) in lane s & 63 of ra[s >> 6] / rb[s >> 6] -- one gather for every
+    // row instead of a dependent load per row
+    const int nyb = Y1 - Y0 + 1, nrows = (Z1 - Z0 + 1) * nyb;
+    uint32_t ra[kCorrRowSlots / 64], rb[kCorrRowSlots / 64];
+#pragma unroll
+    for (int k = 0; k < kCorrRowSlots / 64; ++k) {
+      const int sl = lane + 64 * k;
+      ra[k] = rb[k] = 0;
+      if (sl < nrows) {
+        const uint32_t row = (static_cast<uint32_t>(Z0 + sl / nyb) * tg.ny + static_cast<uint32_t>(Y0 + sl % nyb)) * tg.nx;
+        ra[k] = tg.cell_start[row + X0];
+        rb[k] = tg.cell_start[row + X1 + 1];
+      }
+    }
+    // the union scan keeps, per lane, the smallest d2 seen (bcur) and the pair index of the block
+    // holding it (bpi); a later block reaching exactly bcur is a tie between two distinct points
+    // (every position is tested once: out-of-row positions of a row's edge blocks are masked), left
+    // to the per-lane search.  The winner inside the block is resolved exactly after the scan.
+    float bcur = INFINITY;
+    uint32_t bpi = 0;
+    // rows nearest the box centre first (the bounds shrink sooner; the order changes no result)
+    const int zc = (Z0 + Z1) >> 1, yc = (Y0 + Y1) >> 1;
+    const int zspan = 2 * max(zc - Z0, Z1 - zc), yspan = 2 * max(yc - Y0, Y1 - yc);
+    for (int mz = 0; mz <= zspan; ++mz) {
+      const int z = zc + ((mz & 1) ? 1 : -1) * ((mz + 1) >> 1);
+      if (z < Z0 || z > Z1) continue;
+      const float gz = cell_gap(qz, tg.oz, tg.h, z, tg.slop);
+      const float gz2 = gz * gz;
+      if (!__builtin_amdgcn_ballot_w64(incl && gz2 <= fminf(bd0, bcur) * 1.00001f)) continue;
+      for (int my = 0; my <= yspan; ++my) {
+        const int y = yc + ((my & 1) ? 1 : -1) * ((my + 1) >> 1);
+        if (y < Y0 || y > Y1) continue;
+        const float gy = cell_gap(qy, tg.oy, tg.h, y, tg.slop);
+        if (!__builtin_amdgcn_ballot_w64(incl && gy * gy + gz2 <= fminf(bd0, bcur) * 1.00001f)) continue;
+        const int sl = (z - Z0) * nyb + (y - Y0);
+        uint32_t a = 0, b = 0;
+#pragma unroll
+        for (int k = 0; k < kCorrRowSlots / 64; ++k)
+          if ((sl >> 6) == k) {
+            a = __builtin_amdgcn_readlane(ra[k], sl & 63);
+            b = __builtin_amdgcn_readlane(rb[k], sl & 63);
+          }
+#if MGICP_CORR_STATS
+        ncand += b - a;
+#endif
+        // stage the row's pairs [a / 2, ceil(b / 2)) in chunks (coalesced: lane l loads float4 l)
+        const uint32_t pe = (b + 1) >> 1;
+        for (uint32_t c0 = a >> 1; c0 < pe; c0 += kStagePairs) {
+          const uint32_t np = min(static_cast<uint32_t>(kStagePairs), pe - c0);
+          // always a whole chunk (pair_count pads kStagePairs + 2 far pairs past the cloud): both
+          // loads in flight at once; pairs past the row are staged but not scanned
+          const f4v v0 = pairs[2 * c0 + lane], v1 = pairs[2 * c0 + 64 + lane];
+          st[lane] = v0;
+          st[lane + 64] = v1;
+          for (uint32_t k = 0; k < np; k += 2) {
+            const uint32_t pi = c0 + k, j = 2 * pi;
+            f2v r0, r1;
+            pair_d2(qx, qy, qz, st[2 * k], st[2 * k + 1], st[2 * k + 2], st[2 * k + 3], r0, r1);
+            if (j < a || j + 3 >= b) {  // a row's edge block: positions outside [a, b) are another row's
+              if (j < a) r0.x = INFINITY;
+              if (j + 1 < a || j + 1 >= b) r0.y = INFINITY;
+              if (j + 2 >= b) r1.x = INFINITY;
+              if (j + 3 >= b) r1.y = INFINITY;
+            }
+            const float m = fminf(fminf(r0.x, r0.y), fminf(r1.x, r1.y));
+            const bool lt = m < bcur;
+            tie = lt ? false : (tie || m == bcur);
+            bcur = lt ? m : bcur;
+            bpi = lt ? pi : bpi;
+          }
+        }
+      }
+    }
+    // the winner of the lane's best block: exact (d2, index) keys of its 4 candidates, masked like
+    // the scan (a position outside the block's row cannot hold bcur: it was masked there, and it is
+    // a real point tested in its own row -- taking it is still exact, the keys decide)
+    if (bcur < INFINITY) {
+      const f4v a0 = pairs[2 * bpi], a1 = pairs[2 * bpi + 1], b0 = pairs[2 * bpi + 2], b1 = pairs[2 * bpi + 3];
+      f2v r0, r1;
+      pair_d2(qx, qy, qz, a0, a1, b0, b1, r0, r1);
+      const uint32_t j = 2 * bpi;
+      const unsigned long long k0 = (static_cast<unsigned long long>(__float_as_uint(r0.x)) << 32) | __float_as_uint(a1.z);
+      const unsigned long long k1 = (static_cast<unsigned long long>(__float_as_uint(r0.y)) << 32) | __float_as_uint(a1.w);
+      const unsigned long long k2 = (static_cast<unsigned long long>(__float_as_uint(r1.x)) << 32) | __float_as_uint(b1.z);
+      const unsigned long long k3 = (static_cast<unsigned long long>(__float_as_uint(r1.y)) << 32) | __float_as_uint(b1.w);
+      if (k0 < vis.best) { vis.best = k0; vis.pos = j; }
+      if (k1 < vis.best) { vis.best = k1; vis.pos = j + 1; }
+      if (k2 < vis.best) { vis.best = k2; vis.pos = j + 2; }
+      if (k3 < vis.best) { vis.best = k3; vis.pos = j + 3; }
+    }
+#if MGICP_CORR_STATS
+    if (lane == 0) {
+      atomicAdd(&g_corr_stats[6], ncand);
+      atomicAdd(&g_corr_stats[7], 1ull);
+    }
+#endif
+  }
+  // ---- lanes the union scan did not settle (not included, or a tie between two distinct points
+  // at the scan minimum): the per-lane exact search from their best
+  if (live && (!incl || tie)) {
+    if (vis.best != ~0ull) box_search(tg, qx, qy, qz, vis);
+    else ring_search(tg, qx, qy, qz, vis);
+  }
+  if (!live) return;
+  const bool ok = vis.best != ~0ull &&
+                  static_cast<double>(__uint_as_float(static_cast<uint32_t>(vis.best >> 32))) < thr;
+  nn_pos[p - p0] = ok ? vis.pos : 0xffffffffu;
+  flags[p - p0] = ok ? 1u : 0u;
+#if MGICP_CORR_STATS
+  // [0] queries [1] accepted [2] rejected [3] per-lane tests (seeds + fallback) [4] per-lane ranges
+  // [5] lanes left to the per-lane search [6] union candidates (per wave) [7] union-scan waves
+  atomicAdd(&g_corr_stats[0], 1ull);
+  atomicAdd(&g_corr_stats[ok ? 1 : 2], 1ull);
+  atomicAdd(&g_corr_stats[3], static_cast<unsigned long long>(vis.ntest));
+  atomicAdd(&g_corr_stats[4], static_cast<unsigned long long>(vis.nrange));
+  if (!incl || tie) atomicAdd(&g_corr_stats[5], 1ull);
+#endif
+}
+
+// pair-interleaved copy of the sorted points (GridView::pairs): pair i = {x_2i, x_2i+1, y.., y..,
+// z.., z.., bits(w_2i), bits(w_2i+1)}; positions past n are far sentinels (d2 = +inf, w = ~0)
+__global__ void pairs_kernel(const float4* __restrict__ pts, size_t n, size_t npairs, float4* __restrict__ out) {
+  const size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= npairs) return;
+  const float far = 3.0e38f;
+  const float4 s = make_float4(far, far, far, __uint_as_float(0xffffffffu));
+  const float4 a = 2 * i < n ? pts[2 * i] : s, b = 2 * i + 1 < n ? pts[2 * i + 1] : s;
+  out[2 * i] = make_float4(a.x, b.x, a.y, b.y);
+  out[2 * i + 1] = make_float4(a.z, b.z, a.w, b.w);
+}
+
 __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_kernel(GridView tg, const float4* __restrict__ src,
                                                          size_t p0, size_t p1, Xf34 T, double thr,
                                                          int seeded, uint32_t* __restrict__ nn_pos,
@@ -2247,6 +2515,24 @@ hipError_t launch_correspond(const GridView& tgt, const float4* src, size_t p0, 
                              const uint32_t* qperm, hipStream_t s) {
   if (p1 <= p0) return hipSuccess;
   correspond_kernel<<<nblk(p1 - p0), 256, 0, s>>>(tgt, src, p0, p1, T, thr, seeded, nn_pos, flags, qperm);
+  return hipGetLastError();
+}
+
+hipError_t launch_correspond_wave(const GridView& tgt, const float4* src, size_t p0, size_t p1, Xf34 T,
+                                  double thr, int seeded, uint32_t* nn_pos, uint32_t* flags, const uint32_t* qperm,
+                                  float rcap2, int max_rows, int max_xcells, float union_min_r, hipStream_t s) {
+  if (p1 <= p0) return hipSuccess;
+  if (!tgt.pairs) return hipErrorInvalidValue;
+  correspond_wave_kernel<<<nblk(p1 - p0), 256, 0, s>>>(tgt, src, p0, p1, T, thr, seeded, nn_pos, flags, qperm, rcap2,
+                                                       max_rows, max_xcells, union_min_r);
+  return hipGetLastError();
+}
+
+size_t pair_count(size_t n) { return (n + 1) / 2 + kStagePairs + 2; }
+
+hipError_t launch_pairs(const float4* pts, size_t n, float4* out, hipStream_t s) {
+  const size_t np = pair_count(n);
+  pairs_kernel<<<nblk(np), 256, 0, s>>>(pts, n, np, out);
   return hipGetLastError();
 }
 
