@@ -216,6 +216,10 @@ int mgicp_debug_supers(mgicp_ctx* ctx, int kind, const double* arg, double* out,
  * nranks rows of maxsup supers (row r = rank r's supers; padding rows are never read) */
 int mgicp_debug_finish_supers(mgicp_ctx* ctx, int nv, const double* rows, long long nsup, long long maxsup,
                               int nranks, double* out);
+/* the chunk reduction of every pass (one wave, 16 values per lane): for each of nwaves waves of
+ * in[w][lane][16], out_tree[w][16] = 16 wave_sum shuffle trees (lane 0's sums) and out_rs[w][16] =
+ * the register reduce-scatter the passes use (permlane swaps + DPP); the two must agree bit for bit */
+int mgicp_debug_wave_reduce(mgicp_ctx* ctx, const double* in, int nwaves, double* out_tree, double* out_rs);
 /* per-iteration transformation_ of the last align (col-major, iterations x 16) */
 int mgicp_debug_trace(mgicp_ctx* ctx, float* out, int max_iters);
 /* average device time (ms) of each kernel family while profiling is on, for roofline

@@ -102,6 +102,7 @@ _SIGNATURES = {
     "mgicp_debug_supers": (ctypes.c_int, [_P, ctypes.c_int, _DP, _DP, ctypes.c_int]),
     "mgicp_debug_finish_supers": (ctypes.c_int, [_P, ctypes.c_int, _DP, ctypes.c_longlong, ctypes.c_longlong,
                                                  ctypes.c_int, _DP]),
+    "mgicp_debug_wave_reduce": (ctypes.c_int, [_P, _DP, ctypes.c_int, _DP, _DP]),
     "mgicp_debug_trace": (ctypes.c_int, [_P, _FP, ctypes.c_int]),
     "mgicp_debug_kernel_times": (ctypes.c_int, [_P, _DP, _IP]),
     "mgicp_set_profiling": (ctypes.c_int, [_P, ctypes.c_int]),

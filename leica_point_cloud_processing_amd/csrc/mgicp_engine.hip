@@ -287,6 +287,8 @@ struct mgicp_ctx {
   // compacted accepted correspondences of the current outer iteration (shard-relative)
   DevBuf<uint32_t> prev_pos;  // matched target sorted position per shard point (also the next 1-NN seed)
   DevBuf<uint32_t> flags, cpos;
+  DevBuf<unsigned char> nn_work;      // NnWork list of the wave sweep's stragglers (r03)
+  DevBuf<unsigned int> nn_work_n;
   DevBuf<float> corr_f;    // 6 streams
   DevBuf<double> corr_d;   // 6 streams
   DevBuf<unsigned char> cscratch;
@@ -351,6 +353,8 @@ struct mgicp_ctx {
   int srv_waves = 4;                    // server shape: 4 or 8 waves per CU (env MGICP_SRV_WAVES)
   int stall_pass = -1;                  // env MGICP_SRV_STALL_PASS (tests): a server block withholds this pass
   bool corr_wave = true;                // wave-uniform 1-NN sweeps (env MGICP_CORR_WAVE)
+  int corr_split = 0;                   // waves of the wave sweep with <= this many stragglers hand them to a kernel of
+                                        // their own (MGICP_CORR_SPLIT; 0 = every straggler finishes in place)
   float corr_rcap = 5.f;                // cells: lanes with a larger seed bound search alone (MGICP_CORR_RCAP)
   // r03 A/B (profiles/r03/corrsweep): union boxes of <= 96 rows and 16 cells along x, for waves whose
   // mean seed bound is >= 1.25 cells (the first sweep mostly): 2455 -> 2300 us per C4 align's sweeps
@@ -1247,9 +1251,16 @@ hipError_t launch_sweep(mgicp_ctx* ctx, const Mat4& T, double thr, bool seeded, 
   const GridView& g = ctx->tgt.view;
   if (ctx->corr_wave && g.pairs) {
     const float rc = ctx->corr_rcap * g.h;
+    void* work = nullptr;
+    if (ctx->corr_split > 0) {
+      hipError_t e = ctx->nn_work.reserve(nn_work_bytes(p1 - p0));
+      if (e == hipSuccess) e = ctx->nn_work_n.reserve(1);
+      if (e != hipSuccess) return e;
+      work = ctx->nn_work.p;
+    }
     return launch_correspond_wave(g, ctx->d_out, p0, p1, T.xf(), thr, seeded ? 1 : 0, ctx->prev_pos.p,
                                   ctx->flags.p, qp, rc * rc, ctx->corr_max_rows, ctx->corr_max_x, ctx->corr_union_min_r,
-                                  ctx->stream);
+                                  work, ctx->nn_work_n.p, ctx->corr_split, ctx->stream);
   }
   return launch_correspond(g, ctx->d_out, p0, p1, T.xf(), thr, seeded ? 1 : 0, ctx->prev_pos.p, ctx->flags.p, qp,
                            ctx->stream);
@@ -1272,6 +1283,18 @@ int correspond(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
     HIPCK(launch_sweep(ctx, T, thr, seeded, qp));
   }
   ctx->seed_valid = true;
+#if defined(MGICP_CORR_PHASES) && MGICP_CORR_PHASES
+  {
+    unsigned long long ph[16];
+    HIPCK(hipStreamSynchronize(s));
+    HIPCK(corr_phase_take(ph));
+    const double w = ph[7] ? static_cast<double>(ph[7]) : 1.0;
+    std::fprintf(stderr, "[corr-phase] waves %llu (per-lane finish %llu) | cycles/wave seeds %.0f box %.0f scan %.0f "
+                 "winner %.0f finish %.0f | waves by stragglers 0:%llu 1-4:%llu 5-16:%llu 17-63:%llu 64:%llu, "
+                 "stragglers %llu\n", ph[7], ph[6], ph[0] / w, ph[1] / w, ph[2] / w, ph[3] / w, ph[4] / w, ph[8], ph[9],
+                 ph[10], ph[11], ph[12], ph[13]);
+  }
+#endif
 #if MGICP_CORR_STATS
   {
     unsigned long long st[8];
@@ -1723,6 +1746,7 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
   ctx->tgt.want_boxes = false;
   // the wave-uniform 1-NN scan (r03) and the target's pair copy it reads
   if (const char* cw = std::getenv("MGICP_CORR_WAVE")) ctx->corr_wave = std::atoi(cw) != 0;
+  if (const char* cs = std::getenv("MGICP_CORR_SPLIT")) ctx->corr_split = std::atoi(cs);
   if (const char* rc = std::getenv("MGICP_CORR_RCAP")) ctx->corr_rcap = static_cast<float>(std::atof(rc));
   if (const char* mr = std::getenv("MGICP_CORR_MAX_ROWS")) ctx->corr_max_rows = std::max(1, std::atoi(mr));
   if (const char* mx = std::getenv("MGICP_CORR_MAX_X")) ctx->corr_max_x = std::max(1, std::atoi(mx));
@@ -1787,6 +1811,7 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   ctx->tickets_n = 0;
   ctx->chunk_base.release(); ctx->spart.release(); ctx->gath.release(); ctx->msuper.release();
   ctx->prev_pos.release(); ctx->flags.release(); ctx->cpos.release();
+  ctx->nn_work.release(); ctx->nn_work_n.release();
   ctx->corr_f.release(); ctx->corr_d.release(); ctx->cscratch.release();
   ctx->xyz_dev.release();
   if (ctx->mail) (void)hipFree(ctx->mail);
@@ -2578,6 +2603,25 @@ int mgicp_debug_finish_supers(mgicp_ctx* ctx, int nv, const double* rows, long l
   int rc = sync(ctx);
   d.release();
   o.release();
+  return rc;
+}
+
+int mgicp_debug_wave_reduce(mgicp_ctx* ctx, const double* in, int nwaves, double* out_tree, double* out_rs) {
+  if (!ctx || !in || !out_tree || !out_rs || nwaves <= 0) return MGICP_E_INVALID;
+  HIPCK(hipSetDevice(ctx->device));
+  const size_t nin = static_cast<size_t>(nwaves) * 64 * 16, nout = static_cast<size_t>(nwaves) * 16;
+  DevBuf<double> d, t, r;
+  HIPCK(d.reserve(nin));
+  HIPCK(t.reserve(nout));
+  HIPCK(r.reserve(nout));
+  HIPCK(hipMemcpyAsync(d.p, in, nin * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  HIPCK(launch_wave_reduce_check(d.p, nwaves, t.p, r.p, ctx->stream));
+  HIPCK(hipMemcpyAsync(out_tree, t.p, nout * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCK(hipMemcpyAsync(out_rs, r.p, nout * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+  int rc = sync(ctx);
+  d.release();
+  t.release();
+  r.release();
   return rc;
 }
 

@@ -136,7 +136,11 @@ hipError_t launch_correspond(const GridView& tgt, const float4* src, size_t p0, 
 // union_min_r cells, finish with the per-lane search
 hipError_t launch_correspond_wave(const GridView& tgt, const float4* src, size_t p0, size_t p1, Xf34 T,
                                   double thr, int seeded, uint32_t* nn_pos, uint32_t* flags, const uint32_t* qperm,
-                                  float rcap2, int max_rows, int max_xcells, float union_min_r, hipStream_t s);
+                                  float rcap2, int max_rows, int max_xcells, float union_min_r,
+                                  void* work /*nullable: NnWork list of stragglers, nn_work_bytes(p1 - p0)*/,
+                                  unsigned int* work_n, int split_max /*waves with at most this many stragglers hand them on*/,
+                                  hipStream_t s);
+size_t nn_work_bytes(size_t n);
 size_t     pair_count(size_t n);
 hipError_t launch_pairs(const float4* pts, size_t n, float4* out, hipStream_t s);
 // Morton keys (30 bit, bbox lo, 1024 / extent = inv) of points [p0, p0 + n) and values 0..n-1
@@ -190,6 +194,8 @@ hipError_t launch_fdf_server(const CorrSoA& c, const uint32_t* pos, const uint32
 // super partials of nch chunk partials of nv (kRedVals or kMomVals) values
 hipError_t launch_super_reduce(const double* chunk, int nch, int nv, double* sup, hipStream_t s);
 // totals of nsup supers held as nranks rows of maxsup (row r: rank r's supers, from super_first(r))
+// tests: wave_sum x 16 vs wave_sum16 on in[w][lane][16] (mgicp_debug_wave_reduce)
+hipError_t launch_wave_reduce_check(const double* in, int nwaves, double* out_tree, double* out_rs, hipStream_t s);
 hipError_t launch_finish_supers(const double* sup, long long nsup, long long maxsup, int nranks, int nv,
                                 double* out, hipStream_t s);
 // Gauss-Newton moments of the accepted correspondences of [p0, p1) at T0 (R = rot(T0 * guess),
@@ -230,6 +236,9 @@ hipError_t launch_voxel_minpts(const float4* vox, const uint32_t* vox_rgba, size
                                uint32_t* flags, uint32_t* pos, void* scratch, size_t scratch_bytes,
                                float4* out, uint32_t* out_rgba, hipStream_t s);
 
+#if defined(MGICP_CORR_PHASES) && MGICP_CORR_PHASES
+hipError_t corr_phase_take(unsigned long long out[16]);  // diagnostic builds: read and reset
+#endif
 #if defined(MGICP_CORR_STATS) && MGICP_CORR_STATS
 hipError_t corr_stats_take(unsigned long long out[8]);  // diagnostic builds: read and reset
 #endif

@@ -43,6 +43,12 @@
 #ifndef MGICP_PACKED_RESID
 #define MGICP_PACKED_RESID 0  // 1: objective-pass residuals two per packed fp32 instruction (A/B: no gain, more spills; profiles/r02/ab_server)
 #endif
+#ifndef MGICP_CORR_PHASES
+#define MGICP_CORR_PHASES 0  // 1: per-phase shader-clock totals of the wave 1-NN sweep (diagnostic builds only)
+#endif
+#ifndef MGICP_CHUNK_SHFL
+#define MGICP_CHUNK_SHFL 0  // 1: chunk partials by 13 wave_sum shuffle trees (r02 form; 0 = wave_sum16, same bits)
+#endif
 #ifndef MGICP_SEED_BOX
 #define MGICP_SEED_BOX 1  // seeded 1-NN queries search the cube of their seed's ball (box_search)
 #endif
@@ -339,6 +345,19 @@ struct KnnVisitor {
   }
 };
 
+#if MGICP_CORR_PHASES
+// [0] seeds [1] union box + row table [2] union scan [3] winner [4] per-lane finish [5] stores,
+// shader-clock cycles summed over waves; [6] waves with a per-lane finish, [7] waves
+__device__ unsigned long long g_corr_phase[16];  // [8..12] waves by straggler count 0, 1-4, 5-16, 17-63, 64; [13] stragglers
+#define MGICP_PH(k)                                                                         \
+  do {                                                                                      \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();                             \
+    if (lane == 0) atomicAdd(&g_corr_phase[k], t_ - ph_t);                                  \
+    ph_t = t_;                                                                              \
+  } while (0)
+#else
+#define MGICP_PH(k) do {} while (0)
+#endif
 #if MGICP_CORR_STATS
 // [0] queries [1] accepted [2] rejected [3] candidates tested (accepted) [4] (rejected)
 // [5] cell ranges scanned (accepted) [6] (rejected)
@@ -914,35 +933,39 @@ __device__ __forceinline__ void load_cov(const Cov3& c, size_t i, double M[3][3]
 // its 6 face neighbours)
 __device__ __forceinline__ void seed_query(const GridView& tg, int seeded, uint32_t prev, float qx, float qy, float qz,
                                            NnVisitor& vis) {
-  if (seeded) {
-    // seed with last iteration's match: a real candidate, so the exact search only tightens it,
-    // and the ball-cell pruning starts from a near-final radius
-    if (prev != 0xffffffffu) vis.range(tg, prev, prev + 1);
-  }
-  if ((!seeded || MGICP_SEED_BOTH) && tg.seed) {
-#if MGICP_SEED_NEIGHBOURS
-    if (!seeded || MGICP_SEED_NEIGHBOURS > 1) {
-      const int cx = qcell(qx, tg.ox, tg.inv_h), cy = qcell(qy, tg.oy, tg.inv_h), cz = qcell(qz, tg.oz, tg.inv_h);
-      const int dd[7][3] = {{0, 0, 0}, {-1, 0, 0}, {1, 0, 0}, {0, -1, 0}, {0, 1, 0}, {0, 0, -1}, {0, 0, 1}};
+  // r03: every seed index first, then every seed point -- two dependent round trips for up to 8
+  // seeds instead of one per seed (a branch per seed serialised them: ~90k cycles per wave in
+  // the first sweep).  Loads are unconditional from valid addresses, results masked; the
+  // visitor's minimum does not depend on the order of the candidates.
+  constexpr uint32_t kNone = 0xffffffffu;
+  uint32_t sp[8];
 #pragma unroll
-      for (int k = 0; k < 7; ++k) {
-        const int x = cx + dd[k][0], y = cy + dd[k][1], z = cz + dd[k][2];
-        if (x >= 0 && x < tg.nx && y >= 0 && y < tg.ny && z >= 0 && z < tg.nz) {
-          const uint32_t pp = tg.seed[static_cast<size_t>(x) +
-                                      static_cast<size_t>(tg.nx) * (static_cast<size_t>(y) + static_cast<size_t>(tg.ny) * z)];
-          if (pp != 0xffffffffu) vis.range(tg, pp, pp + 1);
-        }
-      }
-      return;
-    }
-#endif
+  for (int k = 0; k < 8; ++k) sp[k] = kNone;
+  if (seeded) sp[7] = prev;  // last iteration's match
+  if ((!seeded || MGICP_SEED_BOTH) && tg.seed) {
+    // the seed map: a point of a Chebyshev-nearest non-empty cell of the query's cell (and, in the
+    // first sweep, of its 6 face neighbours)
     const int cx = qcell(qx, tg.ox, tg.inv_h), cy = qcell(qy, tg.oy, tg.inv_h), cz = qcell(qz, tg.oz, tg.inv_h);
-    if (cx >= 0 && cx < tg.nx && cy >= 0 && cy < tg.ny && cz >= 0 && cz < tg.nz) {
-      const uint32_t pp = tg.seed[static_cast<size_t>(cx) +
-                                  static_cast<size_t>(tg.nx) * (static_cast<size_t>(cy) + static_cast<size_t>(tg.ny) * cz)];
-      if (pp != 0xffffffffu) vis.range(tg, pp, pp + 1);
+    const bool seven = MGICP_SEED_NEIGHBOURS && (!seeded || MGICP_SEED_NEIGHBOURS > 1);
+    const int dd[7][3] = {{0, 0, 0}, {-1, 0, 0}, {1, 0, 0}, {0, -1, 0}, {0, 1, 0}, {0, 0, -1}, {0, 0, 1}};
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      if (k > 0 && !seven) break;
+      const int x = cx + dd[k][0], y = cy + dd[k][1], z = cz + dd[k][2];
+      const bool in = x >= 0 && x < tg.nx && y >= 0 && y < tg.ny && z >= 0 && z < tg.nz;
+      const size_t ci = in ? static_cast<size_t>(x) + static_cast<size_t>(tg.nx) *
+                                                          (static_cast<size_t>(y) + static_cast<size_t>(tg.ny) * z)
+                           : 0;
+      const uint32_t v = tg.seed[ci];
+      sp[k] = in ? v : kNone;
     }
   }
+  float4 pt[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) pt[k] = tg.pts[sp[k] != kNone ? sp[k] : 0u];
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+    if (sp[k] != kNone) vis.test(pt[k], sp[k]);
 }
 
 // ---- wave-uniform 1-NN sweep (r03) ----------------------------------------------------------
@@ -963,6 +986,15 @@ __device__ __forceinline__ void seed_query(const GridView& tg, int seeded, uint3
 // per-lane search from their best.
 typedef float f2v __attribute__((ext_vector_type(2)));
 typedef float f4v __attribute__((ext_vector_type(4)));
+
+// r03: lanes the union scan does not settle are handed to correspond_finish_kernel through a work
+// list instead of finishing in place -- in place, a wave waited for its slowest straggler with the
+// other lanes idle (62 % of the first sweep's waves had one; 66 % of its wave time)
+struct NnWork {
+  uint32_t q;     // shard-relative source position
+  uint32_t pos;   // the visitor's best so far (sorted target position)
+  unsigned long long best;  // its (d2 bits << 32 | index) key, ~0 = none
+};
 
 __device__ __forceinline__ int wave_min_i(int v) {
 #pragma unroll
@@ -998,11 +1030,15 @@ constexpr int kCorrRowSlots = 256;  // union-box rows whose cell bounds a wave k
 __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_wave_kernel(
     GridView tg, const float4* __restrict__ src, size_t p0, size_t p1, Xf34 T, double thr, int seeded,
     uint32_t* __restrict__ nn_pos, uint32_t* __restrict__ flags, const uint32_t* __restrict__ qperm, float rcap2,
-    int max_rows, int max_xcells, float union_min_r) {
+    int max_rows, int max_xcells, float union_min_r, NnWork* __restrict__ work, unsigned int* __restrict__ work_n,
+    int split_max) {
   __shared__ f4v stage[4][2 * kStagePairs];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const size_t t = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   const bool live = t < p1 - p0;  // no early exit: every lane of the wave takes part in the union scan
+#if MGICP_CORR_PHASES
+  unsigned long long ph_t = __builtin_amdgcn_s_memtime();
+#endif
   const size_t p = p0 + (live ? (qperm ? qperm[t] : t) : 0);
   float qx = 0.f, qy = 0.f, qz = 0.f;
   NnVisitor vis;
@@ -1012,6 +1048,7 @@ __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_wave_kernel(
   }
   vis.init(qx, qy, qz, thr);
   if (live) seed_query(tg, seeded, seeded ? nn_pos[p - p0] : 0xffffffffu, qx, qy, qz, vis);
+  MGICP_PH(0);
   // ---- the union box of the included lanes' seed balls
   const float bd0 = vis.prune2();
   bool incl = live && bd0 <= rcap2;
@@ -1066,6 +1103,7 @@ __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_wave_kernel(
     // to the per-lane search.  The winner inside the block is resolved exactly after the scan.
     float bcur = INFINITY;
     uint32_t bpi = 0;
+    MGICP_PH(1);
     // rows nearest the box centre first (the bounds shrink sooner; the order changes no result)
     const int zc = (Z0 + Z1) >> 1, yc = (Y0 + Y1) >> 1;
     const int zspan = 2 * max(zc - Z0, Z1 - zc), yspan = 2 * max(yc - Y0, Y1 - yc);
@@ -1119,6 +1157,7 @@ __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_wave_kernel(
         }
       }
     }
+    MGICP_PH(2);
     // the winner of the lane's best block: exact (d2, index) keys of its 4 candidates, masked like
     // the scan (a position outside the block's row cannot hold bcur: it was masked there, and it is
     // a real point tested in its own row -- taking it is still exact, the keys decide)
@@ -1143,11 +1182,41 @@ __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_wave_kernel(
     }
 #endif
   }
+  MGICP_PH(3);
   // ---- lanes the union scan did not settle (not included, or a tie between two distinct points
   // at the scan minimum): the per-lane exact search from their best
-  if (live && (!incl || tie)) {
-    if (vis.best != ~0ull) box_search(tg, qx, qy, qz, vis);
-    else ring_search(tg, qx, qy, qz, vis);
+  const bool fin = live && (!incl || tie);
+#if MGICP_CORR_PHASES
+  {
+    const int nf = __builtin_popcountll(__builtin_amdgcn_ballot_w64(fin));
+    if (lane == 0) {
+      if (nf) atomicAdd(&g_corr_phase[6], 1ull);
+      atomicAdd(&g_corr_phase[7], 1ull);
+      atomicAdd(&g_corr_phase[nf == 0 ? 8 : nf <= 4 ? 9 : nf <= 16 ? 10 : nf < 64 ? 11 : 12], 1ull);
+      atomicAdd(&g_corr_phase[13], static_cast<unsigned long long>(nf));
+    }
+  }
+#endif
+  const unsigned long long fm = __builtin_amdgcn_ballot_w64(fin);
+  if (work && __builtin_popcountll(fm) <= split_max) {
+    // hand the stragglers on: one atomic per wave, slots in lane order
+    const unsigned long long m = fm;
+    if (m) {
+      unsigned int base = 0;
+      if (lane == 0) base = atomicAdd(work_n, static_cast<unsigned int>(__builtin_popcountll(m)));
+      base = __builtin_amdgcn_readfirstlane(base);
+      const unsigned int off = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned int>(m >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo(static_cast<unsigned int>(m), 0u));
+      if (fin) work[base + off] = NnWork{static_cast<uint32_t>(p - p0), vis.pos, vis.best};
+    }
+    MGICP_PH(4);
+    if (!live || fin) return;
+  } else {
+    if (fin) {
+      if (vis.best != ~0ull) box_search(tg, qx, qy, qz, vis);
+      else ring_search(tg, qx, qy, qz, vis);
+    }
+    MGICP_PH(4);
   }
   if (!live) return;
   const bool ok = vis.best != ~0ull &&
@@ -1163,6 +1232,31 @@ __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_wave_kernel(
   atomicAdd(&g_corr_stats[4], static_cast<unsigned long long>(vis.nrange));
   if (!incl || tie) atomicAdd(&g_corr_stats[5], 1ull);
 #endif
+}
+
+// The stragglers of correspond_wave_kernel: the per-lane exact search from the visitor state the
+// union scan left (a real candidate and its key, or none), 64 of them per wave.  Grid-stride over
+// the device-side count.
+__global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_finish_kernel(
+    GridView tg, const float4* __restrict__ src, size_t p0, Xf34 T, double thr, const NnWork* __restrict__ work,
+    const unsigned int* __restrict__ work_n, uint32_t* __restrict__ nn_pos, uint32_t* __restrict__ flags) {
+  const unsigned int n = *work_n;
+  for (unsigned int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const NnWork w = work[i];
+    const float4 s = src[p0 + w.q];
+    float qx, qy, qz;
+    xform(T, s.x, s.y, s.z, qx, qy, qz);
+    NnVisitor vis;
+    vis.init(qx, qy, qz, thr);
+    vis.best = w.best;
+    vis.pos = w.pos;
+    if (vis.best != ~0ull) box_search(tg, qx, qy, qz, vis);
+    else ring_search(tg, qx, qy, qz, vis);
+    const bool ok = vis.best != ~0ull &&
+                    static_cast<double>(__uint_as_float(static_cast<uint32_t>(vis.best >> 32))) < thr;
+    nn_pos[w.q] = ok ? vis.pos : 0xffffffffu;
+    flags[w.q] = ok ? 1u : 0u;
+  }
 }
 
 // pair-interleaved copy of the sorted points (GridView::pairs): pair i = {x_2i, x_2i+1, y.., y..,
@@ -1241,6 +1335,14 @@ __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_kernel(GridV
 #endif
 }
 
+#if MGICP_CORR_PHASES
+hipError_t corr_phase_take(unsigned long long out[16]) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_corr_phase), 16 * sizeof(unsigned long long));
+  unsigned long long z[16] = {};
+  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_corr_phase), z, sizeof(z));
+  return e;
+}
+#endif
 #if MGICP_CORR_STATS
 hipError_t corr_stats_take(unsigned long long out[8]) {
   hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_corr_stats), 8 * sizeof(unsigned long long));
@@ -1390,6 +1492,65 @@ __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
   return v;
+}
+
+// ---- 16 values at once: wave_sum's tree as a reduce-scatter in registers (r03) -----------------
+// wave_sum pairs lanes (l, l + d) for d = 32, 16, 8, 4, 2, 1 -- the same pairs as l ^ d on the
+// lanes that carry the result -- so any scheme that adds exactly those pairs at every level gives
+// lane 0's sums bit for bit (fp64 addition is commutative).  Here, instead of 16 x 6 shuffles
+// through the LDS crossbar (192 ds_bpermute and ~60 exposed lgkmcnt waits per chunk at one wave per
+// SIMD), each level halves the values a lane keeps and exchanges only those: d = 32 and 16 by
+// gfx950's v_permlane32_swap / v_permlane16_swap, d = 8 by DPP row_ror:8, the last three levels on
+// two values by row_ror:12 and quad_perm (row_ror:n makes lane l read lane (l - n) mod 16 of its row;
+// the pairs needed are those of the lanes with bit 2 clear, where row_ror:12 reads lane l + 4 = l ^ 4).
+// About 70 VALU instructions, no LDS traffic.
+// Afterwards lane 8k (k = 0..7) holds values 2k and 2k + 1 (lane bits 5, 4, 3 = value bits 3, 2, 1).
+__device__ __forceinline__ unsigned int lo32(double v) {
+  return static_cast<unsigned int>(__double_as_longlong(v));
+}
+__device__ __forceinline__ unsigned int hi32(double v) {
+  return static_cast<unsigned int>(static_cast<unsigned long long>(__double_as_longlong(v)) >> 32);
+}
+__device__ __forceinline__ double mk64(unsigned int lo, unsigned int hi) {
+  return __longlong_as_double(static_cast<long long>((static_cast<unsigned long long>(hi) << 32) | lo));
+}
+template <int kCtrl>
+__device__ __forceinline__ double dpp64(double v) {
+  return mk64(static_cast<unsigned int>(__builtin_amdgcn_mov_dpp(static_cast<int>(lo32(v)), kCtrl, 0xF, 0xF, false)),
+              static_cast<unsigned int>(__builtin_amdgcn_mov_dpp(static_cast<int>(hi32(v)), kCtrl, 0xF, 0xF, false)));
+}
+// lanes with bit log2(kD) clear: a[l] + a[l ^ kD]; set: b[l] + b[l ^ kD]   (kD = 32 or 16)
+template <int kD>
+__device__ __forceinline__ double swap_add(double a, double b) {
+  unsigned int alo = lo32(a), ahi = hi32(a), blo = lo32(b), bhi = hi32(b);
+  if constexpr (kD == 32) {
+    const auto l = __builtin_amdgcn_permlane32_swap(alo, blo, false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap(ahi, bhi, false, false);
+    alo = l[0]; blo = l[1]; ahi = h[0]; bhi = h[1];
+  } else {
+    const auto l = __builtin_amdgcn_permlane16_swap(alo, blo, false, false);
+    const auto h = __builtin_amdgcn_permlane16_swap(ahi, bhi, false, false);
+    alo = l[0]; blo = l[1]; ahi = h[0]; bhi = h[1];
+  }
+  return mk64(alo, ahi) + mk64(blo, bhi);
+}
+__device__ __forceinline__ void wave_sum16(double (&v)[16], int lane) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = swap_add<32>(v[i], v[i + 8]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = swap_add<16>(v[i], v[i + 4]);
+  const bool b3 = (lane & 8) != 0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const double x = b3 ? v[i + 2] : v[i], y = b3 ? v[i] : v[i + 2];
+    v[i] = x + dpp64<0x128>(y);  // row_ror:8 = lane l ^ 8
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) v[i] = v[i] + dpp64<0x12C>(v[i]);  // row_ror:12 reads lane l + 4 = l ^ 4 where bit 2 is clear
+#pragma unroll
+  for (int i = 0; i < 2; ++i) v[i] = v[i] + dpp64<0x4E>(v[i]);   // quad_perm [2,3,0,1] = l ^ 2
+#pragma unroll
+  for (int i = 0; i < 2; ++i) v[i] = v[i] + dpp64<0xB1>(v[i]);   // quad_perm [1,0,3,2] = l ^ 1
 }
 
 // reduce kRedVals doubles across a 256-thread block; thread 0 writes dst[0..15]
@@ -1702,9 +1863,11 @@ __device__ __forceinline__ void chunk_store(int j, double (&acc)[kRedVals], cons
                                             size_t ns, double* __restrict__ partial, int lane) {
   const size_t e = min(static_cast<size_t>(j + 1) * kChunkPts, ns);
   const double cnt = static_cast<double>(pos[e] - pos[static_cast<size_t>(j) * kChunkPts]);
+  double* pj = partial + static_cast<size_t>(j) * kRedVals;
+#if MGICP_CHUNK_SHFL
+  // r02 form (A/B): 13 wave_sum shuffle trees, lane 0 stores
 #pragma unroll
   for (int v = 0; v < 13; ++v) acc[v] = wave_sum(acc[v]);
-  double* pj = partial + static_cast<size_t>(j) * kRedVals;
   if (lane == 0) {
 #pragma unroll
     for (int v = 0; v < 13; ++v) st_sc1(pj + v, acc[v]);
@@ -1712,6 +1875,17 @@ __device__ __forceinline__ void chunk_store(int j, double (&acc)[kRedVals], cons
     st_sc1(pj + 14, 0.0);
     st_sc1(pj + 15, 0.0);
   }
+#else
+  // acc[13..15] are never accumulated (+0.0), so value 13 -- the count -- is replaced after the
+  // tree and 14, 15 come out +0.0 as the r02 form stored them
+  wave_sum16(acc, lane);
+  if ((lane & 7) == 0) {
+    const double v1 = lane == 48 ? cnt : acc[1];
+    u32x4 w;
+    w.x = lo32(acc[0]); w.y = hi32(acc[0]); w.z = lo32(v1); w.w = hi32(v1);
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(pj + (lane >> 2)), "v"(w) : "memory");
+  }
+#endif
 }
 
 // After a wave stored all its chunk partials (chunks w0, w0 + nw, ...; reverse & 1: counted from
@@ -2520,13 +2694,26 @@ hipError_t launch_correspond(const GridView& tgt, const float4* src, size_t p0, 
 
 hipError_t launch_correspond_wave(const GridView& tgt, const float4* src, size_t p0, size_t p1, Xf34 T,
                                   double thr, int seeded, uint32_t* nn_pos, uint32_t* flags, const uint32_t* qperm,
-                                  float rcap2, int max_rows, int max_xcells, float union_min_r, hipStream_t s) {
+                                  float rcap2, int max_rows, int max_xcells, float union_min_r, void* work,
+                                  unsigned int* work_n, int split_max, hipStream_t s) {
   if (p1 <= p0) return hipSuccess;
-  if (!tgt.pairs) return hipErrorInvalidValue;
+  if (!tgt.pairs || (work && !work_n)) return hipErrorInvalidValue;
+  NnWork* w = static_cast<NnWork*>(work);
+  if (w) {
+    hipError_t e = hipMemsetAsync(work_n, 0, sizeof(unsigned int), s);
+    if (e != hipSuccess) return e;
+  }
   correspond_wave_kernel<<<nblk(p1 - p0), 256, 0, s>>>(tgt, src, p0, p1, T, thr, seeded, nn_pos, flags, qperm, rcap2,
-                                                       max_rows, max_xcells, union_min_r);
+                                                       max_rows, max_xcells, union_min_r, w, work_n, split_max);
+  if (w) {
+    // grid-stride over the stragglers: 8 blocks of 4 waves per CU (the count is known on the device only)
+    const unsigned int nb = static_cast<unsigned int>(std::min<size_t>(nblk(p1 - p0), 2048));
+    correspond_finish_kernel<<<nb, 256, 0, s>>>(tgt, src, p0, T, thr, w, work_n, nn_pos, flags);
+  }
   return hipGetLastError();
 }
+
+size_t nn_work_bytes(size_t n) { return n * sizeof(NnWork); }
 
 size_t pair_count(size_t n) { return (n + 1) / 2 + kStagePairs + 2; }
 
@@ -2638,6 +2825,31 @@ hipError_t launch_super_reduce(const double* chunk, int nch, int nv, double* sup
   if (nv == kRedVals) super_reduce_kernel<kRedVals><<<nsup, 64, 0, s>>>(chunk, nch, sup);
   else if (nv == kMomVals) super_reduce_kernel<kMomVals><<<nsup, 128, 0, s>>>(chunk, nch, sup);
   else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+// one wave per block: the 16 shuffle trees (lane 0) and the register reduce-scatter (lanes 8k)
+__global__ __launch_bounds__(64) void wave_reduce_check_kernel(const double* __restrict__ in, double* __restrict__ out_tree,
+                                                               double* __restrict__ out_rs) {
+  const int lane = threadIdx.x;
+  const double* row = in + (static_cast<size_t>(blockIdx.x) * 64 + lane) * 16;
+  double a[16], b[16];
+#pragma unroll
+  for (int v = 0; v < 16; ++v) a[v] = b[v] = row[v];
+#pragma unroll
+  for (int v = 0; v < 16; ++v) a[v] = wave_sum(a[v]);
+  if (lane == 0)
+    for (int v = 0; v < 16; ++v) out_tree[static_cast<size_t>(blockIdx.x) * 16 + v] = a[v];
+  wave_sum16(b, lane);
+  if ((lane & 7) == 0) {
+    out_rs[static_cast<size_t>(blockIdx.x) * 16 + (lane >> 2)] = b[0];
+    out_rs[static_cast<size_t>(blockIdx.x) * 16 + (lane >> 2) + 1] = b[1];
+  }
+}
+
+hipError_t launch_wave_reduce_check(const double* in, int nwaves, double* out_tree, double* out_rs, hipStream_t s) {
+  if (nwaves <= 0) return hipErrorInvalidValue;
+  wave_reduce_check_kernel<<<nwaves, 64, 0, s>>>(in, out_tree, out_rs);
   return hipGetLastError();
 }
 

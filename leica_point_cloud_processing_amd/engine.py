@@ -322,6 +322,17 @@ class GICPEngine:
         self._check(self._lib.mgicp_debug_fdf_sums(self._h, _dp(x), _dp(out)), "debug_fdf_sums")
         return out
 
+    def debug_wave_reduce(self, vals) -> tuple:
+        """(shuffle-tree sums, reduce-scatter sums) of vals[w][64][16] per wave w (the chunk reduction)"""
+        vals = np.ascontiguousarray(vals, np.float64)
+        nw = vals.shape[0]
+        assert vals.shape == (nw, 64, 16)
+        tree = np.zeros((nw, 16), np.float64)
+        rs = np.zeros((nw, 16), np.float64)
+        self._check(self._lib.mgicp_debug_wave_reduce(self._h, _dp(vals), int(nw), _dp(tree), _dp(rs)),
+                    "debug_wave_reduce")
+        return tree, rs
+
     def debug_pass_bench(self, x, npasses: int, mode: int = 0):
         """(ms per pass, sums of the last pass): npasses objective passes at x over the last sweep,
         back to back (mode 0: the resident pass server, 1: one launch per pass), HIP-event timed"""

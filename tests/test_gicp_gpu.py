@@ -117,6 +117,30 @@ def test_objective_pass(engine_mod, part_small):
         assert np.abs(g_gpu - g_ref).max() <= 1e-9 * max(1.0, np.abs(g_ref).max())
 
 
+def test_chunk_reduce_scatter_bitwise_equals_shuffle_tree(engine_mod):
+    """r03: the passes' chunk partials come from a register reduce-scatter (permlane swaps + DPP)
+    instead of 16 wave_sum shuffle trees; both add the same lane pairs at every level, so the sums
+    must be identical bit for bit -- on values whose rounding depends on the order (mixed signs and
+    magnitudes 1e-12..1e12, cancellations, zeros of both signs, subnormals)."""
+    rng = np.random.default_rng(11)
+    nw = 512
+    mag = 10.0 ** rng.uniform(-12, 12, size=(nw, 64, 16))
+    vals = rng.choice([-1.0, 1.0], size=(nw, 64, 16)) * mag * rng.uniform(0.5, 1.0, size=(nw, 64, 16))
+    vals[:8] = rng.normal(size=(8, 64, 16))  # plain data
+    vals[8, :, :] = 0.0
+    vals[8, ::2, 3] = -0.0  # signed zeros
+    vals[9, :, :] = 5e-324 * rng.integers(-3, 4, size=(64, 16))  # subnormals
+    vals[10, :32] = 1e16
+    vals[10, 32:] = -1e16  # cancellation against the tree's pairing
+    vals[10, 7] = 1.0
+    e = engine_mod()
+    tree, rs = e.debug_wave_reduce(vals)
+    assert np.array_equal(tree.view(np.int64), rs.view(np.int64))
+    # the tree really is order-sensitive on this data: a plain sequential sum differs somewhere
+    seq = vals.sum(axis=1)
+    assert not np.array_equal(seq, tree)
+
+
 def test_inlaunch_finish_no_stale_partials(engine_mod, part_small):
     """The in-launch reduction finish (sc1 partials + agent ticket) must never read a partial of
     a previous launch: alternate two states many times, every repeat bit-identical."""
