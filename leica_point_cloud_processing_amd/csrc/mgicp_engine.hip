@@ -1285,14 +1285,15 @@ int correspond(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
   ctx->seed_valid = true;
 #if defined(MGICP_CORR_PHASES) && MGICP_CORR_PHASES
   {
-    unsigned long long ph[16];
+    unsigned long long ph[24];
     HIPCK(hipStreamSynchronize(s));
     HIPCK(corr_phase_take(ph));
     const double w = ph[7] ? static_cast<double>(ph[7]) : 1.0;
     std::fprintf(stderr, "[corr-phase] waves %llu (per-lane finish %llu) | cycles/wave seeds %.0f box %.0f scan %.0f "
                  "winner %.0f finish %.0f | waves by stragglers 0:%llu 1-4:%llu 5-16:%llu 17-63:%llu 64:%llu, "
-                 "stragglers %llu\n", ph[7], ph[6], ph[0] / w, ph[1] / w, ph[2] / w, ph[3] / w, ph[4] / w, ph[8], ph[9],
-                 ph[10], ph[11], ph[12], ph[13]);
+                 "stragglers %llu | per-lane waves: none included %llu, rows %llu, x cells %llu, small balls %llu\n", ph[7],
+                 ph[6], ph[0] / w, ph[1] / w, ph[2] / w, ph[3] / w, ph[4] / w, ph[8], ph[9], ph[10], ph[11], ph[12], ph[13],
+                 ph[14], ph[15], ph[16], ph[17]);
   }
 #endif
 #if MGICP_CORR_STATS

@@ -237,7 +237,7 @@ hipError_t launch_voxel_minpts(const float4* vox, const uint32_t* vox_rgba, size
                                float4* out, uint32_t* out_rgba, hipStream_t s);
 
 #if defined(MGICP_CORR_PHASES) && MGICP_CORR_PHASES
-hipError_t corr_phase_take(unsigned long long out[16]);  // diagnostic builds: read and reset
+hipError_t corr_phase_take(unsigned long long out[24]);  // diagnostic builds: read and reset
 #endif
 #if defined(MGICP_CORR_STATS) && MGICP_CORR_STATS
 hipError_t corr_stats_take(unsigned long long out[8]);  // diagnostic builds: read and reset

@@ -348,7 +348,7 @@ struct KnnVisitor {
 #if MGICP_CORR_PHASES
 // [0] seeds [1] union box + row table [2] union scan [3] winner [4] per-lane finish [5] stores,
 // shader-clock cycles summed over waves; [6] waves with a per-lane finish, [7] waves
-__device__ unsigned long long g_corr_phase[16];  // [8..12] waves by straggler count 0, 1-4, 5-16, 17-63, 64; [13] stragglers
+__device__ unsigned long long g_corr_phase[24];  // [8..12] waves by straggler count 0, 1-4, 5-16, 17-63, 64; [13] stragglers
 #define MGICP_PH(k)                                                                         \
   do {                                                                                      \
     const unsigned long long t_ = __builtin_amdgcn_s_memtime();                             \
@@ -1074,6 +1074,16 @@ __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_wave_kernel(
                       static_cast<long long>(Z1 - Z0 + 1) * (Y1 - Y0 + 1) <= min(max_rows, kCorrRowSlots) &&
                       X1 - X0 + 1 <= max_xcells &&
                       __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(rsum))) >= union_min_r * tg.h * nincl;
+#if MGICP_CORR_PHASES
+  // why a wave is left to the per-lane search: [14] no lane included, [15] rows, [16] x cells,
+  // [17] mean seed bound below union_min_r (first failing test counted)
+  if (lane == 0 && !box_ok) {
+    const bool c0 = Z0 <= Z1 && Y0 <= Y1 && X0 <= X1;
+    const bool c1 = c0 && static_cast<long long>(Z1 - Z0 + 1) * (Y1 - Y0 + 1) <= min(max_rows, kCorrRowSlots);
+    const bool c2 = c1 && X1 - X0 + 1 <= max_xcells;
+    atomicAdd(&g_corr_phase[!c0 ? 14 : !c1 ? 15 : !c2 ? 16 : 17], 1ull);
+  }
+#endif
   if (!box_ok) incl = false;
   bool tie = false;
   if (box_ok) {
@@ -1336,9 +1346,9 @@ __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_kernel(GridV
 }
 
 #if MGICP_CORR_PHASES
-hipError_t corr_phase_take(unsigned long long out[16]) {
-  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_corr_phase), 16 * sizeof(unsigned long long));
-  unsigned long long z[16] = {};
+hipError_t corr_phase_take(unsigned long long out[24]) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_corr_phase), 24 * sizeof(unsigned long long));
+  unsigned long long z[24] = {};
   if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_corr_phase), z, sizeof(z));
   return e;
 }
