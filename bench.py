@@ -71,7 +71,7 @@ def parse():
                     help="1 = run the oracle on the full workload on the box's granted CPU share "
                          "(min(OMP_NUM_THREADS, affinity) threads: the thread-share CPU baseline + full-size "
                          "frob_vs_oracle; rank 0, N = 1 only)")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r02", "final", "pmc_summary.json"))
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "scripts", "pmc_summary_c4.json"))
     ap.add_argument("--gn-steps", type=int, default=5,
                     help="timed aligns of the opt-in Gauss-Newton mode (MGICP_SOLVER_GN; 0 = skip)")
     ap.add_argument("--fod-cpu-sample", type=int, default=500_000,
@@ -512,7 +512,7 @@ def main():
         "fdf_72B_stored": stored,
         "fdf_launched_52B": launched,
         "correspondence_plus_mahalanobis": roof(
-            "correspond_kernel + compact_kernel (1-NN sweep, Mahalanobis, compaction; once per outer iteration)",
+            "correspond_wave_kernel + compact_kernel (1-NN sweep, Mahalanobis, compaction; once per outer iteration)",
             CORR_BYTES, n_shard, corr_ms, kt["correspond"]["count"], "correspond_plus_compact",
             "SURVEY 8d: 72 B per source point (s 12 + Cs 24 + NN 12 + Ct 24)"),
         "knn_cov": roof(

@@ -25,7 +25,7 @@ STREAMING = {"fdf_soa_kernel", "fdf_server_kernel<true"}
 # --pass-bench-passes): its figures are per pass (dispatch / PASSES, the one-time resident load
 # included pro rata)
 PASSES = {"fdf_server_kernel<true": int(os.environ.get("PASS_BENCH_PASSES", "50"))}
-KERNELS = ("fdf_server_kernel<true", "fdf_soa_kernel", "correspond_kernel", "compact_kernel", "chunk_base_kernel", "knn_cov2_kernel",
+KERNELS = ("fdf_server_kernel<true", "fdf_soa_kernel", "correspond_wave_kernel", "correspond_kernel", "compact_kernel", "chunk_base_kernel", "knn_cov2_kernel",
            "knn_cov_kernel", "fitness_kernel", "gn_moments_kernel", "segdiff_kernel", "voxel_key_kernel",
            "voxel_centroid_kernel")
 
@@ -67,8 +67,9 @@ def main():
                 kernels[k]["per"] = f"pass (dispatch / {PASSES[k]})"
     if "fdf_server_kernel<true" in kernels:  # bench.py's key for the server's roofline traffic
         kernels["fdf_server_kernel"] = kernels.pop("fdf_server_kernel<true")
-    if "correspond_kernel" in kernels and "compact_kernel" in kernels:
-        a, b = kernels["correspond_kernel"], kernels["compact_kernel"]
+    sweep = "correspond_wave_kernel" if "correspond_wave_kernel" in kernels else "correspond_kernel"
+    if sweep in kernels and "compact_kernel" in kernels:
+        a, b = kernels[sweep], kernels["compact_kernel"]
         kernels["correspond_plus_compact"] = {
             "hbm_bytes_per_launch": a["hbm_bytes_per_launch"] + b["hbm_bytes_per_launch"],
             "correction": a["correction"],
