@@ -353,6 +353,7 @@ struct mgicp_ctx {
   int srv_waves = 4;                    // server shape: 4 or 8 waves per CU (env MGICP_SRV_WAVES)
   int stall_pass = -1;                  // env MGICP_SRV_STALL_PASS (tests): a server block withholds this pass
   bool corr_wave = true;                // wave-uniform 1-NN sweeps (env MGICP_CORR_WAVE)
+  int corr_lds_pts = -1;                // small-ball waves: union-box cell bounds in LDS (-1), + points when <= N fit (N > 0), off (0) (MGICP_CORR_LDS_PTS)
   int corr_split = 0;                   // waves of the wave sweep with <= this many stragglers hand them to a kernel of
                                         // their own (MGICP_CORR_SPLIT; 0 = every straggler finishes in place)
   float corr_rcap = 5.f;                // cells: lanes with a larger seed bound search alone (MGICP_CORR_RCAP)
@@ -1260,7 +1261,7 @@ hipError_t launch_sweep(mgicp_ctx* ctx, const Mat4& T, double thr, bool seeded, 
     }
     return launch_correspond_wave(g, ctx->d_out, p0, p1, T.xf(), thr, seeded ? 1 : 0, ctx->prev_pos.p,
                                   ctx->flags.p, qp, rc * rc, ctx->corr_max_rows, ctx->corr_max_x, ctx->corr_union_min_r,
-                                  work, ctx->nn_work_n.p, ctx->corr_split, ctx->stream);
+                                  work, ctx->nn_work_n.p, ctx->corr_split, ctx->corr_lds_pts, ctx->stream);
   }
   return launch_correspond(g, ctx->d_out, p0, p1, T.xf(), thr, seeded ? 1 : 0, ctx->prev_pos.p, ctx->flags.p, qp,
                            ctx->stream);
@@ -1748,6 +1749,7 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
   // the wave-uniform 1-NN scan (r03) and the target's pair copy it reads
   if (const char* cw = std::getenv("MGICP_CORR_WAVE")) ctx->corr_wave = std::atoi(cw) != 0;
   if (const char* cs = std::getenv("MGICP_CORR_SPLIT")) ctx->corr_split = std::atoi(cs);
+  if (const char* cl = std::getenv("MGICP_CORR_LDS_PTS")) ctx->corr_lds_pts = std::atoi(cl);
   if (const char* rc = std::getenv("MGICP_CORR_RCAP")) ctx->corr_rcap = static_cast<float>(std::atof(rc));
   if (const char* mr = std::getenv("MGICP_CORR_MAX_ROWS")) ctx->corr_max_rows = std::max(1, std::atoi(mr));
   if (const char* mx = std::getenv("MGICP_CORR_MAX_X")) ctx->corr_max_x = std::max(1, std::atoi(mx));

@@ -453,6 +453,61 @@ __device__ __forceinline__ void box_search(const GridView& g, float qx, float qy
   }
 }
 
+// LDS written by some lanes of a wave and read by others: LDS executes one wave's instructions in
+// order, so only the compiler must not move the reads above the writes
+__device__ __forceinline__ void lds_wave_sync() {
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  __builtin_amdgcn_wave_barrier();
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
+// box_search over a wave's union box staged in LDS (r03, correspond_wave_kernel's small-ball
+// waves): the same rows, x-ranges, pruning and candidate keys as box_search -- so the same result --
+// with the cell bounds and the points read from the wave's LDS copy instead of dependent global
+// gathers.  Row s = (z - Z0) * nyb + (y - Y0) of the box holds its cells' starts for x = X0 .. X1 + 1
+// at lb[s * (nxb + 1) ..] (global sorted positions) and its points from lp[loff[s]] on; the
+// lane's ball (radius from its current best) lies inside the box by construction.
+template <class V>
+__device__ __forceinline__ void box_search_lds(const GridView& g, float qx, float qy, float qz, V& vis, int Z0,
+                                               int Y0, int X0, int nyb, int nxb, const uint32_t* lb,
+                                               const uint32_t* loff, const float4* lp) {
+  const float R = sqrtf(vis.prune2() * 1.00001f) + g.slop;
+  const int za = max(qcell(qz - R, g.oz, g.inv_h), 0), zb = min(qcell(qz + R, g.oz, g.inv_h), g.nz - 1);
+  const int ya = max(qcell(qy - R, g.oy, g.inv_h), 0), yb = min(qcell(qy + R, g.oy, g.inv_h), g.ny - 1);
+  const int zc = min(max(qcell(qz, g.oz, g.inv_h), za), zb), yc = min(max(qcell(qy, g.oy, g.inv_h), ya), yb);
+  const int zdn = near_side(qz, g.oz, g.h, zc), ydn = near_side(qy, g.oy, g.h, yc);
+  const int zspan = 2 * max(zc - za, zb - zc), yspan = 2 * max(yc - ya, yb - yc);
+  const int nb = nxb + 1;
+  for (int mz = 0; mz <= zspan; ++mz) {
+    const int z = zc + ((mz & 1) ? zdn : -zdn) * ((mz + 1) >> 1);
+    if (z < za || z > zb) continue;
+    const float gz = cell_gap(qz, g.oz, g.h, z, g.slop);
+    const float gz2 = gz * gz;
+    if (gz2 > vis.prune2() * 1.00001f) continue;
+    for (int my = 0; my <= yspan; ++my) {
+      const int y = yc + ((my & 1) ? ydn : -ydn) * ((my + 1) >> 1);
+      if (y < ya || y > yb) continue;
+      const float w = vis.prune2() * 1.00001f;
+      const float gy = cell_gap(qy, g.oy, g.h, y, g.slop);
+      const float gyz = gy * gy + gz2;
+      if (gyz > w) continue;
+      const float rx = sqrtf(w - gyz) + g.slop;
+      const int xa = max(qcell(qx - rx, g.ox, g.inv_h), 0);
+      const int xb = min(qcell(qx + rx, g.ox, g.inv_h), g.nx - 1);
+      if (xa > xb) continue;
+      const int sr = (z - Z0) * nyb + (y - Y0);
+      const uint32_t* b = lb + sr * nb;
+      const uint32_t a0 = b[0], ja = b[xa - X0], jb = b[xb + 1 - X0];
+      if (lp) {
+        const float4* q = lp + loff[sr] + (ja - a0);
+        for (uint32_t j = ja; j < jb; ++j, ++q) vis.test(*q, j);
+      } else {
+        vis.range(g, ja, jb);  // bounds from LDS, candidates from the global sorted points
+      }
+    }
+  }
+}
+
 // radius-count visitor: counts points with float d2 < r2 (FLANN RadiusResultSet: dist < radius),
 // stopping as soon as `need` are found
 struct RadiusCountVisitor {
@@ -1026,13 +1081,20 @@ __device__ __forceinline__ void pair_d2(float qx, float qy, float qz, const f4v&
 
 constexpr int kStagePairs = 64;     // pairs staged per wave and chunk (128 candidates, 2 KiB of LDS)
 constexpr int kCorrRowSlots = 256;  // union-box rows whose cell bounds a wave keeps in registers (4 per lane)
+constexpr int kLdsRows = 64;        // small-ball LDS path: rows of the union box (one per lane in the scan)
+constexpr int kLdsBounds = 256;     // cell starts of the box kept in LDS (rows x (x cells + 1))
+constexpr int kLdsMeta = (kLdsBounds + kLdsRows) / 4;  // float4 slots of the bounds + row offsets
+constexpr int kLdsMaxPts = 512;     // largest lds_cap the kernel is built for (points per wave)
 
 __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_wave_kernel(
     GridView tg, const float4* __restrict__ src, size_t p0, size_t p1, Xf34 T, double thr, int seeded,
     uint32_t* __restrict__ nn_pos, uint32_t* __restrict__ flags, const uint32_t* __restrict__ qperm, float rcap2,
     int max_rows, int max_xcells, float union_min_r, NnWork* __restrict__ work, unsigned int* __restrict__ work_n,
-    int split_max) {
+    int split_max, int lds_cap) {
   __shared__ f4v stage[4][2 * kStagePairs];
+  // small-ball waves: the union box's cell bounds, row offsets and points (dynamic LDS, lds_cap
+  // points per wave; 0 = off)
+  extern __shared__ float4 s_lds[];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const size_t t = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   const bool live = t < p1 - p0;  // no early exit: every lane of the wave takes part in the union scan
@@ -1084,6 +1146,7 @@ __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_wave_kernel(
     atomicAdd(&g_corr_phase[!c0 ? 14 : !c1 ? 15 : !c2 ? 16 : 17], 1ull);
   }
 #endif
+  const bool incl0 = incl;
   if (!box_ok) incl = false;
   bool tie = false;
   if (box_ok) {
@@ -1191,6 +1254,72 @@ __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_wave_kernel(
       atomicAdd(&g_corr_stats[7], 1ull);
     }
 #endif
+  }
+  // ---- small-ball waves (union scan not worth it): stage the union box once per wave in LDS, then
+  // every included lane runs the exact box search from its seed bound on the LDS copy
+  if (!box_ok && lds_cap != 0 && Z0 <= Z1 && Y0 <= Y1 && X0 <= X1) {
+    const int nyb = Y1 - Y0 + 1, nxb = X1 - X0 + 1, nrows = (Z1 - Z0 + 1) * nyb, nb = nxb + 1;
+    if (nrows <= kLdsRows && nrows * nb <= kLdsBounds) {
+      const int cap = max(lds_cap, 0);  // lds_cap < 0: cell bounds only, candidates stay global gathers
+      uint32_t* lb = reinterpret_cast<uint32_t*>(s_lds + static_cast<size_t>(wid) * (cap + kLdsMeta));
+      uint32_t* loff = lb + kLdsBounds;
+      float4* lp = s_lds + static_cast<size_t>(wid) * (cap + kLdsMeta) + kLdsMeta;
+      // cell starts of every row of the box for x = X0 .. X1 + 1 (independent loads)
+      uint32_t cb[kLdsBounds / 64];
+#pragma unroll
+      for (int k = 0; k < kLdsBounds / 64; ++k) {
+        const int tt = lane + 64 * k;
+        const int sr = tt / nb, x = tt - sr * nb;
+        const uint32_t row = (static_cast<uint32_t>(Z0 + sr / nyb) * tg.ny + static_cast<uint32_t>(Y0 + sr % nyb)) * tg.nx;
+        cb[k] = tt < nrows * nb ? tg.cell_start[row + X0 + x] : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < kLdsBounds / 64; ++k)
+        if (lane + 64 * k < nrows * nb) lb[lane + 64 * k] = cb[k];
+      lds_wave_sync();
+      // row s (lane s) holds lb[s][nxb] - lb[s][0] points: exclusive scan over the rows
+      const uint32_t cnt = lane < nrows ? lb[lane * nb + nxb] - lb[lane * nb] : 0u;
+      uint32_t inc = cnt;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t u = __shfl_up(inc, off, 64);
+        if (lane >= off) inc += u;
+      }
+      const uint32_t npts = __builtin_amdgcn_readlane(inc, 63);
+      if (lane < nrows) loff[lane] = inc - cnt;
+      lds_wave_sync();
+      if (lds_cap < 0) {
+        if (incl0) box_search_lds(tg, qx, qy, qz, vis, Z0, Y0, X0, nyb, nxb, lb, loff, static_cast<const float4*>(nullptr));
+        incl = incl0;
+        tie = false;
+      } else if (npts <= static_cast<uint32_t>(cap)) {
+        // the points, in box order: slot t belongs to the last row whose offset is <= t
+        for (uint32_t k0 = 0; k0 < npts; k0 += 256) {  // 4 loads per lane in flight per round
+        float4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t tt = k0 + static_cast<uint32_t>(lane + 64 * k);
+          uint32_t gp = 0;
+          if (tt < npts) {
+            int lo = 0, hi = nrows - 1;
+            while (lo < hi) {
+              const int mid = (lo + hi + 1) >> 1;
+              if (loff[mid] <= tt) lo = mid; else hi = mid - 1;
+            }
+            gp = lb[lo * nb] + (tt - loff[lo]);
+          }
+          v[k] = tg.pts[gp];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (k0 + static_cast<uint32_t>(lane + 64 * k) < npts) lp[k0 + lane + 64 * k] = v[k];
+        }
+        lds_wave_sync();
+        if (incl0) box_search_lds(tg, qx, qy, qz, vis, Z0, Y0, X0, nyb, nxb, lb, loff, lp);
+        incl = incl0;  // settled exactly (keys decide ties): only lanes without a seed ball remain
+        tie = false;
+      }
+    }
   }
   MGICP_PH(3);
   // ---- lanes the union scan did not settle (not included, or a tie between two distinct points
@@ -2705,7 +2834,7 @@ hipError_t launch_correspond(const GridView& tgt, const float4* src, size_t p0, 
 hipError_t launch_correspond_wave(const GridView& tgt, const float4* src, size_t p0, size_t p1, Xf34 T,
                                   double thr, int seeded, uint32_t* nn_pos, uint32_t* flags, const uint32_t* qperm,
                                   float rcap2, int max_rows, int max_xcells, float union_min_r, void* work,
-                                  unsigned int* work_n, int split_max, hipStream_t s) {
+                                  unsigned int* work_n, int split_max, int lds_cap, hipStream_t s) {
   if (p1 <= p0) return hipSuccess;
   if (!tgt.pairs || (work && !work_n)) return hipErrorInvalidValue;
   NnWork* w = static_cast<NnWork*>(work);
@@ -2713,8 +2842,11 @@ hipError_t launch_correspond_wave(const GridView& tgt, const float4* src, size_t
     hipError_t e = hipMemsetAsync(work_n, 0, sizeof(unsigned int), s);
     if (e != hipSuccess) return e;
   }
-  correspond_wave_kernel<<<nblk(p1 - p0), 256, 0, s>>>(tgt, src, p0, p1, T, thr, seeded, nn_pos, flags, qperm, rcap2,
-                                                       max_rows, max_xcells, union_min_r, w, work_n, split_max);
+  if (lds_cap > 0) lds_cap = std::min(lds_cap, kLdsMaxPts) & ~63;
+  const size_t shm = lds_cap ? 4 * static_cast<size_t>(std::max(lds_cap, 0) + kLdsMeta) * sizeof(float4) : 0;
+  correspond_wave_kernel<<<nblk(p1 - p0), 256, shm, s>>>(tgt, src, p0, p1, T, thr, seeded, nn_pos, flags, qperm,
+                                                         rcap2, max_rows, max_xcells, union_min_r, w, work_n,
+                                                         split_max, lds_cap);
   if (w) {
     // grid-stride over the stragglers: 8 blocks of 4 waves per CU (the count is known on the device only)
     const unsigned int nb = static_cast<unsigned int>(std::min<size_t>(nblk(p1 - p0), 2048));
