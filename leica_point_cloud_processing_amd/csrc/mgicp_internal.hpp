@@ -190,7 +190,9 @@ hipError_t launch_fdf_server(const CorrSoA& c, const uint32_t* pos, const uint32
                              unsigned long long* host_rows /*nullable: super rows to the host, parity 0*/,
                              size_t rows_stride /*words from the parity-0 to the parity-1 row buffer*/, int nb,
                              int waves, int pollers /*blocks reading cmd themselves (1 or nb)*/,
-                             int stall_pass /*tests: -1, or the pass the last block withholds*/, hipStream_t s);
+                             int stall_pass /*tests: -1, or the pass the last block withholds*/,
+                             unsigned long long* tpart /*nullable: stamped chunk partials, 32 words per chunk (r03)*/,
+                             hipStream_t s);
 
 // super partials of nch chunk partials of nv (kRedVals or kMomVals) values
 hipError_t launch_super_reduce(const double* chunk, int nch, int nv, double* sup, hipStream_t s);

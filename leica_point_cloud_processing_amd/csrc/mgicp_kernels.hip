@@ -46,6 +46,9 @@
 #ifndef MGICP_CORR_PHASES
 #define MGICP_CORR_PHASES 0  // 1: per-phase shader-clock totals of the wave 1-NN sweep (diagnostic builds only)
 #endif
+#ifndef MGICP_SRV_NOTAIL
+#define MGICP_SRV_NOTAIL 0  // diagnostic builds: the server's timing form without its reduction tail
+#endif
 #ifndef MGICP_CHUNK_SHFL
 #define MGICP_CHUNK_SHFL 0  // 1: chunk partials by 13 wave_sum shuffle trees (r02 form; 0 = wave_sum16, same bits)
 #endif
@@ -2043,6 +2046,95 @@ __device__ __forceinline__ void chunk_store(int j, double (&acc)[kRedVals], cons
 #endif
 }
 
+// ---- the tagged tail of the resident server (r03) ------------------------------------------------
+// A chunk partial as 32 stamped words, value v in words 2v (low half) and 2v + 1 (high half), each
+// (rstamp << 32) | half and written whole by one write-through store (the 8-byte {data, tag}
+// granule of MI355X_MICROARCH "Valid forms"): a reader needs no ticket, drain or fence -- a word is
+// current when it carries this pass's stamp.
+__device__ __forceinline__ void chunk_store_tagged(int j, double (&acc)[kRedVals], const uint32_t* __restrict__ pos,
+                                                   size_t ns, unsigned long long* __restrict__ tpart, int lane,
+                                                   unsigned int rstamp) {
+  const size_t e = min(static_cast<size_t>(j + 1) * kChunkPts, ns);
+  const double cnt = static_cast<double>(pos[e] - pos[static_cast<size_t>(j) * kChunkPts]);
+  wave_sum16(acc, lane);
+  if ((lane & 7) == 0) {  // lane 8k: values 2k, 2k + 1 -> words 4k .. 4k + 3
+    const double v1 = lane == 48 ? cnt : acc[1];
+    unsigned long long* pj = tpart + static_cast<size_t>(j) * 32 + (lane >> 1);
+    u32x4 w0, w1;
+    w0.x = lo32(acc[0]); w0.y = rstamp; w0.z = hi32(acc[0]); w0.w = rstamp;
+    w1.x = lo32(v1); w1.y = rstamp; w1.z = hi32(v1); w1.w = rstamp;
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(pj), "v"(w0) : "memory");
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(pj + 2), "v"(w1) : "memory");
+  }
+}
+
+__device__ __forceinline__ unsigned long long ld_sc1_u64(const unsigned long long* p) {
+  return __hip_atomic_load(const_cast<unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The designated reducer of super sj (wave sj): its 16 sums -- lane v < 16 returns value v, the
+// chunks summed in chunk order exactly as wave_tickets does -- once every chunk of the super carries
+// this pass's stamp.  false (no row) when the host has moved on: a newer stamp in the command block
+// than the current pass `cur` in the command block (`cmd`, device memory the host writes through the
+// BAR; nullptr: not checked) or `limit`
+// wall-clock ticks without the super completing.
+// lane l reads chunks 8 (l >> 4) .. 8 (l >> 4) + 7 of value l & 15 (one round of 16 loads per lane);
+// the chunk-order chain then runs in lanes 0..15, the other quarters brought over by permlane swaps
+__device__ __forceinline__ double lane_from(double x, int q) {  // lane v < 16: x of lane v + 16 q
+  unsigned int l = lo32(x), h = hi32(x);
+  if (q & 2) {
+    l = __builtin_amdgcn_permlane32_swap(l, l, false, false)[1];
+    h = __builtin_amdgcn_permlane32_swap(h, h, false, false)[1];
+  }
+  if (q & 1) {
+    l = __builtin_amdgcn_permlane16_swap(l, l, false, false)[1];
+    h = __builtin_amdgcn_permlane16_swap(h, h, false, false)[1];
+  }
+  return mk64(l, h);
+}
+
+__device__ __forceinline__ bool super_sum_tagged(const unsigned long long* __restrict__ tpart, int sj, int nch,
+                                                 int lane, unsigned int rstamp, const PassCmd* cmd, unsigned int cur,
+                                                 unsigned long long limit, double& a) {
+  const int c0 = sj * kSuperChunks, nin = min(kSuperChunks, nch - c0);
+  const int v = lane & 15, qb = 8 * (lane >> 4);
+  const unsigned long long t0 = wall_clock64();
+  double t[8];
+  for (;;) {
+    bool ok = true;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const unsigned long long* w = tpart + static_cast<size_t>(c0 + min(qb + q, nin - 1)) * 32 + 2 * v;
+      const unsigned long long lo = ld_sc1_u64(w), hi = ld_sc1_u64(w + 1);
+      ok = ok && static_cast<unsigned int>(lo >> 32) == rstamp && static_cast<unsigned int>(hi >> 32) == rstamp;
+      t[q] = mk64(static_cast<unsigned int>(lo), static_cast<unsigned int>(hi));
+    }
+    if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
+    if (cmd) {
+      unsigned long long c[16];
+      read_cmd<true>(cmd, c);
+      const unsigned int st = __builtin_amdgcn_readfirstlane(static_cast<unsigned int>(c[0] >> 32));
+      if (static_cast<int>(st - cur) > 0) return false;  // a newer command: the host took the pass over
+    }
+    if (wall_clock64() - t0 > limit) return false;
+    __builtin_amdgcn_s_sleep(4);
+  }
+  // chunk order: a = t_0 + t_1 + ... + t_(nin-1), chunks 8k .. 8k + 7 from lane v + 16 k
+  a = t[0];
+#pragma unroll
+  for (int q = 1; q < 8; ++q)
+    if (q < nin) a = a + t[q];
+#pragma unroll
+  for (int k = 1; k < 4; ++k) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const double x = lane_from(t[q], k);
+      if (8 * k + q < nin) a = a + x;
+    }
+  }
+  return true;
+}
+
 // After a wave stored all its chunk partials (chunks w0, w0 + nw, ...; reverse & 1: counted from
 // the back): tickets, the supers it completes, and -- for the wave completing the last super -- the
 // total into `out` and `seq` into done_flag.  Returns true on that finishing wave.
@@ -2241,7 +2333,8 @@ __global__ __launch_bounds__(64 * kWaves, 1) void fdf_server_kernel(
     double* __restrict__ partial, double* __restrict__ spart, unsigned int* __restrict__ tickets,
     double* __restrict__ out, unsigned long long* done_flag, unsigned long long seq0, const PassCmd* cmd,
     PassCmd* mail, unsigned long long timeout, unsigned long long* ptimes, int bench_passes, Xf34 Abench,
-    unsigned long long* host_rows, size_t rows_stride, int pollers, int stall_pass) {
+    unsigned long long* host_rows, size_t rows_stride, int pollers, int stall_pass,
+    unsigned long long* __restrict__ tpart) {
   constexpr int kR = SrvShape<kWaves>::kReg, kL = SrvShape<kWaves>::kLds;
   static_assert(kR <= 4 && (kR == 4 || kR + kL <= 4), "resident groups: chunk 0, then chunk 1 only after a full chunk 0");
   __shared__ float4 lf[kWaves][kL][6][64];
@@ -2304,6 +2397,14 @@ __global__ __launch_bounds__(64 * kWaves, 1) void fdf_server_kernel(
       continue;  // tests: withhold this block's share of the pass
     unsigned long long* rows = host_rows ? host_rows + (rstamp & 1u) * rows_stride : nullptr;
     if (ptimes && blockIdx.x == 0 && threadIdx.x == 0) ptimes[2 * (seq & 1023)] = wall_clock64();
+    // r03: with host rows (and at most one super per wave) the chunk partials are stamped words and
+    // wave s reduces super s once all its chunks carry this pass's stamp: no chunk tickets, no drain
+    const int nsup = (nch + kSuperChunks - 1) / kSuperChunks;
+    const bool tagged = tpart != nullptr && rows != nullptr && nsup <= nw;
+    auto store = [&](int j, double (&acc)[kRedVals]) {
+      if (tagged) chunk_store_tagged(j, acc, pos, ns, tpart, lane, rstamp);
+      else chunk_store(j, acc, pos, ns, partial, lane);
+    };
     // odd waves take their streamed chunks first and their resident ones last, even waves the
     // reverse: the CU's memory pipe is never left idle while all its waves compute resident data
     // (the order of a wave's chunks does not change any sum)
@@ -2319,7 +2420,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void fdf_server_kernel(
           load_group(c, i, g);
           fdf_group(A, g, acc);
         }
-        chunk_store(w, acc, pos, ns, partial, lane);
+        store(w, acc);
       }
     };
     // stagger: wave wid computes its resident chunks after split(wid) of its streamed ones, so the
@@ -2346,7 +2447,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void fdf_server_kernel(
           fdf_group(A, g, acc);
         }
       }
-      chunk_store(w0, acc, pos, ns, partial, lane);
+      store(w0, acc);
     }
     if (w1 < nch) {
       double acc[kRedVals];
@@ -2365,14 +2466,57 @@ __global__ __launch_bounds__(64 * kWaves, 1) void fdf_server_kernel(
         load_group(c, i, g);
         fdf_group(A, g, acc);
       }
-      chunk_store(w1, acc, pos, ns, partial, lane);
+      store(w1, acc);
     }
     stream_chunks(split, nst);
     if (w0 >= nch) continue;
     // the timing form writes host rows too when given them (chained on the device by a global
     // ticket), so it times the pass the aligns run
-    const bool fin = wave_tickets(w0, nw, nch, 0, tickets, partial, spart, out, done_flag, seq, lane, rows,
-                                  kBench && rows, rstamp);
+#if MGICP_SRV_NOTAIL
+    // diagnostic build (timing form only): no chunk tickets, super sums or rows -- every wave takes
+    // the chain ticket once its chunks are stored; what the pass costs without its reduction tail
+    bool fin = false;
+    if (kBench) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned int nact = static_cast<unsigned int>(min(nw, nch));
+      const int nsup = (nch + kSuperChunks - 1) / kSuperChunks;
+      int l = 0;
+      if (lane == 0)
+        l = __hip_atomic_fetch_add(tickets + nsup, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) % nact == nact - 1 ? 1 : 0;
+      fin = __shfl(l, 0, 64) != 0;
+    } else {
+      fin = wave_tickets(w0, nw, nch, 0, tickets, partial, spart, out, done_flag, seq, lane, rows, false, rstamp);
+    }
+#else
+    bool fin = false;
+    if (tagged) {
+      if (w0 < nsup) {
+        double a = 0.0;
+        const PassCmd* watch = !kBench && host_pollers >= static_cast<int>(gridDim.x) ? cmd : nullptr;
+        if (super_sum_tagged(tpart, w0, nch, lane, rstamp, watch, static_cast<unsigned int>(seq), timeout >> 3, a)) {
+          // the super's row, as wave_tickets writes it: lane l < 32 stores half l & 1 of value l >> 1
+          const long long bits = __double_as_longlong(__shfl(a, lane >> 1, 64));
+          const unsigned int half = static_cast<unsigned int>((lane & 1) ? (bits >> 32) : bits);
+          if (lane < 32) {
+            const unsigned long long w = (static_cast<unsigned long long>(rstamp) << 32) | half;
+            asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1" ::"v"(rows + static_cast<size_t>(w0) * 32 + lane),
+                         "v"(w)
+                         : "memory");
+          }
+          if (kBench) {  // timing form: the reducer of the last super forwards the next command
+            int lastc = 0;
+            if (lane == 0)
+              lastc = __hip_atomic_fetch_add(tickets + nsup, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) %
+                              static_cast<unsigned>(nsup) == static_cast<unsigned>(nsup - 1) ? 1 : 0;
+            fin = __shfl(lastc, 0, 64) != 0;
+          }
+        }
+      }
+    } else {
+      fin = wave_tickets(w0, nw, nch, 0, tickets, partial, spart, out, done_flag, seq, lane, rows, kBench && rows,
+                         rstamp);
+    }
+#endif
     if (fin && lane == 0) {
       if (ptimes) ptimes[2 * (seq & 1023) + 1] = wall_clock64();
       if (kBench) {
@@ -2942,7 +3086,7 @@ hipError_t launch_fdf_server(const CorrSoA& c, const uint32_t* pos, const uint32
                              unsigned long long seq0, const PassCmd* cmd, PassCmd* mail,
                              unsigned long long timeout_ticks, unsigned long long* ptimes, int bench_passes,
                              Xf34 A, unsigned long long* host_rows, size_t rows_stride, int nb, int waves,
-                             int pollers, int stall_pass, hipStream_t s) {
+                             int pollers, int stall_pass, unsigned long long* tpart, hipStream_t s) {
   int nch = chunk_count(ns);
   if (nch == 0 || nb <= 0 || (waves != 4 && waves != 8)) return hipErrorInvalidValue;
   // a pass completes only when every block has run it, so refuse a grid the device cannot hold at
@@ -2965,7 +3109,7 @@ hipError_t launch_fdf_server(const CorrSoA& c, const uint32_t* pos, const uint32
 #define MGICP_SRV_LAUNCH(B, W)                                                                                  \
   fdf_server_kernel<B, W><<<nb, 64 * (W), 0, s>>>(c, pos, base, ns, nch, partial, spart, tickets, out, done_flag, \
                                                   seq0, cmd, mail, timeout_ticks, ptimes, bench_passes, A, host_rows, \
-                                                  rows_stride, pollers, stall_pass)
+                                                  rows_stride, pollers, stall_pass, tpart)
   if (waves == 4) {
     if (b) MGICP_SRV_LAUNCH(true, 4);
     else MGICP_SRV_LAUNCH(false, 4);
