@@ -860,6 +860,16 @@ int compute_cov(mgicp_ctx* ctx, Cloud& cl, size_t p0, size_t p1, size_t stride =
   }
   int rc = sync(ctx);
   if (rc) return rc;
+#if defined(MGICP_CORR_PHASES) && MGICP_CORR_PHASES
+  {
+    unsigned long long ph[24];
+    HIPCK(corr_phase_take(ph));
+    const double w = ph[21] ? static_cast<double>(ph[21]) : 1.0;
+    std::fprintf(stderr, "[knn-div] waves %llu | per wave: test iterations %.1f, max lane tests %.1f, mean lane tests %.1f"
+                 " | cycles/wave search %.0f, moments + finish %.0f\n",
+                 ph[21], ph[18] / w, ph[19] / w, ph[20] / w / 64.0, ph[22] / w, ph[23] / w);
+  }
+#endif
   MGICP_TRACE_AT("cov: done");
   cl.have_cov = true;
   cl.cov_p0 = p0;

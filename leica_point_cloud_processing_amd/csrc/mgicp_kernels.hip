@@ -27,6 +27,9 @@
 #ifndef MGICP_COV_WAVES
 #define MGICP_COV_WAVES 1  // resident waves per SIMD requested for the k-NN covariance kernel
 #endif
+#ifndef MGICP_KNN_DIV
+#define MGICP_KNN_DIV 0  // 1 (with MGICP_CORR_PHASES): k-NN candidate tests per lane vs per wave (diagnostic)
+#endif
 #ifndef MGICP_CORR_STATS
 #define MGICP_CORR_STATS 0  // 1: count 1-NN work per sweep (diagnostic builds only)
 #endif
@@ -761,6 +764,14 @@ __device__ __forceinline__ double sel3(int i, double a, double b, double c) {
 // lane's LDS log as its sorted position (the (d2, original index) key is recomputed from the point,
 // bit-identically, when the log is read): thresholds only fall, so the log holds every member of the
 // final k-NN set (ties at the final k-th included) -- no second search.
+#ifndef MGICP_KNN_LOG_BATCH
+#define MGICP_KNN_LOG_BATCH 8  // log entries read per batch (compaction, moments): loads in flight together
+#endif
+constexpr int kLogBatch = MGICP_KNN_LOG_BATCH;
+#ifndef MGICP_KNN_RANGE_BATCH
+#define MGICP_KNN_RANGE_BATCH 0  // candidates per guarded batch of the logged k-NN rows (0: 4-wide + tail)
+#endif
+
 template <int K>
 struct KthVisitor {
   static constexpr bool kNearFirst = true;
@@ -768,6 +779,9 @@ struct KthVisitor {
   float key[K];  // ascending; the first nsent slots hold the sentinel -1 (always in front)
   uint32_t* lpos;  // lane-strided LDS log of sorted positions, cap entries
   int cnt, cap;
+#if MGICP_KNN_DIV
+  unsigned ntest = 0, witer = 0;  // this lane's tests; wave iterations counted by the first active lane
+#endif
   __device__ __forceinline__ void init(float x, float y, float z, int nsent) {
     qx = x; qy = y; qz = z;
     cnt = 0;
@@ -778,15 +792,28 @@ struct KthVisitor {
   __device__ __forceinline__ float prune2() const { return key[K - 1]; }
   const float4* pts;
   // a full log drops the entries the threshold has since passed (d2 recomputed from the point)
+  // (entries in batches of kLogBatch: all loads of a batch in flight at once; writes only reach
+  // entries already read)
   __device__ __forceinline__ void compact() {
     int m = 0;
-    for (int i = 0; i < cnt; ++i) {
-      const uint32_t j = lpos[i * 64];
-      if (dist2(qx, qy, qz, pts[j]) <= key[K - 1]) lpos[(m++) * 64] = j;
+    for (int i0 = 0; i0 < cnt; i0 += kLogBatch) {
+      uint32_t j[kLogBatch];
+      float4 pt[kLogBatch];
+#pragma unroll
+      for (int u = 0; u < kLogBatch; ++u) j[u] = lpos[min(i0 + u, cnt - 1) * 64];
+#pragma unroll
+      for (int u = 0; u < kLogBatch; ++u) pt[u] = pts[j[u]];
+#pragma unroll
+      for (int u = 0; u < kLogBatch; ++u)
+        if (i0 + u < cnt && dist2(qx, qy, qz, pt[u]) <= key[K - 1]) lpos[(m++) * 64] = j[u];
     }
     cnt = m;
   }
   __device__ __forceinline__ void test(float d, float w, uint32_t j) {
+#if MGICP_KNN_DIV
+    ++ntest;
+    if (static_cast<unsigned>(__lane_id()) == static_cast<unsigned>(__builtin_ctzll(__builtin_amdgcn_read_exec()))) ++witer;
+#endif
     if (d <= key[K - 1]) {
       if (cnt == cap) compact();
       if (cnt < cap) lpos[cnt * 64] = j;
@@ -799,6 +826,18 @@ struct KthVisitor {
     }
   }
   __device__ __forceinline__ void range(const GridView& g, uint32_t a, uint32_t b) {
+#if MGICP_KNN_RANGE_BATCH
+    // guarded batches: every load of a batch in flight at once, a row's tail included (the
+    // clamped duplicate loads hit the same lines; their tests are skipped)
+    for (uint32_t j0 = a; j0 < b; j0 += MGICP_KNN_RANGE_BATCH) {
+      float4 pb[MGICP_KNN_RANGE_BATCH];
+#pragma unroll
+      for (int u = 0; u < MGICP_KNN_RANGE_BATCH; ++u) pb[u] = g.pts[min(j0 + u, b - 1)];
+#pragma unroll
+      for (int u = 0; u < MGICP_KNN_RANGE_BATCH; ++u)
+        if (j0 + u < b) test(dist2(qx, qy, qz, pb[u]), pb[u].w, j0 + u);
+    }
+#else
     const float4* q = g.pts + a;
     uint32_t j = a;
     for (; j + 4 <= b; j += 4, q += 4) {
@@ -809,6 +848,7 @@ struct KthVisitor {
       test(dist2(qx, qy, qz, p3), p3.w, j + 3);
     }
     for (; j < b; ++j, ++q) test(dist2(qx, qy, qz, *q), q->w, j);
+#endif
   }
 };
 
@@ -939,12 +979,35 @@ __global__ __launch_bounds__(64) void knn_cov2_kernel(GridView g, double eps, si
   if (t >= p1 - p0) return;
   const size_t p = p0 + (perm ? perm[t] : t);
   const float4 q = g.pts[p];
+#if MGICP_KNN_DIV
+  unsigned long long kt0 = __builtin_amdgcn_s_memtime();
+#endif
   KthVisitor<K> v1;
   v1.init(q.x, q.y, q.z, nsent);
   v1.lpos = s_pos + threadIdx.x;
   v1.pts = g.pts;
   v1.cap = cap;
   ring_search(g, q.x, q.y, q.z, v1);
+#if MGICP_KNN_DIV
+  {  // [18] wave iterations of test() [19] max over lanes of the lane's tests [20] lane tests [21] waves
+    // [22] search cycles [23] moments + finish cycles (shader clock, summed over waves)
+    const unsigned long long kt1 = __builtin_amdgcn_s_memtime();
+    if (threadIdx.x == 0) atomicAdd(&g_corr_phase[22], kt1 - kt0);
+    kt0 = kt1;
+    unsigned long long it = v1.witer, c = v1.ntest, cm = v1.ntest;
+    for (int o = 32; o; o >>= 1) {
+      it += __shfl_xor(it, o);
+      c += __shfl_xor(c, o);
+      cm = max(cm, __shfl_xor(cm, o));
+    }
+    if (threadIdx.x == 0) {
+      atomicAdd(&g_corr_phase[18], it);
+      atomicAdd(&g_corr_phase[19], cm);
+      atomicAdd(&g_corr_phase[20], c);
+      atomicAdd(&g_corr_phase[21], 1ull);
+    }
+  }
+#endif
   const int kreal = K - nsent;
   bool ok = v1.cnt <= cap;
   if (ok) {
@@ -953,9 +1016,14 @@ __global__ __launch_bounds__(64) void knn_cov2_kernel(GridView g, double eps, si
     double a[3][3] = {{0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}};
     SumCert c0, c1, c2, c00, c10, c11, c20, c21, c22;
     int m = 0;
-    for (int i = 0; i < v1.cnt; ++i) {
-      const float4 pt = g.pts[s_pos[i * 64 + threadIdx.x]];
-      if (dist2(q.x, q.y, q.z, pt) > tau) continue;
+    for (int i0 = 0; i0 < v1.cnt; i0 += kLogBatch) {
+     float4 pb[kLogBatch];
+#pragma unroll
+     for (int u = 0; u < kLogBatch; ++u) pb[u] = g.pts[s_pos[min(i0 + u, v1.cnt - 1) * 64 + threadIdx.x]];
+#pragma unroll
+     for (int u = 0; u < kLogBatch; ++u) {
+      const float4 pt = pb[u];
+      if (i0 + u >= v1.cnt || dist2(q.x, q.y, q.z, pt) > tau) continue;
       ++m;
       const float xx = pt.x * pt.x, yx = pt.y * pt.x, yy = pt.y * pt.y;
       const float zx = pt.z * pt.x, zy = pt.z * pt.y, zz = pt.z * pt.z;
@@ -977,11 +1045,15 @@ __global__ __launch_bounds__(64) void knn_cov2_kernel(GridView g, double eps, si
       c20.add(zx);
       c21.add(zy);
       c22.add(zz);
+     }
     }
     ok = m == kreal && c0.ok() && c1.ok() && c2.ok() && c00.ok() && c10.ok() && c11.ok() && c20.ok() &&
          c21.ok() && c22.ok();
     if (ok) cov_finish(m0, m1, m2, a, static_cast<double>(kreal), eps, cov, p);
   }
+#if MGICP_KNN_DIV
+  if (threadIdx.x == 0) atomicAdd(&g_corr_phase[23], __builtin_amdgcn_s_memtime() - kt0);
+#endif
   // log overflow, ties at tau or an uncertified sum: KnnVisitor's sorted (d2, index) list finishes
   // this point in a follow-up launch over the list (knn_cov_kernel with perm = fb)
   if (!ok) fb[atomicAdd(fb_count, 1u)] = static_cast<uint32_t>(p);
