@@ -769,7 +769,7 @@ __device__ __forceinline__ double sel3(int i, double a, double b, double c) {
 #endif
 constexpr int kLogBatch = MGICP_KNN_LOG_BATCH;
 #ifndef MGICP_KNN_RANGE_BATCH
-#define MGICP_KNN_RANGE_BATCH 0  // candidates per guarded batch of the logged k-NN rows (0: 4-wide + tail)
+#define MGICP_KNN_RANGE_BATCH 8  // candidates per guarded batch of the logged k-NN rows (0: 4-wide + tail)
 #endif
 
 template <int K>
