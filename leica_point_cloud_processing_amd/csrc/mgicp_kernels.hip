@@ -27,6 +27,9 @@
 #ifndef MGICP_COV_WAVES
 #define MGICP_COV_WAVES 1  // resident waves per SIMD requested for the k-NN covariance kernel
 #endif
+#ifndef MGICP_KNN_REGLIST_BATCH
+#define MGICP_KNN_REGLIST_BATCH 8  // register-list k-NN rows in guarded batches of this many points (0: 4-wide + tail)
+#endif
 #ifndef MGICP_KNN_DIV
 #define MGICP_KNN_DIV 0  // 1 (with MGICP_CORR_PHASES): k-NN candidate tests per lane vs per wave (diagnostic)
 #endif
@@ -340,6 +343,17 @@ struct KnnVisitor {
   }
   __device__ __forceinline__ void range(const GridView& g, uint32_t a, uint32_t b) {
     uint32_t j = a;
+#if MGICP_KNN_REGLIST_BATCH
+    // guarded batches (r03): every load of a batch in flight at once, the row's tail included
+    for (; j < b; j += MGICP_KNN_REGLIST_BATCH) {
+      float4 pb[MGICP_KNN_REGLIST_BATCH];
+#pragma unroll
+      for (int u = 0; u < MGICP_KNN_REGLIST_BATCH; ++u) pb[u] = g.pts[min(j + u, b - 1)];
+#pragma unroll
+      for (int u = 0; u < MGICP_KNN_REGLIST_BATCH; ++u)
+        if (j + u < b) test(pb[u], j + u);
+    }
+#else
     for (; j + 4 <= b; j += 4) {  // four gathers in flight per lane (latency-bound loop)
       const float4 p0 = g.pts[j], p1 = g.pts[j + 1], p2 = g.pts[j + 2], p3 = g.pts[j + 3];
       test(p0, j);
@@ -348,6 +362,7 @@ struct KnnVisitor {
       test(p3, j + 3);
     }
     for (; j < b; ++j) test(g.pts[j], j);
+#endif
   }
 };
 
