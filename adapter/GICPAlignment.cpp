@@ -10,6 +10,9 @@
  *  - iterate re-registers the original source with cached grids/covariances, fine_tf = T*fine_tf
  *  - applyTFtoCloud(cloud) writes aligned_cloud_, not cloud
  *  - transform_exists_ only changes on converged runs; getFineTransform logs when false
+ *  - every engine failure (invalid / too small cloud, device or transport error) is logged with
+ *    ROS_ERROR and leaves transform_exists_ and fine_tf_ untouched (failure row);
+ *    a failed fitness query is logged as a failure, never as a score
  */
 #include <GICPAlignment.h>
 
@@ -124,20 +127,39 @@ bool GICPAlignment::alignOnce(PointCloudRGB::Ptr output, Eigen::Matrix4f& T)
     if (!engine_)
         return false;
     mgicp_result res;
-    int rc = mgicp_align(engine_, nullptr, T.data(), &res);  // Eigen storage is column-major
-    if (output)
-    {
-        pcl::copyPointCloud(*source_cloud_, *output);
-        mgicp_transform_source(engine_, T.data(), xyzOf(*output), sizeof(pcl::PointXYZRGB));
-    }
+    Eigen::Matrix4f out = Eigen::Matrix4f::Identity();
+    int rc = mgicp_align(engine_, nullptr, out.data(), &res);  // Eigen storage is column-major
     if (rc == MGICP_E_SOLVER)
         return false;  // PCL swallowed the solver exception: hasConverged() == false
     if (rc != MGICP_OK)
     {
+        // no cloud, too few points, device / transport failure: the align did not run, T untouched
         reportEngineError(engine_, rc, "align");
         return false;
     }
+    if (output)
+    {
+        pcl::copyPointCloud(*source_cloud_, *output);
+        const int trc = mgicp_transform_source(engine_, out.data(), xyzOf(*output), sizeof(pcl::PointXYZRGB));
+        if (trc != MGICP_OK)
+        {
+            reportEngineError(engine_, trc, "transform of the aligned output");
+            return false;
+        }
+    }
+    T = out;
     return res.converged != 0;
+}
+
+// getFitnessScore for the log line; an engine failure is logged as such, never as a score
+void GICPAlignment::logFitness(const Eigen::Matrix4f& T)
+{
+    double fitness = 0.0;
+    const int rc = mgicp_fitness(engine_, T.data(), 0.0, &fitness);
+    if (rc != MGICP_OK)
+        reportEngineError(engine_, rc, "fitness score");
+    else
+        ROS_INFO("Converged in %f FitnessScore", fitness);
 }
 
 void GICPAlignment::fineAlignment()
@@ -148,8 +170,17 @@ void GICPAlignment::fineAlignment()
         ROS_ERROR("GICP no converge");
         return;
     }
-    mgicp_set_source(engine_, xyzOf(*source_cloud_), source_cloud_->points.size(), sizeof(pcl::PointXYZRGB));
-    mgicp_set_target(engine_, xyzOf(*target_cloud_), target_cloud_->points.size(), sizeof(pcl::PointXYZRGB));
+    // PCL's setInputSource / setInputTarget + initCompute: an empty or malformed cloud ends the
+    // align with an error and converged_ == false -- transform_exists_ and fine_tf_ stay as they were
+    int rc = mgicp_set_source(engine_, xyzOf(*source_cloud_), source_cloud_->points.size(), sizeof(pcl::PointXYZRGB));
+    if (rc == MGICP_OK)
+        rc = mgicp_set_target(engine_, xyzOf(*target_cloud_), target_cloud_->points.size(), sizeof(pcl::PointXYZRGB));
+    if (rc != MGICP_OK)
+    {
+        reportEngineError(engine_, rc, "GICP inputs");
+        ROS_ERROR("GICP no converge");
+        return;
+    }
 
     ros::Time begin = ros::Time::now();
     ROS_INFO("This step may take a while ...");
@@ -162,9 +193,7 @@ void GICPAlignment::fineAlignment()
         ROS_ERROR("GICP no converge");
         return;
     }
-    double fitness = 0.0;
-    mgicp_fitness(engine_, T.data(), 0.0, &fitness);
-    ROS_INFO("Converged in %f FitnessScore", fitness);
+    logFitness(T);
     fine_tf_ = T;
     transform_exists_ = Utils::isValidTransform(fine_tf_);
 }
@@ -181,9 +210,7 @@ void GICPAlignment::iterateFineAlignment(PointCloudRGB::Ptr cloud)
     }
     fine_tf_ = temp_tf * fine_tf_;
     Utils::printTransform(fine_tf_);
-    double fitness = 0.0;
-    mgicp_fitness(engine_, temp_tf.data(), 0.0, &fitness);
-    ROS_INFO("Converged in %f FitnessScore", fitness);
+    logFitness(temp_tf);
 }
 
 void GICPAlignment::iterate()
@@ -205,8 +232,12 @@ void GICPAlignment::applyTFtoCloud(PointCloudRGB::Ptr cloud)
 {
     pcl::copyPointCloud(*cloud, *aligned_cloud_);
     if (engine_ && !cloud->points.empty())
-        mgicp_transform_cloud(engine_, fine_tf_.data(), xyzOf(*cloud), cloud->points.size(), sizeof(pcl::PointXYZRGB),
-                              xyzOf(*aligned_cloud_), sizeof(pcl::PointXYZRGB));
+    {
+        const int rc = mgicp_transform_cloud(engine_, fine_tf_.data(), xyzOf(*cloud), cloud->points.size(),
+                                             sizeof(pcl::PointXYZRGB), xyzOf(*aligned_cloud_), sizeof(pcl::PointXYZRGB));
+        if (rc != MGICP_OK)
+            reportEngineError(engine_, rc, "applyTFtoCloud");
+    }
 }
 
 Eigen::Matrix4f GICPAlignment::getFineTransform()

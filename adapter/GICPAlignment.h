@@ -67,6 +67,7 @@ private:
     void iterateFineAlignment(PointCloudRGB::Ptr cloud);
     void backUp(PointCloudRGB::Ptr cloud);
     bool alignOnce(PointCloudRGB::Ptr output, Eigen::Matrix4f& T);
+    void logFitness(const Eigen::Matrix4f& T);
 };
 
 #endif

@@ -52,6 +52,11 @@ CONFIGS = {
                text="C4: 5M-pt scan vs 5M-pt CAD-sampled synthetic aero part"),
     "C5": dict(n_source=20_000_000, n_target=5_000_000, max_iter=100, fixed=False, occlusion=0.25,
                text="C5: 20M-pt scan (25% of the surface occluded) vs 5M-pt CAD, guess=I, full converge"),
+    # C4 with scan content that has no CAD partner: 4 % clutter 5-30 cm off the
+    # part, 40k points in 40 debris blobs 0.5-5 cm off it -- the gate rejects part of every sweep
+    "C4F": dict(n_source=5_000_000, n_target=5_000_000, max_iter=100, fixed=False, occlusion=0.0,
+                clutter=0.04, debris=40_000,
+                text="C4F: 5M-pt scan with 4% clutter + 40 debris blobs (no CAD partner) vs 5M-pt CAD"),
 }
 
 
@@ -94,7 +99,17 @@ def parse():
     args.n_source = args.n_source or cfg["n_source"]
     args.n_target = args.n_target or cfg["n_target"]
     args.max_iter, args.fixed, args.occlusion, args.cfg_text = cfg["max_iter"], cfg["fixed"], cfg["occlusion"], cfg["text"]
+    args.clutter, args.debris = cfg.get("clutter", 0.0), cfg.get("debris", 0)
     return args
+
+
+def gen_clouds(args, n_source=None, n_target=None):
+    """the config's synthetic scan-vs-CAD clouds (synth.scan_vs_cad), optionally at another size"""
+    from leica_point_cloud_processing_amd import synth
+
+    ns, nt = n_source or args.n_source, n_target or args.n_target
+    debris = int(round(args.debris * ns / args.n_source)) if args.debris else 0
+    return synth.scan_vs_cad(ns, nt, occlusion=args.occlusion, clutter=args.clutter, debris=debris)
 
 
 def dist_setup(args):
@@ -180,14 +195,13 @@ def dry_run(args, world, rank, pg):
                           "local_rank": int(os.environ.get("LOCAL_RANK", "0"))}))
 
 
-def cpu_baseline(n, threads, occlusion=0.0):
+def cpu_baseline(args, n, threads):
     """Oracle (PCL 1.8.1 restatement, single thread like PCL GICP) on a bounded sample of the
     same synthetic workload; per-iteration cost grows at least linearly with N, so the
     5M-equivalent rate is reported as sample_rate * n / 5M (an upper bound for the CPU)."""
-    from leica_point_cloud_processing_amd import synth
     from oracle import ref
 
-    scan, cad, _ = synth.scan_vs_cad(n, n, occlusion=occlusion)
+    scan, cad, _ = gen_clouds(args, n, n)
     g = ref.RefGICP(threads=threads)
     g.set_source(scan)
     g.set_target(cad)
@@ -292,11 +306,10 @@ def main():
     if args.dry_run:
         dry_run(args, world, rank, pg)
         return
-    from leica_point_cloud_processing_amd import synth
     from leica_point_cloud_processing_amd.engine import GICPEngine
 
     t_gen = time.time()
-    scan, cad, T_true = synth.scan_vs_cad(args.n_source, args.n_target, occlusion=args.occlusion)
+    scan, cad, T_true = gen_clouds(args)
     t_gen = time.time() - t_gen
 
     t_c = time.perf_counter()
@@ -340,6 +353,8 @@ def main():
     # timed region: K full align loops with no per-launch instrumentation (pre-launched, gated
     # objective passes on).  align() is host-synchronous (it returns with T on the host after its
     # stream drained), so the barrier on each side is the whole device synchronisation.
+    st0 = eng.pass_stats()
+    eng.server_time(reset=True)
     pg.barrier()
     t0 = time.perf_counter()
     total_iters = 0
@@ -351,6 +366,15 @@ def main():
     pg.barrier()
     dt = time.perf_counter() - t0
     dt = pg.allreduce_max(dt)
+    # which pass path the timed aligns ran: every pass on the resident server,
+    # none taken over by a launched pass; and the server's own in-align time per pass (two HIP events
+    # per server launch on the engine stream -- launch to exit, host round trips between passes
+    # included)
+    st1 = eng.pass_stats()
+    pass_stats_timed = {k: st1[k] - st0[k] for k in ("server_launches", "server_passes", "launched_passes",
+                                                      "takeovers", "server_denied")}
+    pass_stats_timed["bar_commands"] = st1["bar_commands"]
+    srv_inalign = eng.server_time(reset=True)
     # kernel-time leg (roofline): the same aligns with HIP events on the engine's stream around
     # every kernel family (objective passes sampled every 8th); events turn the gating off, so each
     # pass is timed from its own start -- the gated launches of the timed leg also hold the host's
@@ -471,11 +495,20 @@ def main():
                 "algorithmic_bytes_per_launch": int(alg), "avg_launch_ms": avg_ms,
                 "launches_timed": launches_timed, "numerator": note}
 
-    if srv is not None:
-        # the pass the aligns use: the resident server (timing form), per pass
+    traffic_src = os.path.relpath(args.pmc_json, ROOT) if pmc else None
+    if srv_inalign["passes"] > 0:
+        # the headline: the pass exactly as the timed aligns ran it -- fdf_server_kernel<false, 4>, one
+        # launch per BFGS run, duration / passes it served
+        pass_ms, pass_n = srv_inalign["ms_per_pass"], srv_inalign["passes"]
+        pass_name = ("fdf_server_kernel<false, 4> (resident pass server as the timed aligns ran it: BFGS objective "
+                     "pass, dominant; launch duration / passes served, host BFGS round trip between passes "
+                     "included)")
+        pass_pmc = "fdf_server_kernel"
+    elif srv is not None:
+        # no server ran in the timed aligns (another context held the device): the timing form
         pass_ms, pass_n = srv["ms_per_pass"], srv["passes_per_launch"] * srv["launches"]
-        pass_name = ("fdf_server_kernel (resident pass server: BFGS objective pass, dominant: 145 passes per C4 "
-                     "align; timing form fdf_server_kernel<true>, duration / passes_per_launch = one pass)")
+        pass_name = ("fdf_server_kernel (resident pass server, timing form fdf_server_kernel<true>, duration / "
+                     "passes_per_launch = one pass)")
         pass_pmc = "fdf_server_kernel"
     else:
         pass_ms, pass_n = fdf_ms, kt["fdf"]["count"]
@@ -484,14 +517,31 @@ def main():
     roofline = roof(pass_name, FDF_BYTES_SURVEY, m_shard, pass_ms, pass_n, pass_pmc,
                     "SURVEY 8d / BASELINE.md: 52 B per accepted correspondence per pass (M as 6 fp32)")
     roofline["launches"] = n_evals
+    roofline["traffic_source"] = (f"{traffic_src}: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of the timing form "
+                                  "(fdf_server_kernel<true, 4>, per pass), committed from the last profiled GPU job "
+                                  "(profiles/<round>/final/pmc_summary.json), not measured in this run"
+                                  if traffic_src else None)
+    roofline["pass_stats_timed"] = pass_stats_timed
     if srv is not None:
-        roofline["timing"] = (f"HIP events on the engine stream around {srv['launches']} server launches of "
-                              f"{srv['passes_per_launch']} back-to-back passes each (mgicp_debug_pass_bench mode 0: "
-                              "the aligns' pass -- super partials to host rows -- chained on the device by a "
-                              "global ticket instead of the host's next command) over the last timed align's "
-                              "correspondences; ~31 % of the bytes are register / LDS resident, the rest stream "
-                              "from HBM / Infinity Cache")
-        roofline["server"] = srv
+        tf_frac = (FDF_BYTES_SURVEY * m_shard / (srv["ms_per_pass"] * 1e-3) / 1e9 / HBM_PEAK_GBS
+                   if srv["ms_per_pass"] > 0 else None)
+        roofline["timing_form"] = {
+            **srv,
+            "frac_52B": round(tf_frac, 4) if tf_frac else None,
+            "timing": (f"HIP events on the engine stream around {srv['launches']} server launches of "
+                       f"{srv['passes_per_launch']} back-to-back passes each (mgicp_debug_pass_bench mode 0: the "
+                       "aligns' pass chained on the device by a global ticket instead of the host's next command, "
+                       "i.e. without the host BFGS round trip) over the last timed align's correspondences; "
+                       "~31 % of the bytes are register / LDS resident, the rest stream from HBM / Infinity Cache"),
+        }
+    if srv_inalign["passes"] > 0:
+        roofline["timing"] = (f"HIP events on the engine stream around each of the {srv_inalign['launches']} resident-"
+                              f"server launches of the timed aligns ({srv_inalign['passes']} passes, "
+                              f"{srv_inalign['ms']:.3f} ms in total): in-align time per pass = launch duration / "
+                              "passes served, the host's BFGS step between passes included")
+        roofline["server_in_align"] = srv_inalign
+    elif srv is not None:
+        roofline["timing"] = roofline["timing_form"]["timing"]
     else:
         roofline["timing"] = ("HIP events on the engine stream around every 8th objective pass of the timed region "
                               "(identical work per pass; sampling keeps the events' own cost out of value)")
@@ -534,7 +584,7 @@ def main():
     full = None
     if args.cpu_sample > 0 and world == 1:  # the CPU baseline is an N=1 figure
         n_cpu = min(args.cpu_sample, args.n_source)
-        rate, info, T_cpu, (s_scan, s_cad) = cpu_baseline(n_cpu, args.cpu_threads, args.occlusion)
+        rate, info, T_cpu, (s_scan, s_cad) = cpu_baseline(args, n_cpu, args.cpu_threads)
         scale = n_cpu / args.n_source
         single = {
             "value": rate * scale,
@@ -645,8 +695,14 @@ def main():
         "data_gen_s": round(t_gen, 2),
         "grid_occupancy": float(os.environ.get("MGICP_GRID_OCC", "0") or 0) or None,
     }
+    line["pass_stats_timed"] = pass_stats_timed
     eng.close()
     print(json.dumps(line))
+    if pass_stats_timed["takeovers"] > 0:
+        # a pass of the timed region missed its deadline and ran on the launched kernel: the number
+        # above does not describe the resident path
+        sys.stderr.write(f"bench.py: {pass_stats_timed['takeovers']} server take-over(s) in the timed region\n")
+        sys.exit(3)
 
 
 if __name__ == "__main__":

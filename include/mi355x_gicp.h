@@ -237,6 +237,13 @@ int mgicp_debug_kernel_times(mgicp_ctx* ctx, double out_ms[MGICP_KERNEL_FAMILIES
  * [6] transport (0 local, 1 RCCL, 2 shared segment, 3 shared segment + RCCL), [7] server launches
  * refused because another context of this process ran a server on the same device */
 int mgicp_debug_pass_stats(mgicp_ctx* ctx, long long out[8]);
+/* the resident pass server as the aligns run it (always on, two HIP events per server launch on the
+ * engine's stream, resolved when an align drains): *out_ms = summed device duration of the server
+ * launches (first command .. cancel, host round trips between passes included), *out_passes = the
+ * passes those launches ran, *out_launches = the launches; reset = 1 zeroes the counters after the
+ * read.  out_ms / out_passes = the in-align time of one objective pass. */
+int mgicp_debug_server_time(mgicp_ctx* ctx, double* out_ms, long long* out_passes, long long* out_launches,
+                            int reset);
 /* enable (1) / disable (0) per-launch HIP event timing (off by default); objective passes
  * ([2]) are sampled every 8th launch (env MGICP_PROF_STRIDE), every other family is timed on
  * every launch */

@@ -383,6 +383,11 @@ struct mgicp_ctx {
   shm::Segment shm;
   unsigned char* shm_d = nullptr;       // device view of the segment (hipHostRegister'ed)
   long long st[kStCount] = {};          // pass-path counters
+  // the resident server as the aligns run it (mgicp_debug_server_time): two events per launch
+  struct SrvEv { hipEvent_t a, b; long long passes; };
+  std::vector<SrvEv> srv_ev;            // launches not yet resolved (the last one may be live)
+  double srv_time_ms = 0;
+  long long srv_time_passes = 0, srv_time_launches = 0;
   bool spin_pause = false;              // env MGICP_SPIN_PAUSE: pause instruction in the row spin
   // MGICP_PASS_TIMES: host view of the server passes -- command published -> rows complete
   // (device pass + PCIe both ways) and rows complete -> next command (host BFGS step)
@@ -536,10 +541,43 @@ void cancel_gated(mgicp_ctx* ctx) {
   ctx->gated_seq = 0;
 }
 
+// server launches whose events have completed (after a drain: all of them) -> the in-align totals
+void srv_resolve(mgicp_ctx* ctx) {
+  for (auto& e : ctx->srv_ev) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, e.a, e.b) == hipSuccess) {
+      ctx->srv_time_ms += ms;
+      ctx->srv_time_passes += e.passes;
+      ctx->srv_time_launches += 1;
+    }
+    ctx->pool.push_back(e.a);
+    ctx->pool.push_back(e.b);
+  }
+  ctx->srv_ev.clear();
+}
+
 int sync(mgicp_ctx* ctx) {
   cancel_gated(ctx);  // a queued gated pass would otherwise hold the stream until its timeout
   HIPCK(hipStreamSynchronize(ctx->stream));
   if (ctx->profiling) prof_resolve(ctx);
+  if (!ctx->srv_ev.empty()) srv_resolve(ctx);
+  return MGICP_OK;
+}
+
+// Row stamps count objective passes; every buffer that holds stamps of earlier passes (the server's
+// stamped chunk partials, this context's private host rows) is cleared whenever the count restarts
+// (an attach or detach of the shared segment, the 2^31 wrap), so a stale word can never carry the
+// stamp of a new pass.  The stream is drained first: no server still writes them.
+int reset_stamps(mgicp_ctx* ctx) {
+  int rc = sync(ctx);
+  if (rc) return rc;
+  if (ctx->tpart.p && ctx->tpart_n) {
+    HIPCK(hipMemsetAsync(ctx->tpart.p, 0xff, ctx->tpart_n * sizeof(unsigned long long), ctx->stream));
+    HIPCK(hipStreamSynchronize(ctx->stream));
+  }
+  if (ctx->h_rows) std::memset(ctx->h_rows, 0, 2 * ctx->rows_cap * shm::kRowWords * sizeof(unsigned long long));
+  ctx->pass_idx = 0;
+  ctx->gather_idx = 0;
   return MGICP_OK;
 }
 
@@ -1366,11 +1404,12 @@ struct DeviceFunctor {
     // of the previous one (deterministic: the sums do not depend on the direction)
     const int reverse = (ctx->alt_sweep ? (ctx->n_evals & 1) : 0) | ctx->fdf_diag;
     const bool poll = ctx->poll && !ctx->fdf_diag;
+    // the pass's row stamp: the objective-pass index, identical on every rank (0 is never a stamp;
+    // stamps >= 2^31 belong to mgicp_debug_pass_bench's timing form).  At the wrap every stamped
+    // buffer is cleared and the count restarts at 1, so parity buffers keep alternating.
+    if (ctx->pass_idx + 1 >= 0x80000000u && (rc = reset_stamps(ctx))) return rc;
     const unsigned long long seq = ++ctx->pass_seq;
-    // the pass's row stamp: the objective-pass index, identical on every rank
-    // (0 is never a stamp; stamps >= 2^31 belong to mgicp_debug_pass_bench's timing form)
-    if (++ctx->pass_idx >= 0x80000000u) ctx->pass_idx = 1;
-    const unsigned int rstamp = ctx->pass_idx;
+    const unsigned int rstamp = ++ctx->pass_idx;
     // single GPU: the finishing wave writes the totals straight into mapped pinned host memory.
     // Shared row segment (any rank count): every pass -- server or launched -- writes its super rows
     // there and every host takes the total.  Otherwise (RCCL only) the pass leaves its super
@@ -1386,6 +1425,9 @@ struct DeviceFunctor {
                           (gate || (shm_rows && ctx->poll));
     const int cap = ctx->srv_cus > 0 ? std::min(ctx->srv_cus, ctx->cus) : ctx->cus;
     int nsrv = want_srv ? fdf_server_blocks(ns, cap, ctx->srv_waves) : 0;
+    // the host rows first: a failure here (e.g. a source larger than the shared segment) must not
+    // leave the device's server slot taken
+    if (!ctx->srv_live && (shm_rows || (nsrv > 0 && ctx->host_rows)) && (rc = ensure_rows(ctx))) return rc;
     if (nsrv > 0 && !ctx->srv_live) {
       int idle = 0;  // one server per device and process (g_srv_busy)
       ctx->srv_locked = g_srv_busy[ctx->device & 63].compare_exchange_strong(idle, 1, std::memory_order_acq_rel);
@@ -1395,29 +1437,42 @@ struct DeviceFunctor {
       }
     }
     const bool rows = shm_rows || (nsrv > 0 && ctx->host_rows);
-    if (rows && !ctx->srv_live && (rc = ensure_rows(ctx))) return rc;
     if (nsrv > 0) {
       // the resident server runs every pass of this BFGS run: start it with the first one
       if (!ctx->srv_live) {
         cancel_gated(ctx);
         ctx->ht_last_rows = 0;  // host-view diagnostics: a new BFGS run, not a host step
-        HIPCK(hipMemsetAsync(ctx->tickets.p, 0, ctx->tickets_n * sizeof(unsigned int), ctx->stream));
         const RowView rv = row_view(ctx);
-        ProfScope ps(ctx, kFamFdf);
-        const hipError_t e = launch_fdf_server(
-            c, ctx->cpos.p, ctx->chunk_base.p, ns, ctx->partial.p, ctx->spart.p, ctx->tickets.p, out, ctx->d_flag, seq,
-            ctx->bar_cmd ? ctx->bar_cmd : ctx->d_cmd, ctx->mail, ctx->gate_timeout, ctx->d_ptimes, 0, Ax,
-            rows ? rv.dev_rows(0) : nullptr, rv.stride, nsrv, ctx->srv_waves, ctx->bar_cmd ? nsrv : 1,
-            ctx->stall_pass, ctx->srv_tagged ? ctx->tpart.p : nullptr, ctx->stream);
+        hipEvent_t ea = ev_get(ctx);
+        hipError_t e = hipEventRecord(ea, ctx->stream);
+        if (e == hipSuccess) e = hipMemsetAsync(ctx->tickets.p, 0, ctx->tickets_n * sizeof(unsigned int), ctx->stream);
+        {
+          ProfScope ps(ctx, kFamFdf);
+          if (e == hipSuccess)
+            e = launch_fdf_server(c, ctx->cpos.p, ctx->chunk_base.p, ns, ctx->partial.p, ctx->spart.p, ctx->tickets.p,
+                                  out, ctx->d_flag, seq, ctx->bar_cmd ? ctx->bar_cmd : ctx->d_cmd, ctx->mail,
+                                  ctx->gate_timeout, ctx->d_ptimes, 0, Ax, rows ? rv.dev_rows(0) : nullptr, rv.stride,
+                                  nsrv, ctx->srv_waves, ctx->bar_cmd ? nsrv : 1, ctx->stall_pass,
+                                  ctx->srv_tagged ? ctx->tpart.p : nullptr, ctx->stream);
+        }
+        hipEvent_t eb = nullptr;
+        if (e == hipSuccess) {
+          eb = ev_get(ctx);
+          e = hipEventRecord(eb, ctx->stream);  // completes when the server exits (stream order)
+        }
         if (e != hipSuccess) {
           g_srv_busy[ctx->device & 63].store(0, std::memory_order_release);
           ctx->srv_locked = false;
+          ctx->pool.push_back(ea);
+          if (eb) ctx->pool.push_back(eb);
           HIPCK(e);
         }
+        ctx->srv_ev.push_back({ea, eb, 0});
         ctx->srv_live = true;
         ctx->st[kStSrvLaunch]++;
         ctx->st[kStBar] = ctx->bar_cmd ? 1 : 0;
       }
+      if (!ctx->srv_ev.empty()) ctx->srv_ev.back().passes++;
       const double t_pub = ctx->h_ptimes ? now_ms() : 0.0;
       if (ctx->h_ptimes && ctx->ht_last_rows > 0 && t_pub - ctx->ht_last_rows < 1.0) {
         ctx->ht_host += t_pub - ctx->ht_last_rows;
@@ -1852,6 +1907,7 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   if (ctx->bar_cmd) (void)hipFree(ctx->bar_cmd);
   if (ctx->h_small) (void)hipHostFree(ctx->h_small);
   prof_resolve(ctx);
+  srv_resolve(ctx);
   for (hipEvent_t e : ctx->pool) (void)hipEventDestroy(e);
   if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -2347,7 +2403,7 @@ int mgicp_comm_init(mgicp_ctx* ctx, int nranks, int rank, const unsigned char id
 int mgicp_comm_attach_shm(mgicp_ctx* ctx, const char* name, size_t max_source_points) {
   if (!ctx) return MGICP_E_INVALID;
   HIPCK(hipSetDevice(ctx->device));
-  int rc = sync(ctx);
+  int rc = reset_stamps(ctx);  // the stamp count restarts with the transport on every rank
   if (rc) return rc;
   if (ctx->have_shm) {
     (void)hipHostUnregister(ctx->shm.base);
@@ -2375,9 +2431,7 @@ int mgicp_comm_attach_shm(mgicp_ctx* ctx, const char* name, size_t max_source_po
   }
   ctx->shm = seg;
   ctx->shm_d = static_cast<unsigned char*>(d);
-  ctx->have_shm = true;
-  ctx->pass_idx = 0;    // row stamps and gather indices count from the attach on every rank
-  ctx->gather_idx = 0;
+  ctx->have_shm = true;  // row stamps and gather indices count from the attach (reset_stamps above)
   ctx->st[kStTransport] = ctx->comm ? 3 : 2;
   return MGICP_OK;
 }
@@ -2385,6 +2439,19 @@ int mgicp_comm_attach_shm(mgicp_ctx* ctx, const char* name, size_t max_source_po
 int mgicp_debug_pass_stats(mgicp_ctx* ctx, long long out[8]) {
   if (!ctx || !out) return MGICP_E_INVALID;
   for (int i = 0; i < kStCount; ++i) out[i] = ctx->st[i];
+  return MGICP_OK;
+}
+
+int mgicp_debug_server_time(mgicp_ctx* ctx, double* out_ms, long long* out_passes, long long* out_launches,
+                            int reset) {
+  if (!ctx || !out_ms || !out_passes || !out_launches) return MGICP_E_INVALID;
+  *out_ms = ctx->srv_time_ms;
+  *out_passes = ctx->srv_time_passes;
+  *out_launches = ctx->srv_time_launches;
+  if (reset) {
+    ctx->srv_time_ms = 0;
+    ctx->srv_time_passes = ctx->srv_time_launches = 0;
+  }
   return MGICP_OK;
 }
 

@@ -286,6 +286,18 @@ class GICPEngine:
         self._check(self._lib.mgicp_debug_pass_stats(self._h, out), "pass_stats")
         return {k: int(out[i]) for i, k in enumerate(self.PASS_STATS)}
 
+    def server_time(self, reset: bool = False) -> dict:
+        """The resident pass server as the aligns run it (mgicp_debug_server_time): summed launch
+        duration, passes and launches since the last reset; ms_per_pass = the in-align pass."""
+        ms = ctypes.c_double()
+        passes = ctypes.c_longlong()
+        launches = ctypes.c_longlong()
+        self._check(self._lib.mgicp_debug_server_time(self._h, ctypes.byref(ms), ctypes.byref(passes),
+                                                      ctypes.byref(launches), int(reset)), "server_time")
+        p = int(passes.value)
+        return {"ms": ms.value, "passes": p, "launches": int(launches.value),
+                "ms_per_pass": ms.value / p if p else None}
+
     # -- introspection (parity tests, profiling) ----------------------------------------------
     def debug_covariances(self, which: str, n: int) -> np.ndarray:
         out = np.zeros((n, 6), np.float64)

@@ -389,13 +389,46 @@ def aero_part_mesh(step: float = 0.1):
     return V.astype(np.float32), np.concatenate(tris).astype(np.int64)
 
 
+def _unit_dirs(g: np.random.Generator, m: int) -> np.ndarray:
+    v = g.normal(size=(m, 3))
+    return v / np.linalg.norm(v, axis=1, keepdims=True)
+
+
+def clutter_and_debris(verts, tris, n_clutter: int, n_debris: int, clusters: int, seed: int) -> np.ndarray:
+    """Scan points with no CAD partner -- what FODDetectionState subtracts the CAD for
+    (/root/reference/src/LeicaStateMachine.cpp:180-189):
+      * clutter: surface points pushed 5-30 cm off the part along a random direction (fixtures,
+        the floor, the scanner's mixed pixels), far beyond the 4 cm gate of GICPAlignment
+        (/root/reference/src/GICPAlignment.cpp:31) unless another face of the part lies near;
+      * debris: `clusters` blobs (uniform in balls of radius 0.5-2 cm) whose centres sit 0.5-5 cm
+        off a surface point -- partly inside, partly outside the gate.
+    Rows are in part coordinates (before noise and T_true), float64."""
+    g = np.random.Generator(np.random.PCG64(seed))
+    out = []
+    if n_clutter > 0:
+        base = cad_sample_fast(verts, tris, n_clutter, seed + 1).astype(np.float64)
+        out.append(base + _unit_dirs(g, n_clutter) * g.uniform(0.05, 0.30, size=(n_clutter, 1)))
+    if n_debris > 0:
+        clusters = max(1, min(clusters, n_debris))
+        ctr = cad_sample_fast(verts, tris, clusters, seed + 2).astype(np.float64)
+        ctr += _unit_dirs(g, clusters) * g.uniform(0.005, 0.05, size=(clusters, 1))
+        rad = g.uniform(0.005, 0.02, size=clusters)
+        which = np.arange(n_debris) % clusters
+        r = rad[which][:, None] * np.cbrt(g.uniform(size=(n_debris, 1)))
+        out.append(ctr[which] + _unit_dirs(g, n_debris) * r)
+    return np.concatenate(out) if out else np.zeros((0, 3))
+
+
 def scan_vs_cad(n_scan: int, n_cad: int, noise: float = 5e-4, angle: float = 0.02,
                 axis=(0.3, 0.5, 0.81), t=(0.010, -0.005, 0.008), occlusion: float = 0.0,
-                seeds=(1, 2, 3)):
+                seeds=(1, 2, 3), clutter: float = 0.0, debris: int = 0, debris_clusters: int = 40):
     """(scan_xyz, cad_xyz, T_true): CAD cloud = area-weighted sample (seed 1); scan =
     independent resample (seed 2) + N(0, noise^2) per axis (seed 3), moved by T_true (a
     rotation about `axis` through PART_CENTER plus t).  `occlusion` drops that fraction of
-    the surface area (triangles with the largest x) from the scan."""
+    the surface area (triangles with the largest x) from the scan.  `clutter` (a fraction of
+    n_scan) and `debris` (points in `debris_clusters` blobs) replace that many surface samples
+    by points without a CAD partner (clutter_and_debris, seed 4); they are spread through the
+    scan's order like the surface points.  clutter = debris = 0 gives the same clouds as before."""
     verts, tris = aero_part_mesh()
     cad = cad_sample_fast(verts, tris, n_cad, seeds[0])
     stris = tris
@@ -405,7 +438,20 @@ def scan_vs_cad(n_scan: int, n_cad: int, noise: float = 5e-4, angle: float = 0.0
         area = triangle_areas(verts, tris)[order]
         keep = np.cumsum(area) <= (1.0 - occlusion) * area.sum()
         stris = tris[order[keep]]
-    scan = cad_sample_fast(verts, stris, n_scan, seeds[1]).astype(np.float64)
+    n_clutter = int(round(clutter * n_scan))
+    n_extra = n_clutter + int(debris)
+    if n_extra > n_scan:
+        raise ValueError("clutter + debris exceed the scan size")
+    scan = cad_sample_fast(verts, stris, n_scan - n_extra, seeds[1]).astype(np.float64)
+    if n_extra:
+        extra = clutter_and_debris(verts, stris, n_clutter, int(debris), debris_clusters, 4)
+        pos = np.random.Generator(np.random.PCG64(5)).permutation(n_scan)[:n_extra]
+        full = np.empty((n_scan, 3))
+        mask = np.ones(n_scan, bool)
+        mask[pos] = False
+        full[mask] = scan
+        full[pos] = extra
+        scan = full
     g = np.random.Generator(np.random.PCG64(seeds[2]))
     for s in range(0, n_scan, 1 << 22):
         m = min(1 << 22, n_scan - s)

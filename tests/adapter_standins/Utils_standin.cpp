@@ -6,6 +6,7 @@
 #include <Utils.h>
 
 #include <chrono>
+#include <cstring>
 #include <limits>
 
 namespace ros
@@ -16,8 +17,13 @@ Time Time::now()
     return Time{duration<double>(steady_clock::now().time_since_epoch()).count()};
 }
 
+static int g_errors = 0;
+int error_count() { return g_errors; }
+
 void log(const char* level, const char* fmt, ...)
 {
+    if (std::strcmp(level, "ERROR") == 0)
+        ++g_errors;
     std::fprintf(stderr, "[%s] ", level);
     va_list ap;
     va_start(ap, fmt);

@@ -166,6 +166,37 @@ int main(int argc, char** argv)
         gicp_alignment.getAlignedCloud(undone);
         check(same_xyz(*undone, *aligned_cloud), "testRunWithCov_undo");
     }
+    {  // error paths (src/GICPAlignment.cpp:101-108, SURVEY 5 failure row): a good
+       // run, then an empty source, then a source with fewer points than k = 20 -- each run must log
+       // the failure and leave transform_exists_ and the fine transform untouched
+        PointCloudRGB::Ptr sourceRGB(new PointCloudRGB(*sourceRGB0)), targetRGB(new PointCloudRGB(*targetRGB0));
+        GICPAlignment g(targetRGB, sourceRGB, false);
+        ros::Time::init();
+        g.run();
+        const Eigen::Matrix4f T_good = g.getFineTransform();
+        check(g.transform_exists_, "errors_good_run_exists");
+        PointCloudRGB::Ptr empty(new PointCloudRGB);
+        g.setSourceCloud(empty);
+        const int e0 = ros::error_count();
+        g.run();
+        check(ros::error_count() > e0, "errors_empty_source_logged");
+        check(g.transform_exists_ && g.getFineTransform() == T_good, "errors_empty_source_untouched");
+        PointCloudRGB::Ptr few(new PointCloudRGB);
+        for (int i = 0; i < 10; ++i)
+            few->push_back(sourceRGB0->points[static_cast<size_t>(i)]);
+        g.setSourceCloud(few);
+        const int e1 = ros::error_count();
+        g.run();
+        check(ros::error_count() > e1, "errors_too_few_points_logged");
+        check(g.transform_exists_ && g.getFineTransform() == T_good, "errors_too_few_points_untouched");
+        g.setTargetCloud(empty);
+        g.setSourceCloud(sourceRGB);
+        const int e2 = ros::error_count();
+        g.run();
+        check(ros::error_count() > e2, "errors_empty_target_logged");
+        check(g.transform_exists_ && g.getFineTransform() == T_good, "errors_empty_target_untouched");
+        std::printf("errors_logged %d\n", ros::error_count());
+    }
     {  // the Filter members either side of the path (adapter/Filter_mi355x.cpp)
         PointCloudRGB::Ptr src(new PointCloudRGB(*sourceRGB0));
         Filter f(0.25);

@@ -171,6 +171,7 @@ struct Time
     Duration operator-(const Time& o) const { return Duration{s - o.s}; }
 };
 void log(const char* level, const char* fmt, ...);
+int error_count();  // ROS_ERROR lines so far (test stand-in only)
 }  // namespace ros
 
 #define ROS_INFO(...) ::ros::log("INFO", __VA_ARGS__)

@@ -85,3 +85,6 @@ def test_adapter_replays_reference_gicp_tests(cube_clouds, tmp_path):
     from leica_point_cloud_processing_amd.gicp_alignment import matmul4f
 
     np.testing.assert_array_equal(T_it, matmul4f(T_run, T_run))
+    # error paths: logged, transform_exists_ / fine_tf_ untouched
+    for name in ("errors_empty_source", "errors_too_few_points", "errors_empty_target"):
+        assert checks[name + "_logged"] and checks[name + "_untouched"], name

@@ -513,6 +513,103 @@ def test_concurrent_contexts_share_one_device(part_small):
         e.close()
 
 
+@pytest.mark.gpu
+def test_shm_attach_detach_reattach_bitwise(part_small):
+    """the row stamps restart at every attach / detach of the shared segment, so
+    every buffer holding stamps of earlier passes (the server's stamped chunk partials, the private
+    host rows) is cleared with them.  One context: a debug pass at another state and correspondence
+    set (stamp 1), attach, align, detach, align, attach a new segment, align -- each T, iteration and
+    pass count bitwise a fresh context's, every pass on the server, no take-over."""
+    from leica_point_cloud_processing_amd.engine import GICPEngine
+
+    scan, cad, Ttrue = part_small
+    f = GICPEngine()
+    f.set_source_xyz(scan)
+    f.set_target_xyz(cad)
+    T_ref = f.align()
+    res_ref = (f.last_result["iterations"], f.last_result["n_evals"])
+    f.close()
+    e = GICPEngine()
+    e.set_source_xyz(scan)
+    e.set_target_xyz(cad)
+    T_off = np.linalg.inv(Ttrue).astype(np.float32)
+    e.debug_correspondences(T_off, len(scan))
+    e.debug_fdf_sums(np.array([0.002, -0.001, 0.001, 0.0005, -0.0004, 0.0003]))  # pass stamp 1, other sums
+    names = [f"/mgicp_reattach_{os.getpid()}_{k}" for k in range(2)]
+    try:
+        for step in ("attach", "detach", "attach2"):
+            if step == "detach":
+                e.detach_shm()
+            else:
+                e.attach_shm(names[0 if step == "attach" else 1], len(scan))
+            st0 = e.pass_stats()
+            T = e.align()
+            st1 = e.pass_stats()
+            np.testing.assert_array_equal(T, T_ref, err_msg=step)
+            assert (e.last_result["iterations"], e.last_result["n_evals"]) == res_ref, step
+            assert st1["server_passes"] - st0["server_passes"] == res_ref[1], (step, st0, st1)
+            assert st1["takeovers"] == 0 and st1["launched_passes"] == st0["launched_passes"], (step, st1)
+            assert st1["transport"] == (0 if step == "detach" else 2), (step, st1)
+    finally:
+        e.close()
+    for nm in names:
+        assert not os.path.exists("/dev/shm" + nm)
+
+
+@pytest.mark.gpu
+def test_oversize_source_after_attach_frees_server_slot(part_small):
+    """a source larger than the shared segment (a recoverable user error) fails
+    the align before the device's server slot is taken -- another context then still gets a server."""
+    from leica_point_cloud_processing_amd import _lib
+    from leica_point_cloud_processing_amd import synth
+    from leica_point_cloud_processing_amd.engine import GICPEngine
+
+    big = synth.scan_vs_cad(100_000, 100_000)[:2]
+    name = f"/mgicp_oversize_{os.getpid()}"
+    e = GICPEngine()
+    try:
+        e.attach_shm(name, 40_000)  # 2 supers
+        e.set_source_xyz(big[0])   # 4 supers
+        e.set_target_xyz(big[1])
+        with pytest.raises(_lib.MgicpError):
+            e.align()
+        assert e.pass_stats()["server_launches"] == 0
+        g = GICPEngine()
+        g.set_source_xyz(part_small[0])
+        g.set_target_xyz(part_small[1])
+        g.align()
+        st = g.pass_stats()
+        g.close()
+        assert st["server_denied"] == 0 and st["server_passes"] == g.last_result["n_evals"] > 0, st
+    finally:
+        e.close()
+
+
+@pytest.mark.gpu
+def test_server_in_align_time_counts_every_pass():
+    """mgicp_debug_server_time (bench.py's headline roofline): after aligns on
+    the resident server, the summed launch durations cover every pass of every BFGS run."""
+    from leica_point_cloud_processing_amd import synth
+    from leica_point_cloud_processing_amd.engine import GICPEngine
+
+    scan, cad, _ = synth.scan_vs_cad(300_000, 300_000)
+    e = GICPEngine()
+    e.set_source_xyz(scan)
+    e.set_target_xyz(cad)
+    e.align()
+    e.server_time(reset=True)
+    its = evs = 0
+    for _ in range(3):
+        e.align()
+        its += e.last_result["iterations"]
+        evs += e.last_result["n_evals"]
+    t = e.server_time()
+    loop_ms = e.last_result["ms_loop"]
+    e.close()
+    assert t["launches"] == its and t["passes"] == evs, t
+    assert 0 < t["ms_per_pass"] < loop_ms, t
+
+
 def _shm_rank(name, world, rank, n, solver, env, q):
     """One rank of an RCCL-free multi-process run on ONE device: detached shard + shared rows."""
     try:

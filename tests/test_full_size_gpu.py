@@ -110,3 +110,39 @@ def test_c5_occluded_scan_deterministic():
     T2 = e.align()
     assert np.array_equal(T1, T2)
     assert np.abs(T1.astype(np.float64) @ T_true - np.eye(4)).max() < 0.05
+
+
+def test_c4f_gate_rejections_brute_force():
+    """VERDICT r03 item 1 at full size: the C4F scan (4 % clutter 5-30 cm off the part, 40 debris
+    blobs 0.5-5 cm off it) aligned, then the last sweep's gate decisions checked against a
+    brute-force float64 1-NN over the whole 5M target for accepted AND rejected queries."""
+    from leica_point_cloud_processing_amd import synth
+    from leica_point_cloud_processing_amd.engine import GICPEngine
+
+    scan, cad, T_true = synth.scan_vs_cad(N, N, clutter=0.04, debris=40_000)
+    e = GICPEngine()
+    e.set_source_xyz(scan)
+    e.set_target_xyz(cad)
+    T = e.align()
+    assert e.hasConverged()
+    n_corr = e.last_result["n_corr"]
+    assert n_corr < N
+    m, tj, _ = e.debug_correspondences(T, len(scan))  # a fresh (unseeded) sweep at the final T
+    assert 0 < m < N
+    q_all = synth.transform_points(T, scan).astype(np.float64)
+    tgt = cad.astype(np.float64)
+    rng = np.random.default_rng(12)
+    rej = np.flatnonzero(tj < 0)
+    acc = np.flatnonzero(tj >= 0)
+    assert len(rej) == N - m
+    gate = MAX_CORR * MAX_CORR
+    for i in np.concatenate([rng.choice(rej, 48, replace=False), rng.choice(acc, 48, replace=False)]):
+        d2 = ((tgt - q_all[i]) ** 2).sum(axis=1)
+        dmin = float(d2.min())
+        if abs(dmin - gate) <= 1e-5 * gate:
+            continue
+        if dmin > gate:
+            assert tj[i] == -1, (i, dmin)
+        else:
+            assert tj[i] >= 0, (i, dmin)
+            assert d2[tj[i]] <= dmin * (1 + 1e-5) + 1e-12, (i, d2[tj[i]], dmin)

@@ -30,12 +30,18 @@ ORACLE_THREADS = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS") or os.cpu_
 
 # BASELINE.json configs (sizes, iteration rule) -- identical to bench.py's CONFIGS.  C5 (configs[4]):
 # a 20M-point scan with 25 % of the surface occluded against a 5M CAD cloud, guess = I
-# (InitialAlignment NONE), run to full convergence -- the one config with partial overlap, where the
-# seeded sweeps, the empty-space map and the correspondence count differ most from C4.
+# (InitialAlignment NONE), run to full convergence.  The occlusion removes SCAN points only: the CAD
+# covers the whole part, so every scan point of C2-C5 has a partner within the 4 cm gate and
+# n_corr == N_s there.  C4F / C2F are the gate-rejecting workloads: 4 % of
+# the scan is clutter 5-30 cm off the part and 0.8 % sits in 40 debris blobs 0.5-5 cm off it (the
+# scan content FODDetectionState subtracts the CAD for, /root/reference/src/LeicaStateMachine.cpp:
+# 180-189), so the gate (src/GICPAlignment.cpp:31) rejects part of every sweep: n_corr < N_s.
 CONFIGS = {
     "C2": dict(n=100_000, nt=100_000, max_iter=100, fixed=False, occlusion=0.0),
+    "C2F": dict(n=100_000, nt=100_000, max_iter=100, fixed=False, occlusion=0.0, clutter=0.04, debris=800),
     "C3": dict(n=1_000_000, nt=1_000_000, max_iter=50, fixed=True, occlusion=0.0),
     "C4": dict(n=5_000_000, nt=5_000_000, max_iter=100, fixed=False, occlusion=0.0),
+    "C4F": dict(n=5_000_000, nt=5_000_000, max_iter=100, fixed=False, occlusion=0.0, clutter=0.04, debris=40_000),
     "C5": dict(n=20_000_000, nt=5_000_000, max_iter=100, fixed=False, occlusion=0.25),
 }
 
@@ -46,7 +52,8 @@ def _run_pair(name):
     from oracle import ref
 
     c = CONFIGS[name]
-    scan, cad, T_true = synth.scan_vs_cad(c["n"], c["nt"], occlusion=c["occlusion"])
+    scan, cad, T_true = synth.scan_vs_cad(c["n"], c["nt"], occlusion=c["occlusion"], clutter=c.get("clutter", 0.0),
+                                          debris=c.get("debris", 0))
     e = GICPEngine(max_iter=c["max_iter"], fixed_iterations=int(c["fixed"]))
     e.set_source_xyz(scan)
     e.set_target_xyz(cad)
@@ -63,7 +70,7 @@ def _run_pair(name):
     return T_gpu, tr_gpu, res, conv, T_ref, info, T_true
 
 
-@pytest.mark.parametrize("name", ["C2", "C3", "C4", "C5"])
+@pytest.mark.parametrize("name", ["C2", "C2F", "C3", "C4", "C4F", "C5"])
 def test_config_final_transform_vs_oracle(name):
     T_gpu, tr_gpu, res, conv, T_ref, info, T_true = _run_pair(name)
     err = frob(T_gpu, T_ref)
@@ -76,6 +83,9 @@ def test_config_final_transform_vs_oracle(name):
     assert conv == bool(info["converged"]) and conv
     assert res["iterations"] == info["iterations"]
     assert res["n_corr"] == info["n_corr_last"]  # the gate decisions of the last sweep, exactly
+    if CONFIGS[name].get("clutter"):
+        # the gate's rejection branch at full size: points without a CAD partner are dropped
+        assert res["n_corr"] < CONFIGS[name]["n"], res["n_corr"]
     if CONFIGS[name]["fixed"]:
         assert res["iterations"] == CONFIGS[name]["max_iter"]
     assert len(tr_gpu) == len(info["trace"])
