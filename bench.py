@@ -677,6 +677,8 @@ def main():
             "transport": transport,
         },
         "iterations_per_align": iters_per_align,
+        "n_corr": result["n_corr"],
+        "n_rejected_last_sweep": args.n_source - result["n_corr"] if world == 1 else None,
         "objective_passes_per_align": result["n_evals"],
         "ms_to_converge_first": round(first["ms_total"], 3),
         "ms_create": round(ms_create, 3),
