@@ -244,6 +244,11 @@ int mgicp_debug_pass_stats(mgicp_ctx* ctx, long long out[8]);
  * read.  out_ms / out_passes = the in-align time of one objective pass. */
 int mgicp_debug_server_time(mgicp_ctx* ctx, double* out_ms, long long* out_passes, long long* out_launches,
                             int reset);
+/* the target's 1-NN cell lists (DESIGN.md "1-NN cell lists"): out[0] cells requested and out[1]
+ * queries left to the exact per-lane search by the last sweep, out[2] cells with a list, out[3] list
+ * entries, out[4] reject cells, out[5] overflow cells, out[6] pool entries used, out[7] fine-grid
+ * cells (0 when the lists are off: env MGICP_VLIST=0 or a gate too wide for a fine grid) */
+int mgicp_debug_vlist_stats(mgicp_ctx* ctx, long long out[8]);
 /* enable (1) / disable (0) per-launch HIP event timing (off by default); objective passes
  * ([2]) are sampled every 8th launch (env MGICP_PROF_STRIDE), every other family is timed on
  * every launch */

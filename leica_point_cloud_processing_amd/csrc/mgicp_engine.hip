@@ -402,6 +402,17 @@ struct mgicp_ctx {
   DevBuf<uint32_t> knn_fb;          // points the logged k-NN kernel leaves to the register-list one
   unsigned int knn_fallbacks = 0;   // their count in the last covariance launch
   DevBuf<float> fpartial;
+  // the target's 1-NN cell lists (r04, DESIGN.md "1-NN cell lists"; env MGICP_VLIST=0: the r03 sweeps)
+  bool vlist = true;
+  float vlist_cell = 0.75f;           // fine cell edge / the target grid's cell edge (env MGICP_VLIST_CELL)
+  bool vl_stats = false;              // env MGICP_VLIST_STATS: per-sweep list diagnostics on stderr
+  bool vl_valid = false;              // lists belong to the current target grid and gate
+  bool vl_off = false;                // the gate is too large for a fine grid of this target: r03 sweeps
+  VListView vl{};
+  size_t vl_ncells = 0;
+  DevBuf<uint32_t> vl_cell, vl_pool_pos, vl_build, vl_bcentre, vl_pend;
+  DevBuf<float4> vl_pool;
+  DevBuf<unsigned int> vl_ctr;
   // multi-GPU
   int nranks = 1, rank = 0;
   ncclComm_t comm = nullptr;
@@ -823,6 +834,7 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
   cl.n_built = n;
   cl.dirty = false;
   cl.have_cov = false;
+  if (&cl == &ctx->tgt) ctx->vl_valid = false;  // the 1-NN cell lists index the old target
   if (&cl == &ctx->src || &cl == &ctx->tgt) {  // sorted positions changed
     ctx->have_corr = false;
     ctx->seed_valid = false;
@@ -1301,11 +1313,94 @@ CorrSoA corr_soa(mgicp_ctx* ctx) {
                  d, d + c, d + 2 * c, d + 3 * c, d + 4 * c, d + 5 * c};
 }
 
-// The 1-NN sweep kernel of one correspondence phase: the wave-uniform scan when the target has its
-// pair copy (default), else the per-lane search (env MGICP_CORR_WAVE=0); both exact, same results.
+// The fine grid of the target's 1-NN cell lists for the current gate (once per target grid and gate;
+// the lists themselves are built by the sweeps, cell by cell, the first time a query lands in a cell).
+// The grid covers the target's bbox grown by the gate + 2 cells, so a query outside it is farther than
+// the gate from every target point; cells of vlist_cell x the target grid's cell edge, fewer than 2^28
+// cells (else the lists are off for this gate: the r03 sweeps).
+int vl_prepare(mgicp_ctx* ctx) {
+  const double gate = ctx->prm.max_corr_dist;
+  const size_t ns = ctx->shard_p1() - ctx->shard_p0();
+  if (!(ctx->vl_valid && ctx->vl.gate == gate)) {
+    ctx->vl_valid = false;
+    ctx->vl_off = false;
+    const Cloud& t = ctx->tgt;
+    const double h = t.view.h;
+    double c = std::max(h * static_cast<double>(ctx->vlist_cell), 1e-6);
+    double ext = 0, maxabs = 0;
+    for (int d = 0; d < 3; ++d) {
+      ext = std::max(ext, static_cast<double>(t.hi[d] - t.lo[d]));
+      maxabs = std::max(maxabs, std::max(std::fabs(static_cast<double>(t.lo[d])), std::fabs(static_cast<double>(t.hi[d]))));
+    }
+    constexpr size_t kVlMaxCells = size_t(1) << 28;
+    int nd[3] = {0, 0, 0};
+    double pad = 0;
+    for (int it = 0; it < 64; ++it) {
+      pad = gate * (1.0 + 1e-5) + 1e-9 + 2.0 * c;
+      size_t nc = 1;
+      for (int d = 0; d < 3; ++d) {
+        nd[d] = static_cast<int>(std::floor((static_cast<double>(t.hi[d] - t.lo[d]) + 2.0 * pad) / c)) + 1;
+        nc *= static_cast<size_t>(nd[d]);
+      }
+      if (nc <= kVlMaxCells) break;
+      c *= std::cbrt(static_cast<double>(nc) / kVlMaxCells) * 1.01;
+    }
+    ctx->vl.gate = gate;
+    if (c > 4.0 * std::max(h, 1e-6)) {  // a gate this wide against this target: lists would overflow
+      ctx->vl_off = true;
+      ctx->vl_valid = true;
+      return MGICP_OK;
+    }
+    const size_t nc = static_cast<size_t>(nd[0]) * nd[1] * nd[2];
+    VListView& v = ctx->vl;
+    v.ox = static_cast<float>(t.lo[0] - pad);
+    v.oy = static_cast<float>(t.lo[1] - pad);
+    v.oz = static_cast<float>(t.lo[2] - pad);
+    v.c = static_cast<float>(c);
+    v.inv_c = static_cast<float>(1.0 / c);
+    // the fp32 cell assignment floor((q - o) * inv_c) of a query: a few ulps of the coordinates
+    // and of the cell count, covered with a wide margin
+    v.es = static_cast<float>(3.0e-6 * (maxabs + pad + ext) + 1e-4 * c);
+    v.nx = nd[0];
+    v.ny = nd[1];
+    v.nz = nd[2];
+    HIPCK(ctx->vl_cell.reserve(nc));
+    HIPCK(hipMemsetAsync(ctx->vl_cell.p, 0xff, nc * sizeof(uint32_t), ctx->stream));
+    const size_t cap = std::min<size_t>((size_t(1) << 26) - 1, std::max<size_t>(size_t(1) << 22, 16 * t.n));
+    HIPCK(ctx->vl_pool.reserve(cap));
+    HIPCK(ctx->vl_pool_pos.reserve(cap));
+    HIPCK(ctx->vl_ctr.reserve(4));
+    HIPCK(hipMemsetAsync(ctx->vl_ctr.p, 0, 4 * sizeof(unsigned int), ctx->stream));
+    v.cell = ctx->vl_cell.p;
+    v.pool = ctx->vl_pool.p;
+    v.pool_pos = ctx->vl_pool_pos.p;
+    v.pool_cap = static_cast<uint32_t>(cap);
+    v.ctr = ctx->vl_ctr.p;
+    ctx->vl_ncells = nc;
+    ctx->vl_valid = true;
+  }
+  if (ctx->vl_off) return MGICP_OK;
+  // per-sweep lists sized by the shard (one request / pending entry per query at most)
+  const size_t q = std::max<size_t>(ns, 1);
+  HIPCK(ctx->vl_build.reserve(q));
+  HIPCK(ctx->vl_bcentre.reserve(q));
+  HIPCK(ctx->vl_pend.reserve(q));
+  ctx->vl.build = ctx->vl_build.p;
+  ctx->vl.bcentre = ctx->vl_bcentre.p;
+  ctx->vl.build_cap = static_cast<uint32_t>(std::min(ctx->vl_build.cap, ctx->vl_ncells));
+  ctx->vl.pend = ctx->vl_pend.p;
+  return MGICP_OK;
+}
+
+// The 1-NN sweep kernel of one correspondence phase: the target's cell lists (r04, default), else the
+// wave-uniform scan when the target has its pair copy, else the per-lane search (env MGICP_VLIST=0,
+// MGICP_CORR_WAVE=0); all exact, same results.
 hipError_t launch_sweep(mgicp_ctx* ctx, const Mat4& T, double thr, bool seeded, const uint32_t* qp) {
   const size_t p0 = ctx->shard_p0(), p1 = ctx->shard_p1();
   const GridView& g = ctx->tgt.view;
+  if (ctx->vlist && ctx->vl_valid && !ctx->vl_off)
+    return launch_vl_sweep(g, ctx->vl, ctx->d_out, p0, p1, T.xf(), thr, seeded ? 1 : 0, ctx->prev_pos.p, ctx->flags.p,
+                           qp, ctx->cus, ctx->stream);
   if (ctx->corr_wave && g.pairs) {
     const float rc = ctx->corr_rcap * g.h;
     void* work = nullptr;
@@ -1335,11 +1430,34 @@ int correspond(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
   const bool seeded = seed && ctx->seed_valid;
   HIPCK(hipMemsetAsync(ctx->flags.p + ns, 0, sizeof(uint32_t), s));
   const uint32_t* qp = query_perm(ctx);
+  if (ctx->vlist) {
+    int rc = vl_prepare(ctx);
+    if (rc) return rc;
+  }
   {
     ProfScope ps(ctx, kFamCorr);
     HIPCK(launch_sweep(ctx, T, thr, seeded, qp));
   }
   ctx->seed_valid = true;
+  if (ctx->vl_stats && ctx->vlist && !ctx->vl_off) {
+    unsigned int c3[3];
+    HIPCK(hipMemcpyAsync(c3, ctx->vl_ctr.p, 3 * sizeof(unsigned int), hipMemcpyDeviceToHost, s));
+    HIPCK(ctx->u64.reserve(64));
+    HIPCK(launch_vl_stats(ctx->vl, ctx->vl_ncells, ctx->u64.p, s));
+    unsigned long long st[64];
+    HIPCK(hipMemcpyAsync(st, ctx->u64.p, sizeof(st), hipMemcpyDeviceToHost, s));
+    HIPCK(hipStreamSynchronize(s));
+    double hist_mean = st[0] ? static_cast<double>(st[1]) / st[0] : 0.0;
+    unsigned long long acc = 0, p95 = 0;
+    for (int L = 0; L < 56; ++L) {
+      acc += st[8 + L];
+      if (!p95 && acc >= 0.95 * st[0]) p95 = L;
+    }
+    std::fprintf(stderr, "[vlist] cell %.3f mm grid %dx%dx%d | sweep: %u cells requested, %u queries pending | lists %llu "
+                 "(mean %.1f, p95 %llu entries), reject %llu, overflow %llu, pool %u of %u\n",
+                 1e3 * ctx->vl.c, ctx->vl.nx, ctx->vl.ny, ctx->vl.nz, c3[1], c3[2], st[0], hist_mean, p95, st[2], st[3],
+                 c3[0], ctx->vl.pool_cap);
+  }
 #if defined(MGICP_CORR_PHASES) && MGICP_CORR_PHASES
   {
     unsigned long long ph[24];
@@ -1671,6 +1789,10 @@ int correspond_gn(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
   const double thr = ctx->prm.max_corr_dist * ctx->prm.max_corr_dist;
   const bool seeded = seed && ctx->seed_valid;
   const uint32_t* qp = query_perm(ctx);
+  if (ctx->vlist) {
+    int rc = vl_prepare(ctx);
+    if (rc) return rc;
+  }
   {
     ProfScope ps(ctx, kFamCorr);
     HIPCK(launch_sweep(ctx, T, thr, seeded, qp));
@@ -1828,6 +1950,12 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
   if (const char* mr = std::getenv("MGICP_CORR_MAX_ROWS")) ctx->corr_max_rows = std::max(1, std::atoi(mr));
   if (const char* mx = std::getenv("MGICP_CORR_MAX_X")) ctx->corr_max_x = std::max(1, std::atoi(mx));
   if (const char* um = std::getenv("MGICP_CORR_UNION_MIN_R")) ctx->corr_union_min_r = static_cast<float>(std::atof(um));
+  if (const char* vl = std::getenv("MGICP_VLIST")) ctx->vlist = std::atoi(vl) != 0;
+  if (const char* vc = std::getenv("MGICP_VLIST_CELL")) {
+    const float f = static_cast<float>(std::atof(vc));
+    if (f > 0.05f && f < 8.f) ctx->vlist_cell = f;
+  }
+  if (const char* vs = std::getenv("MGICP_VLIST_STATS")) ctx->vl_stats = std::atoi(vs) != 0;
   ctx->tgt.want_pairs = ctx->corr_wave;
   if (const char* cb = std::getenv("MGICP_CELL_BOXES")) ctx->tgt.want_boxes = std::atoi(cb) != 0;
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -1889,6 +2017,8 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   ctx->chunk_base.release(); ctx->spart.release(); ctx->gath.release(); ctx->msuper.release();
   ctx->prev_pos.release(); ctx->flags.release(); ctx->cpos.release();
   ctx->nn_work.release(); ctx->nn_work_n.release();
+  ctx->vl_cell.release(); ctx->vl_pool.release(); ctx->vl_pool_pos.release(); ctx->vl_ctr.release();
+  ctx->vl_build.release(); ctx->vl_bcentre.release(); ctx->vl_pend.release();
   ctx->tpart.release();
   ctx->tpart_n = 0;
   ctx->corr_f.release(); ctx->corr_d.release(); ctx->cscratch.release();
@@ -2452,6 +2582,31 @@ int mgicp_debug_server_time(mgicp_ctx* ctx, double* out_ms, long long* out_passe
     ctx->srv_time_ms = 0;
     ctx->srv_time_passes = ctx->srv_time_launches = 0;
   }
+  return MGICP_OK;
+}
+
+int mgicp_debug_vlist_stats(mgicp_ctx* ctx, long long out[8]) {
+  if (!ctx || !out) return MGICP_E_INVALID;
+  for (int i = 0; i < 8; ++i) out[i] = 0;
+  if (!ctx->vlist || !ctx->vl_valid || ctx->vl_off) return MGICP_OK;
+  HIPCK(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  unsigned int c3[3];
+  HIPCK(hipMemcpyAsync(c3, ctx->vl_ctr.p, 3 * sizeof(unsigned int), hipMemcpyDeviceToHost, s));
+  HIPCK(ctx->u64.reserve(64));
+  HIPCK(launch_vl_stats(ctx->vl, ctx->vl_ncells, ctx->u64.p, s));
+  unsigned long long st[64];
+  HIPCK(hipMemcpyAsync(st, ctx->u64.p, sizeof(st), hipMemcpyDeviceToHost, s));
+  int rc = sync(ctx);
+  if (rc) return rc;
+  out[0] = c3[1];
+  out[1] = c3[2];
+  out[2] = static_cast<long long>(st[0]);
+  out[3] = static_cast<long long>(st[1]);
+  out[4] = static_cast<long long>(st[2]);
+  out[5] = static_cast<long long>(st[3]);
+  out[6] = c3[0];
+  out[7] = static_cast<long long>(ctx->vl_ncells);
   return MGICP_OK;
 }
 

@@ -142,6 +142,43 @@ hipError_t launch_correspond_wave(const GridView& tgt, const float4* src, size_t
                                   int lds_cap /*small-ball waves: union box staged in LDS when it has <= lds_cap points*/,
                                   hipStream_t s);
 size_t nn_work_bytes(size_t n);
+
+// ---- the target's 1-NN cell lists (r04; DESIGN.md "1-NN cell lists") ----
+// A fine uniform grid over the target's bbox grown by the gate.  Per cell: the target points that can
+// be the exact 1-NN (fp32 FLANN d2, original-index tie-break) of some query in the cell whose d2 is
+// below the gate -- a superset, pruned by the affine dominance test against 9 anchor points -- or
+// "reject" (no target point within the gate of the cell).  Lists are built the first time a sweep
+// queries the cell and persist until the target or the gate changes.
+constexpr uint32_t kVlNotBuilt = 0xFFFFFFFFu;  // no list yet (a query requests it)
+constexpr uint32_t kVlRequested = 0xFFFFFFFEu; // queued for this sweep's build
+constexpr uint32_t kVlOverflow = 0xFFFFFFFDu;  // more than kVlMaxList entries / candidates / pool full
+constexpr uint32_t kVlReject = 0xFFFFFFFCu;    // no target point within the gate of the cell
+constexpr uint32_t kVlSpecial = 0xFFFFFFFCu;   // values >= this are states, below: (off << 6) | count
+constexpr int kVlMaxList = 63;
+struct VListView {
+  float ox, oy, oz;      // fine grid origin
+  float c, inv_c;        // fine cell edge and its float reciprocal
+  float es;              // box growth covering the fp32 cell assignment of queries
+  int nx, ny, nz;
+  double gate;           // max correspondence distance the lists are built for
+  uint32_t* cell;        // nx * ny * nz states / (off << 6 | count)
+  float4* pool;          // list entries {x, y, z, bits(original index)}
+  uint32_t* pool_pos;    // their sorted target positions
+  uint32_t pool_cap;     // entries (< 2^26)
+  unsigned int* ctr;     // [0] pool head (persistent), [1] cells requested, [2] queries pending (per sweep)
+  uint32_t* build;       // requested cells of this sweep
+  uint32_t* bcentre;     // per requested cell: sorted position of the cell centre's 1-NN (or none)
+  uint32_t build_cap;
+  uint32_t* pend;        // shard-relative positions of this sweep's queries without a list
+};
+// one sweep over the lists: listed queries answered at once, reject cells rejected, the others
+// queued (pend) and their cells requested; then the requested cells' lists are built and the
+// pending queries answered by the exact per-lane search (seeded like correspond_kernel)
+hipError_t launch_vl_sweep(const GridView& tgt, const VListView& vl, const float4* src, size_t p0, size_t p1,
+                           Xf34 T, double thr, int seeded, uint32_t* nn_pos, uint32_t* flags,
+                           const uint32_t* qperm, int cus, hipStream_t s);
+// diagnostics (env MGICP_VLIST_STATS): per built cell list lengths histogram etc. into out[64]
+hipError_t launch_vl_stats(const VListView& vl, size_t ncells, unsigned long long* out /*device, 64*/, hipStream_t s);
 size_t     pair_count(size_t n);
 hipError_t launch_pairs(const float4* pts, size_t n, float4* out, hipStream_t s);
 // Morton keys (30 bit, bbox lo, 1024 / extent = inv) of points [p0, p0 + n) and values 0..n-1

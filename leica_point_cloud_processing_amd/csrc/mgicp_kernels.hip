@@ -67,6 +67,8 @@ constexpr bool kSeedBox = MGICP_SEED_BOX != 0;
 
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+#include <cmath>
 #include <cstdlib>
 
 namespace mgicp {
@@ -1580,6 +1582,379 @@ __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_kernel(GridV
 #endif
 }
 
+// ---- 1-NN cell lists (r04): DESIGN.md "1-NN cell lists" ---------------------------------------------
+// Exactness (every claim on real numbers, every fp32 d2 within a relative 2.4e-7 of its real value):
+// a query q counted in fine cell C lies in C's box grown by es (the fp32 cell assignment).  Its fp32
+// 1-NN key winner t* -- when accepted (d2 < thr) -- lies within D(1 + 1e-5) of q, and within
+// |q - t_c| <= U of q (t_c: the cell centre's 1-NN, U: its largest distance to a box corner), so the
+// gathered set S = {t : boxdist(t, box) <= min(U, D)(1 + 1e-5)} holds it.  A point t is dropped from
+// S only when some real target point a is closer to EVERY point of the box by more than 1e-5 of t's
+// largest squared distance to the box: |q - t|^2 - |q - a|^2 is affine in q, so its minimum over the
+// box is taken at a corner and computed in closed form; then d2_f32(q, a) < d2_f32(q, t) for every
+// q in the box and t is never the winner.  So the list's minimum key is the exact winner for
+// accepted queries, and a rejected query's list minimum is >= thr as well (every listed point is a
+// real point, no closer than the true 1-NN).  Queries outside the fine grid, or in a cell with no
+// target point within D(1 + 1e-5) + its half diagonal of the centre, are rejected.
+constexpr int kVlCand = 512;  // candidates a build wave keeps in LDS (more: the cell stays a fallback cell)
+
+__device__ __forceinline__ void vl_cell_xyz(const VListView& v, uint32_t ci, uint32_t& ix, uint32_t& iy, uint32_t& iz) {
+  const uint32_t nx = static_cast<uint32_t>(v.nx), ny = static_cast<uint32_t>(v.ny);
+  ix = ci % nx;
+  iy = (ci / nx) % ny;
+  iz = ci / (nx * ny);
+}
+
+__global__ __launch_bounds__(256) void vl_query_kernel(GridView tg, VListView v, const float4* __restrict__ src,
+                                                       size_t p0, size_t p1, Xf34 T, double thr,
+                                                       uint32_t* __restrict__ nn_pos, uint32_t* __restrict__ flags,
+                                                       const uint32_t* __restrict__ qperm) {
+  const int lane = threadIdx.x & 63;
+  const size_t t = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const bool live = t < p1 - p0;
+  const uint32_t k = live ? (qperm ? qperm[t] : static_cast<uint32_t>(t)) : 0u;
+  float qx = 0.f, qy = 0.f, qz = 0.f;
+  if (live) {
+    const float4 s = src[p0 + k];
+    xform(T, s.x, s.y, s.z, qx, qy, qz);
+  }
+  const int ix = qcell(qx, v.ox, v.inv_c), iy = qcell(qy, v.oy, v.inv_c), iz = qcell(qz, v.oz, v.inv_c);
+  const bool inside = live && ix >= 0 && ix < v.nx && iy >= 0 && iy < v.ny && iz >= 0 && iz < v.nz;
+  const uint32_t ci = inside ? static_cast<uint32_t>(ix) +
+                                   static_cast<uint32_t>(v.nx) * (static_cast<uint32_t>(iy) +
+                                                                  static_cast<uint32_t>(v.ny) * static_cast<uint32_t>(iz))
+                             : 0u;
+  const uint32_t st = inside ? v.cell[ci] : kVlReject;
+  const bool pending = live && st >= kVlSpecial && st != kVlReject;
+  bool req = false;
+  if (pending && st == kVlNotBuilt) req = atomicCAS(&v.cell[ci], kVlNotBuilt, kVlRequested) == kVlNotBuilt;
+  // the cell's build request and the query's place in the pending list: one atomic per wave each
+  const unsigned long long rm = __builtin_amdgcn_ballot_w64(req);
+  if (rm) {
+    unsigned int base = 0;
+    if (lane == 0) base = atomicAdd(&v.ctr[1], static_cast<unsigned int>(__builtin_popcountll(rm)));
+    base = __builtin_amdgcn_readfirstlane(base);
+    const unsigned int o = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned int>(rm >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo(static_cast<unsigned int>(rm), 0u));
+    if (req) {
+      if (base + o < v.build_cap) v.build[base + o] = ci;
+      else atomicExch(&v.cell[ci], kVlNotBuilt);  // no room this sweep: requested again next time
+    }
+  }
+  const unsigned long long pm = __builtin_amdgcn_ballot_w64(pending);
+  if (pm) {
+    unsigned int base = 0;
+    if (lane == 0) base = atomicAdd(&v.ctr[2], static_cast<unsigned int>(__builtin_popcountll(pm)));
+    base = __builtin_amdgcn_readfirstlane(base);
+    const unsigned int o = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned int>(pm >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo(static_cast<unsigned int>(pm), 0u));
+    if (pending) v.pend[base + o] = k;
+  }
+  if (!live || pending) return;
+  unsigned long long best = ~0ull;
+  uint32_t bk = 0;
+  if (st < kVlSpecial) {
+    const uint32_t off = st >> 6, cnt = st & 63u;
+    const float4* e = v.pool + off;
+    for (uint32_t j = 0; j < cnt; j += 4) {
+      float4 a[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[u] = e[min(j + u, cnt - 1)];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const unsigned long long key = mkkey(dist2(qx, qy, qz, a[u]), a[u].w);
+        if (j + u < cnt && key < best) {
+          best = key;
+          bk = j + u;
+        }
+      }
+    }
+  }
+  const bool ok = best != ~0ull && static_cast<double>(__uint_as_float(static_cast<uint32_t>(best >> 32))) < thr;
+  nn_pos[k] = ok ? v.pool_pos[(st >> 6) + bk] : 0xffffffffu;
+  flags[k] = ok ? 1u : 0u;
+}
+
+// the requested cells' centres: exact 1-NN within sqrt(thr_c) (none: every point is farther than the
+// gate from the whole cell -> reject)
+__global__ __launch_bounds__(256) void vl_centre_kernel(GridView tg, VListView v, double thr_c) {
+  const unsigned int n = min(v.ctr[1], v.build_cap);
+  for (unsigned int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    uint32_t ix, iy, iz;
+    vl_cell_xyz(v, v.build[i], ix, iy, iz);
+    const float cx = v.ox + (static_cast<float>(ix) + 0.5f) * v.c;
+    const float cy = v.oy + (static_cast<float>(iy) + 0.5f) * v.c;
+    const float cz = v.oz + (static_cast<float>(iz) + 0.5f) * v.c;
+    NnVisitor vis;
+    vis.init(cx, cy, cz, thr_c);
+    seed_query(tg, 0, 0xffffffffu, cx, cy, cz, vis);
+    if (vis.best != ~0ull) box_search(tg, cx, cy, cz, vis);
+    else ring_search(tg, cx, cy, cz, vis);
+    const bool ok = vis.best != ~0ull &&
+                    static_cast<double>(__uint_as_float(static_cast<uint32_t>(vis.best >> 32))) < thr_c;
+    v.bcentre[i] = ok ? vis.pos : 0xffffffffu;
+  }
+}
+
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long y = __shfl_xor(x, o, 64);
+    x = y < x ? y : x;
+  }
+  return x;
+}
+
+// One wave per requested cell: gather S from the target grid (rows of the box grown by R, one round
+// trip for up to 64 rows' bounds, then the points), pick the anchors (the centre's 1-NN and each grown
+// corner's nearest candidate), drop every candidate an anchor dominates, append the rest to the pool.
+__global__ __launch_bounds__(256) void vl_build_kernel(GridView tg, VListView v) {
+  __shared__ float4 cand[4][kVlCand];
+  __shared__ uint32_t cpos[4][kVlCand];
+  __shared__ uint32_t rowa[4][64], rowp[4][64];
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const unsigned int n = min(v.ctr[1], v.build_cap);
+  const unsigned int nwv = gridDim.x * 4u;
+  for (unsigned int sl = blockIdx.x * 4u + static_cast<unsigned int>(wid); sl < n; sl += nwv) {
+    const uint32_t ci = v.build[sl];
+    const uint32_t tc = v.bcentre[sl];
+    if (tc == 0xffffffffu) {
+      if (lane == 0) v.cell[ci] = kVlReject;
+      continue;
+    }
+    uint32_t ix, iy, iz;
+    vl_cell_xyz(v, ci, ix, iy, iz);
+    const uint32_t ii[3] = {ix, iy, iz};
+    const float o3[3] = {v.ox, v.oy, v.oz};
+    double lo[3], hi[3], ctr[3], hx[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      lo[d] = static_cast<double>(o3[d]) + static_cast<double>(ii[d]) * static_cast<double>(v.c) - v.es;
+      hi[d] = lo[d] + static_cast<double>(v.c) + 2.0 * v.es;
+      ctr[d] = 0.5 * (lo[d] + hi[d]);
+      hx[d] = 0.5 * (hi[d] - lo[d]);
+    }
+    const float4 pc = tg.pts[tc];
+    const double pc3[3] = {pc.x, pc.y, pc.z};
+    double U2 = 0.0;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      const double m = fmax(fabs(lo[d] - pc3[d]), fabs(hi[d] - pc3[d]));
+      U2 += m * m;
+    }
+    const double Dp = v.gate * (1.0 + 1e-5) + 1e-9;
+    const double R = fmin(sqrt(U2) * (1.0 + 1e-5) + 1e-9, Dp);
+    const float R2f = static_cast<float>(R * R) * 1.0001f + 1e-12f;
+    const float lof[3] = {static_cast<float>(lo[0]), static_cast<float>(lo[1]), static_cast<float>(lo[2])};
+    const float hif[3] = {static_cast<float>(hi[0]), static_cast<float>(hi[1]), static_cast<float>(hi[2])};
+    const float Rf = static_cast<float>(R) * 1.0001f;
+    const int x0 = max(qcell(lof[0] - Rf, tg.ox, tg.inv_h), 0), x1 = min(qcell(hif[0] + Rf, tg.ox, tg.inv_h), tg.nx - 1);
+    const int y0 = max(qcell(lof[1] - Rf, tg.oy, tg.inv_h), 0), y1 = min(qcell(hif[1] + Rf, tg.oy, tg.inv_h), tg.ny - 1);
+    const int z0 = max(qcell(lof[2] - Rf, tg.oz, tg.inv_h), 0), z1 = min(qcell(hif[2] + Rf, tg.oz, tg.inv_h), tg.nz - 1);
+    int nc = 0;
+    bool ovf = false;
+    if (x0 <= x1 && y0 <= y1 && z0 <= z1) {
+      const int nyr = y1 - y0 + 1, nrows = (z1 - z0 + 1) * nyr;
+      for (int r0 = 0; r0 < nrows && !ovf; r0 += 64) {
+        const int r = r0 + lane;
+        uint32_t a = 0, cnt = 0;
+        if (r < nrows) {
+          const int z = z0 + r / nyr, y = y0 + r % nyr;
+          const float zl = tg.oz + static_cast<float>(z) * tg.h, yl = tg.oy + static_cast<float>(y) * tg.h;
+          const float gz = fmaxf(fmaxf(lof[2] - (zl + tg.h), zl - hif[2]) - tg.slop, 0.f);
+          const float gy = fmaxf(fmaxf(lof[1] - (yl + tg.h), yl - hif[1]) - tg.slop, 0.f);
+          if (gy * gy + gz * gz <= R2f) {
+            const uint32_t row = (static_cast<uint32_t>(z) * static_cast<uint32_t>(tg.ny) + static_cast<uint32_t>(y)) *
+                                 static_cast<uint32_t>(tg.nx);
+            a = tg.cell_start[row + x0];
+            cnt = tg.cell_start[row + x1 + 1] - a;
+          }
+        }
+        uint32_t inc = cnt;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+          const uint32_t u = __shfl_up(inc, off, 64);
+          if (lane >= off) inc += u;
+        }
+        const uint32_t tot = __builtin_amdgcn_readlane(inc, 63);
+        rowa[wid][lane] = a;
+        rowp[wid][lane] = inc - cnt;
+        lds_wave_sync();
+        for (uint32_t t0 = 0; t0 < tot && !ovf; t0 += 256) {
+          float4 pt[4];
+          uint32_t pj[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const uint32_t tt = t0 + static_cast<uint32_t>(lane + 64 * u);
+            uint32_t j = 0;
+            if (tt < tot) {
+              int lo_r = 0, hi_r = 63;  // the last row whose exclusive prefix is <= tt
+              while (lo_r < hi_r) {
+                const int mid = (lo_r + hi_r + 1) >> 1;
+                if (rowp[wid][mid] <= tt) lo_r = mid; else hi_r = mid - 1;
+              }
+              j = rowa[wid][lo_r] + (tt - rowp[wid][lo_r]);
+            }
+            pj[u] = j;
+            pt[u] = tg.pts[j];
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const uint32_t tt = t0 + static_cast<uint32_t>(lane + 64 * u);
+            const float gx = fmaxf(fmaxf(lof[0] - pt[u].x, pt[u].x - hif[0]), 0.f);
+            const float gy = fmaxf(fmaxf(lof[1] - pt[u].y, pt[u].y - hif[1]), 0.f);
+            const float gz = fmaxf(fmaxf(lof[2] - pt[u].z, pt[u].z - hif[2]), 0.f);
+            const bool keep = tt < tot && gx * gx + gy * gy + gz * gz <= R2f;
+            const unsigned long long m = __builtin_amdgcn_ballot_w64(keep);
+            const int o = static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<unsigned int>(m >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo(static_cast<unsigned int>(m), 0u)));
+            if (keep && nc + o < kVlCand) {
+              cand[wid][nc + o] = pt[u];
+              cpos[wid][nc + o] = pj[u];
+            }
+            nc += __builtin_popcountll(m);
+          }
+          if (nc > kVlCand) ovf = true;
+        }
+        lds_wave_sync();  // rowa / rowp are rewritten by the next batch of rows
+      }
+    }
+    if (ovf || nc == 0) {
+      if (lane == 0) v.cell[ci] = ovf ? kVlOverflow : kVlReject;
+      continue;
+    }
+    lds_wave_sync();
+    // anchors: the nearest candidate of each grown corner (box-centred float coordinates suffice:
+    // any real point is a valid anchor) and the centre's 1-NN
+    unsigned long long ak[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) ak[c] = ~0ull;
+    const float cf[3] = {static_cast<float>(ctr[0]), static_cast<float>(ctr[1]), static_cast<float>(ctr[2])};
+    const float hf[3] = {static_cast<float>(hx[0]), static_cast<float>(hx[1]), static_cast<float>(hx[2])};
+    for (int kq = lane; kq < nc; kq += 64) {
+      const float4 tp = cand[wid][kq];
+      const float tx = tp.x - cf[0], ty = tp.y - cf[1], tz = tp.z - cf[2];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const float dx = ((c & 1) ? hf[0] : -hf[0]) - tx, dy = ((c & 2) ? hf[1] : -hf[1]) - ty,
+                    dz = ((c & 4) ? hf[2] : -hf[2]) - tz;
+        const float d2 = dx * dx + dy * dy + dz * dz;
+        const unsigned long long key = (static_cast<unsigned long long>(__float_as_uint(d2)) << 32) |
+                                       static_cast<unsigned int>(kq);
+        ak[c] = key < ak[c] ? key : ak[c];
+      }
+    }
+    double an[9][3];
+    an[0][0] = pc3[0] - ctr[0];
+    an[0][1] = pc3[1] - ctr[1];
+    an[0][2] = pc3[2] - ctr[2];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const unsigned long long m = wave_min_u64(ak[c]);
+      const int kq = static_cast<int>(static_cast<unsigned int>(m));
+      const float4 ap = cand[wid][kq];
+      an[1 + c][0] = static_cast<double>(ap.x) - ctr[0];
+      an[1 + c][1] = static_cast<double>(ap.y) - ctr[1];
+      an[1 + c][2] = static_cast<double>(ap.z) - ctr[2];
+    }
+    double an2[9];
+#pragma unroll
+    for (int a = 0; a < 9; ++a) an2[a] = an[a][0] * an[a][0] + an[a][1] * an[a][1] + an[a][2] * an[a][2];
+    // affine dominance over the grown box (closed form of the minimum over its corners)
+    uint32_t keepm = 0;
+    for (int i = 0; i < kVlCand / 64; ++i) {
+      const int kq = lane + 64 * i;
+      if (kq >= nc) break;
+      const float4 tp = cand[wid][kq];
+      const double t3[3] = {static_cast<double>(tp.x) - ctr[0], static_cast<double>(tp.y) - ctr[1],
+                            static_cast<double>(tp.z) - ctr[2]};
+      double M2 = 0.0, tt = 0.0;
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        const double e = fabs(t3[d]) + hx[d];
+        M2 += e * e;
+        tt += t3[d] * t3[d];
+      }
+      const double margin = 1e-5 * M2 + 1e-15;
+      bool dom = false;
+#pragma unroll
+      for (int a = 0; a < 9; ++a) {
+        const double fmin = tt - an2[a] - 2.0 * (hx[0] * fabs(an[a][0] - t3[0]) + hx[1] * fabs(an[a][1] - t3[1]) +
+                                                 hx[2] * fabs(an[a][2] - t3[2]));
+        dom = dom || fmin > margin;
+      }
+      if (!dom) keepm |= 1u << i;
+    }
+    unsigned int cntl = static_cast<unsigned int>(__builtin_popcount(keepm));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cntl += __shfl_xor(cntl, o, 64);
+    cntl = __builtin_amdgcn_readfirstlane(cntl);
+    if (cntl > static_cast<unsigned int>(kVlMaxList)) {
+      if (lane == 0) v.cell[ci] = kVlOverflow;
+      continue;
+    }
+    unsigned int off = 0;
+    if (lane == 0) off = atomicAdd(&v.ctr[0], cntl);
+    off = __builtin_amdgcn_readfirstlane(off);
+    if (off + cntl > v.pool_cap) {
+      if (lane == 0) v.cell[ci] = kVlOverflow;
+      continue;
+    }
+    unsigned int run = 0;
+    for (int i = 0; i < kVlCand / 64; ++i) {
+      const bool b = (keepm >> i) & 1u;
+      const unsigned long long m = __builtin_amdgcn_ballot_w64(b);
+      if (b) {
+        const unsigned int o = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned int>(m >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo(static_cast<unsigned int>(m), 0u));
+        v.pool[off + run + o] = cand[wid][lane + 64 * i];
+        v.pool_pos[off + run + o] = cpos[wid][lane + 64 * i];
+      }
+      run += static_cast<unsigned int>(__builtin_popcountll(m));
+    }
+    if (lane == 0) v.cell[ci] = (off << 6) | cntl;
+    lds_wave_sync();  // cand / cpos are rewritten for the wave's next cell
+  }
+}
+
+// the sweep's queries without a list: the exact per-lane search, seeded as in correspond_kernel
+__global__ __launch_bounds__(256) void vl_fallback_kernel(GridView tg, VListView v, const float4* __restrict__ src,
+                                                          size_t p0, Xf34 T, double thr, int seeded,
+                                                          uint32_t* __restrict__ nn_pos, uint32_t* __restrict__ flags) {
+  const unsigned int n = v.ctr[2];
+  for (unsigned int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t k = v.pend[i];
+    const float4 s = src[p0 + k];
+    float qx, qy, qz;
+    xform(T, s.x, s.y, s.z, qx, qy, qz);
+    NnVisitor vis;
+    vis.init(qx, qy, qz, thr);
+    seed_query(tg, seeded, seeded ? nn_pos[k] : 0xffffffffu, qx, qy, qz, vis);
+    if (vis.best != ~0ull) box_search(tg, qx, qy, qz, vis);
+    else ring_search(tg, qx, qy, qz, vis);
+    const bool ok = vis.best != ~0ull &&
+                    static_cast<double>(__uint_as_float(static_cast<uint32_t>(vis.best >> 32))) < thr;
+    nn_pos[k] = ok ? vis.pos : 0xffffffffu;
+    flags[k] = ok ? 1u : 0u;
+  }
+}
+
+// diagnostics: [0] cells listed [1] list entries [2] reject [3] overflow [4] requested [5] not built,
+// [8 + L] cells with list length L (L < 56)
+__global__ void vl_stats_kernel(const uint32_t* __restrict__ cell, size_t n, unsigned long long* out) {
+  for (size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<size_t>(gridDim.x) * blockDim.x) {
+    const uint32_t c = cell[i];
+    if (c == kVlNotBuilt) continue;  // the common case: no atomics
+    if (c < kVlSpecial) {
+      atomicAdd(&out[0], 1ull);
+      atomicAdd(&out[1], static_cast<unsigned long long>(c & 63u));
+      atomicAdd(&out[8 + min(c & 63u, 55u)], 1ull);
+    } else {
+      atomicAdd(&out[c == kVlReject ? 2 : c == kVlOverflow ? 3 : 4], 1ull);
+    }
+  }
+}
+
 #if MGICP_CORR_PHASES
 hipError_t corr_phase_take(unsigned long long out[24]) {
   hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_corr_phase), 24 * sizeof(unsigned long long));
@@ -3069,6 +3444,30 @@ hipError_t launch_knn_cov(const GridView& g, int k, double eps, size_t p0, size_
 }
 
 bool knn_logged_enabled() { return knn_two_phase(); }
+
+hipError_t launch_vl_sweep(const GridView& tgt, const VListView& vl, const float4* src, size_t p0, size_t p1,
+                           Xf34 T, double thr, int seeded, uint32_t* nn_pos, uint32_t* flags,
+                           const uint32_t* qperm, int cus, hipStream_t s) {
+  if (p1 <= p0) return hipSuccess;
+  hipError_t e = hipMemsetAsync(vl.ctr + 1, 0, 2 * sizeof(unsigned int), s);
+  if (e != hipSuccess) return e;
+  vl_query_kernel<<<nblk(p1 - p0), 256, 0, s>>>(tgt, vl, src, p0, p1, T, thr, nn_pos, flags, qperm);
+  // requested cells: the centre's 1-NN within the gate + the grown cell's half diagonal, then the lists
+  const double hd = std::sqrt(3.0) * (0.5 * static_cast<double>(vl.c) + static_cast<double>(vl.es));
+  const double rc = vl.gate * (1.0 + 1e-5) + 1e-9 + hd;
+  const unsigned g = static_cast<unsigned>(std::max(cus, 1));
+  vl_centre_kernel<<<4 * g, 256, 0, s>>>(tgt, vl, rc * rc * (1.0 + 1e-5));
+  vl_build_kernel<<<4 * g, 256, 0, s>>>(tgt, vl);
+  vl_fallback_kernel<<<8 * g, 256, 0, s>>>(tgt, vl, src, p0, T, thr, seeded, nn_pos, flags);
+  return hipGetLastError();
+}
+
+hipError_t launch_vl_stats(const VListView& vl, size_t ncells, unsigned long long* out, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(out, 0, 64 * sizeof(unsigned long long), s);
+  if (e != hipSuccess) return e;
+  vl_stats_kernel<<<2048, 256, 0, s>>>(vl.cell, ncells, out);
+  return hipGetLastError();
+}
 
 hipError_t launch_correspond(const GridView& tgt, const float4* src, size_t p0, size_t p1, Xf34 T,
                              double thr, int seeded, uint32_t* nn_pos, uint32_t* flags,

@@ -298,6 +298,14 @@ class GICPEngine:
         return {"ms": ms.value, "passes": p, "launches": int(launches.value),
                 "ms_per_pass": ms.value / p if p else None}
 
+    VLIST_STATS = ("requested", "pending", "lists", "entries", "reject", "overflow", "pool_used", "cells")
+
+    def vlist_stats(self) -> dict:
+        """The target's 1-NN cell lists (mgicp_debug_vlist_stats)."""
+        out = (ctypes.c_longlong * 8)()
+        self._check(self._lib.mgicp_debug_vlist_stats(self._h, out), "vlist_stats")
+        return {k: int(out[i]) for i, k in enumerate(self.VLIST_STATS)}
+
     # -- introspection (parity tests, profiling) ----------------------------------------------
     def debug_covariances(self, which: str, n: int) -> np.ndarray:
         out = np.zeros((n, 6), np.float64)
