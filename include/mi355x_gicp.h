@@ -244,6 +244,12 @@ int mgicp_debug_pass_stats(mgicp_ctx* ctx, long long out[8]);
  * read.  out_ms / out_passes = the in-align time of one objective pass. */
 int mgicp_debug_server_time(mgicp_ctx* ctx, double* out_ms, long long* out_passes, long long* out_launches,
                             int reset);
+/* the r-th of N target-covariance slices exactly as rank r of an N-rank context computes it before
+ * the all-gather (points [r cnt, min(n, (r + 1) cnt)), cnt = ceil(n / N), arrays of N cnt entries):
+ * 6 values per point of the slice, in grid-sorted order, into out_c6 (c00 c01 c02 c11 c12 c22);
+ * returns the slice's point count.  Assembled in rank order the N slices are the all-gathered arrays (tests; the cached target
+ * covariances are recomputed by the next align). */
+int mgicp_debug_target_cov_slice(mgicp_ctx* ctx, int nranks, int rank, double* out_c6);
 /* the target's 1-NN cell lists (DESIGN.md "1-NN cell lists"): out[0] cells requested and out[1]
  * queries left to the exact per-lane search by the last sweep, out[2] cells with a list, out[3] list
  * entries, out[4] reject cells, out[5] overflow cells, out[6] pool entries used, out[7] fine-grid

@@ -94,6 +94,7 @@ _SIGNATURES = {
     "mgicp_debug_pass_stats": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_longlong)]),
     "mgicp_debug_server_time": (ctypes.c_int, [_P, _DP, ctypes.POINTER(ctypes.c_longlong),
                                                ctypes.POINTER(ctypes.c_longlong), ctypes.c_int]),
+    "mgicp_debug_target_cov_slice": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, _DP]),
     "mgicp_debug_vlist_stats": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_longlong)]),
     "mgicp_debug_covariances": (ctypes.c_int, [_P, ctypes.c_int, _DP]),
     "mgicp_debug_correspondences": (ctypes.c_int, [_P, _FP, _IP, _DP]),

@@ -355,6 +355,8 @@ struct mgicp_ctx {
   int srv_cus = 0;                      // env MGICP_SRV_CUS: cap on the server's blocks (0 = every CU)
   int srv_waves = 4;                    // server shape: 4 or 8 waves per CU (env MGICP_SRV_WAVES)
   int stall_pass = -1;                  // env MGICP_SRV_STALL_PASS (tests): a server block withholds this pass
+  int quit_pass = -1;                   // env MGICP_DEBUG_QUIT_PASS (tests): the host gives up at this pass index
+                                        // with MGICP_E_COMM (a rank that dies mid-align, seen from the others)
   bool corr_wave = true;                // wave-uniform 1-NN sweeps (env MGICP_CORR_WAVE)
   int corr_lds_pts = -1;                // small-ball waves: union-box cell bounds in LDS (-1), + points when <= N fit (N > 0), off (0) (MGICP_CORR_LDS_PTS)
   int corr_split = 0;                   // waves of the wave sweep with <= this many stragglers hand them to a kernel of
@@ -1526,6 +1528,8 @@ struct DeviceFunctor {
     // stamps >= 2^31 belong to mgicp_debug_pass_bench's timing form).  At the wrap every stamped
     // buffer is cleared and the count restarts at 1, so parity buffers keep alternating.
     if (ctx->pass_idx + 1 >= 0x80000000u && (rc = reset_stamps(ctx))) return rc;
+    if (ctx->quit_pass >= 0 && ctx->pass_idx + 1 >= static_cast<unsigned int>(ctx->quit_pass))
+      return fail(ctx, MGICP_E_COMM, "MGICP_DEBUG_QUIT_PASS: this rank stops publishing its rows");
     const unsigned long long seq = ++ctx->pass_seq;
     const unsigned int rstamp = ++ctx->pass_idx;
     // single GPU: the finishing wave writes the totals straight into mapped pinned host memory.
@@ -1881,6 +1885,7 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
   if (const char* sp = std::getenv("MGICP_SPIN_PAUSE")) ctx->spin_pause = std::atoi(sp) != 0;
   if (const char* sc = std::getenv("MGICP_SRV_CUS")) ctx->srv_cus = std::max(0, std::atoi(sc));
   if (const char* sp = std::getenv("MGICP_SRV_STALL_PASS")) ctx->stall_pass = std::atoi(sp);
+  if (const char* qp = std::getenv("MGICP_DEBUG_QUIT_PASS")) ctx->quit_pass = std::atoi(qp);
   if (const char* dl = std::getenv("MGICP_ROW_DEADLINE_MS")) {
     const double v = std::atof(dl);
     if (v > 0) ctx->row_deadline_ms = v;
@@ -2583,6 +2588,35 @@ int mgicp_debug_server_time(mgicp_ctx* ctx, double* out_ms, long long* out_passe
     ctx->srv_time_passes = ctx->srv_time_launches = 0;
   }
   return MGICP_OK;
+}
+
+int mgicp_debug_target_cov_slice(mgicp_ctx* ctx, int nranks, int rank, double* out_c6) {
+  if (!ctx || !out_c6 || nranks < 1 || rank < 0 || rank >= nranks) return MGICP_E_INVALID;
+  HIPCK(hipSetDevice(ctx->device));
+  int rc = prepare(ctx, false);
+  if (rc) return rc;
+  Cloud& t = ctx->tgt;
+  const size_t N = static_cast<size_t>(nranks), r = static_cast<size_t>(rank);
+  const size_t cnt = (t.n + N - 1) / N;
+  const size_t a = std::min(t.n, r * cnt), b = std::min(t.n, (r + 1) * cnt);
+  // target_cov's slice call, verbatim: the same range, the same N * cnt array layout
+  if ((rc = compute_cov(ctx, t, a, b, N * cnt))) return rc;
+  t.have_cov = false;  // only a slice is current: the next align recomputes the target's covariances
+  const size_t st = t.cov_stride, m = b - a;
+  std::vector<double2> h(3 * std::max<size_t>(m, 1));
+  if (m) {
+    const Cov3 c = t.cov3();
+    HIPCK(hipMemcpyAsync(h.data(), c.a + a, m * sizeof(double2), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCK(hipMemcpyAsync(h.data() + m, c.b + a, m * sizeof(double2), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCK(hipMemcpyAsync(h.data() + 2 * m, c.c + a, m * sizeof(double2), hipMemcpyDeviceToHost, ctx->stream));
+  }
+  (void)st;
+  if ((rc = sync(ctx))) return rc;
+  for (size_t i = 0; i < m; ++i) {  // grid-sorted order, as the arrays hold them
+    double* o = out_c6 + 6 * i;
+    o[0] = h[i].x; o[1] = h[i].y; o[2] = h[m + i].x; o[3] = h[m + i].y; o[4] = h[2 * m + i].x; o[5] = h[2 * m + i].y;
+  }
+  return static_cast<int>(m);
 }
 
 int mgicp_debug_vlist_stats(mgicp_ctx* ctx, long long out[8]) {

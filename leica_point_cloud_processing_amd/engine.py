@@ -298,6 +298,14 @@ class GICPEngine:
         return {"ms": ms.value, "passes": p, "launches": int(launches.value),
                 "ms_per_pass": ms.value / p if p else None}
 
+    def debug_target_cov_slice(self, nranks: int, rank: int, n_target: int) -> np.ndarray:
+        """slice `rank` of `nranks` of the target covariances as an N-rank context computes it before
+        its all-gather (mgicp_debug_target_cov_slice)"""
+        out = np.zeros((max(1, -(-n_target // nranks)), 6), np.float64)
+        cnt = self._check(self._lib.mgicp_debug_target_cov_slice(self._h, int(nranks), int(rank), _dp(out)),
+                          "debug_target_cov_slice")
+        return out[:cnt].copy()
+
     VLIST_STATS = ("requested", "pending", "lists", "entries", "reject", "overflow", "pool_used", "cells")
 
     def vlist_stats(self) -> dict:

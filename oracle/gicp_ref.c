@@ -372,6 +372,7 @@ void ref_default_params(ref_params* p) {
     p->threads = 1;
     p->objective = 0;
     p->solver = 0;
+    p->variant = 0;
 }
 
 ref_gicp* ref_create(const ref_params* p) {
@@ -1053,13 +1054,14 @@ static void check_extremum(const double c[4], double x, double* xmin, double* fm
 }
 
 static double b_interpolate(double a, double fa, double fpa, double b, double fb, double fpb,
-                            double xmin, double xmax, int order) {
+                            double xmin, double xmax, int order, int variant) {
     double y, alpha, ymin, ymax, fmin;
     ymin = (xmin - a) / (b - a);
     ymax = (xmax - a) / (b - a);
     if (ymin > ymax) { double t = ymin; ymin = ymax; ymax = t; }
     /* PCL 1.8.1 tests !(fpb != fpa) here (GSL: GSL_IS_REAL(fpb)); restated as published */
-    if (order > 2 && !(fpb != fpa) && fpb != INFINITY) {
+    const int cubic = (variant & 2) ? isfinite(fpb) : (!(fpb != fpa) && fpb != INFINITY);
+    if (order > 2 && cubic) {
         fpa = fpa * (b - a);
         fpb = fpb * (b - a);
         double eta = 3 * (fb - fa) - 2 * fpa - fpb;
@@ -1091,7 +1093,7 @@ static double b_interpolate(double a, double fa, double fpa, double b, double fb
         y = ymin;
         fmin = fl;
         if (fh < fmin) { y = ymax; fmin = fh; }
-        if (c > a) { /* PCL 1.8.1 compares against a (GSL: c > 0); restated as published */
+        if ((variant & 4) ? c > 0 : c > a) { /* PCL 1.8.1 compares against a (GSL: c > 0); restated as published */
             double z = -fpa / c;
             if (z > ymin && z < ymax) {
                 double f = fa + z * (fpa + z * (fb - fa - fpa));
@@ -1137,7 +1139,7 @@ static int b_line_search(bfgs_t* b, double rho, double sigma, double tau1, doubl
             double lower = alpha + delta;
             double upper = alpha + tau1 * delta;
             alpha_next = b_interpolate(alpha_prev, falpha_prev, fpalpha_prev, alpha, falpha,
-                                       fpalpha, lower, upper, order);
+                                       fpalpha, lower, upper, order, b->g->prm.variant);
         }
         alpha_prev = alpha;
         falpha_prev = falpha;
@@ -1149,10 +1151,10 @@ static int b_line_search(bfgs_t* b, double rho, double sigma, double tau1, doubl
         {
             double lower = a + tau2 * delta;
             double upper = bb - tau3 * delta;
-            alpha = b_interpolate(a, fa, fpa, bb, fb, fpb, lower, upper, order);
+            alpha = b_interpolate(a, fa, fpa, bb, fb, fpb, lower, upper, order, b->g->prm.variant);
         }
         falpha = b_apply_f(b, alpha);
-        if ((a - alpha) * fpa <= DBL_EPSILON) return BFGS_NO_PROGRESS;
+        if ((a - alpha) * fpa <= ((b->g->prm.variant & 32) ? 0.0 : DBL_EPSILON)) return BFGS_NO_PROGRESS;
         if (falpha > f0 + rho * alpha * fp0 || falpha >= fa) {
             bb = alpha; fb = falpha; fpb = NAN;
         } else {
@@ -1260,8 +1262,10 @@ static int estimate_bfgs(ref_gicp* g, float T[4][4]) {
     memset(&b, 0, sizeof(b));
     b.g = g;
     b.sigma = 0.01; b.rho = 0.01; b.tau1 = 9; b.tau2 = 0.05; b.tau3 = 0.5; b.order = 3;
-    b.step_size = 1; b.bracket_iters = 100; b.section_iters = 100;
-    const double gradient_tol = 1e-2;
+    b.step_size = (g->prm.variant & 16) ? 0.1 : 1;
+    b.bracket_iters = (g->prm.variant & 8) ? 20 : 100;
+    b.section_iters = (g->prm.variant & 8) ? 20 : 100;
+    const double gradient_tol = (g->prm.variant & 1) ? g->prm.gicp_epsilon : 1e-2;
     int inner = 0;
     int result = b_minimize_init(&b, x);
     result = BFGS_RUNNING;

@@ -42,6 +42,15 @@ typedef struct {
                                       engine's MGICP_OBJ_MOMENTS mode) */
     int    solver;                 /* 0: PCL BFGS (default); 1: Gauss-Newton on the moment form
                                       (checker for the engine's MGICP_SOLVER_GN; not in PCL) */
+    int    variant;                /* 0 (default): the restatement as published.  Bits select one
+                                      plausible alternative reading of a bfgs.h / gicp.hpp choice that
+                                      was restated without its source (DESIGN.md "Oracle uncertainty
+                                      ledger"): 1 inner gradient test at gicp_epsilon_ (1e-3) instead of
+                                      1e-2; 2 cubic branch taken on a finite fpb (GSL GSL_IS_REAL) instead
+                                      of !(fpb != fpa); 4 quadratic curvature test c > 0 (GSL) instead of
+                                      c > a; 8 bracket / section caps 20 instead of 100; 16 first trial
+                                      step 0.1 instead of 1; 32 line-search no-progress test against 0
+                                      instead of DBL_EPSILON */
 } ref_params;
 
 typedef struct {

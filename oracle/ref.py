@@ -28,6 +28,7 @@ class RefParams(ctypes.Structure):
         ("threads", ctypes.c_int),
         ("objective", ctypes.c_int),
         ("solver", ctypes.c_int),
+        ("variant", ctypes.c_int),
     ]
 
 
@@ -115,7 +116,7 @@ class RefGICP:
 
     def __init__(self, max_iterations=100, transformation_epsilon=4e-3, rotation_epsilon=2e-3,
                  max_corr_dist=0.04, gicp_epsilon=1e-3, k=20, max_inner_iterations=20,
-                 fixed_iterations=False, threads=1, objective=0, solver=0):
+                 fixed_iterations=False, threads=1, objective=0, solver=0, variant=0):
         self.lib = load()
         self.p = RefParams()
         self.lib.ref_default_params(ctypes.byref(self.p))
@@ -130,6 +131,7 @@ class RefGICP:
         self.p.threads = threads
         self.p.objective = objective
         self.p.solver = solver
+        self.p.variant = variant
         self.h = self.lib.ref_create(ctypes.byref(self.p))
         self.ns = 0
 

@@ -610,6 +610,100 @@ def test_server_in_align_time_counts_every_pass():
     assert 0 < t["ms_per_pass"] < loop_ms, t
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_target_cov_slices_assemble_to_unsharded(part_small, world):
+    """the all-gather's data path without RCCL -- the N target-covariance slices
+    that ranks 0..N-1 compute before their in-place ncclAllGather (target_cov: points [r cnt,
+    (r + 1) cnt) of arrays of N cnt entries), assembled in rank order, are the single-rank target
+    covariances bit for bit."""
+    from leica_point_cloud_processing_amd.engine import GICPEngine
+
+    scan, cad, _ = part_small
+    e = GICPEngine()
+    e.set_source_xyz(scan)
+    e.set_target_xyz(cad)
+    full = e.debug_target_cov_slice(1, 0, len(cad))
+    assert full.shape == (len(cad), 6)
+    parts = [e.debug_target_cov_slice(world, r, len(cad)) for r in range(world)]
+    cnt = -(-len(cad) // world)
+    assert [len(p) for p in parts] == [max(0, min(len(cad), (r + 1) * cnt) - r * cnt) for r in range(world)]
+    asm = np.concatenate(parts)
+    assert np.array_equal(asm.view(np.int64), full.view(np.int64))
+    # and the cached covariances the aligns use are recomputed afterwards (the slice left them stale)
+    T1 = e.align()
+    f = GICPEngine()
+    f.set_source_xyz(scan)
+    f.set_target_xyz(cad)
+    np.testing.assert_array_equal(T1, f.align())
+    e.close()
+    f.close()
+
+
+def _quit_rank(name, world, rank, n, env, q):
+    """one rank of the rank-failure test: rank 1 stops publishing at a pass (MGICP_DEBUG_QUIT_PASS)"""
+    import time as _t
+
+    try:
+        os.environ.update(env)
+        from leica_point_cloud_processing_amd import _lib, synth
+        from leica_point_cloud_processing_amd.engine import GICPEngine
+
+        scan, cad, _ = synth.scan_vs_cad(n, n)
+        e = GICPEngine(device=0)
+        e.comm_init(world, rank, None)
+        e.attach_shm(name, n)
+        e.set_source_xyz(scan)
+        e.set_target_xyz(cad)
+        t0 = _t.perf_counter()
+        err = None
+        try:
+            e.align()
+        except _lib.MgicpError as exc:
+            err = (exc.code, str(exc))
+        dt = _t.perf_counter() - t0
+        st = e.pass_stats()
+        t1 = _t.perf_counter()
+        e.close()  # must not wait on a stuck server
+        q.put((rank, err, dt, st, _t.perf_counter() - t1))
+    except Exception as exc:  # noqa: BLE001
+        q.put((rank, repr(exc), None, None, None))
+
+
+@pytest.mark.gpu
+def test_shm_rank_quits_mid_align_others_fail_fast():
+    """a rank that stops publishing its super rows mid-align (MGICP_DEBUG_QUIT_PASS
+    on rank 1: its host gives up at pass 5, cancels its server and closes).  The surviving rank
+    returns MGICP_E_COMM within the remote deadline (3 s here) -- no hang -- and its context closes at
+    once (its server was cancelled, not left waiting for commands)."""
+    from leica_point_cloud_processing_amd import _lib
+
+    n = 200_000
+    name = f"/mgicp_quit_{os.getpid()}"
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = []
+    for r in range(2):
+        env = {"MGICP_SRV_CUS": "80", "MGICP_REMOTE_DEADLINE_S": "3"}
+        if r == 1:
+            env["MGICP_DEBUG_QUIT_PASS"] = "5"
+        procs.append(ctx.Process(target=_quit_rank, args=(name, 2, r, n, env, q)))
+    for p in procs:
+        p.start()
+    got = sorted((q.get(timeout=240) for _ in procs), key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (r0, err0, dt0, st0, close0), (r1, err1, dt1, st1, close1) = got
+    assert not isinstance(err0, str) and err0 is not None, got
+    assert err0[0] == _lib.MGICP_E_COMM, err0
+    assert err1 is not None and err1[0] == _lib.MGICP_E_COMM, err1
+    assert dt0 < 3.0 + 30.0, dt0  # the remote deadline, not the 120 s default or a hang
+    assert close0 < 5.0 and close1 < 5.0, (close0, close1)
+    assert st0["server_passes"] >= 4, st0
+    assert not os.path.exists("/dev/shm" + name)
+
+
 def _shm_rank(name, world, rank, n, solver, env, q):
     """One rank of an RCCL-free multi-process run on ONE device: detached shard + shared rows."""
     try:
