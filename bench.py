@@ -349,6 +349,9 @@ def main():
             first = dict(eng.last_result)
     iters_per_align = eng.last_result["iterations"]
     kt_cov = eng.kernel_times()  # profiling is off until now; filled below
+    # the target's 1-NN cell lists after the warmup aligns (built by their sweeps; the timed aligns
+    # then find every cell they query listed or rejected -- DESIGN.md "1-NN cell lists")
+    vlist = eng.vlist_stats()
 
     # timed region: K full align loops with no per-launch instrumentation (pre-launched, gated
     # objective passes on).  align() is host-synchronous (it returns with T on the host after its
@@ -680,6 +683,7 @@ def main():
         "n_corr": result["n_corr"],
         "n_rejected_last_sweep": args.n_source - result["n_corr"] if world == 1 else None,
         "objective_passes_per_align": result["n_evals"],
+        "vlist": vlist,
         "ms_to_converge_first": round(first["ms_total"], 3),
         "ms_create": round(ms_create, 3),
         "ms_to_converge_new_clouds_warm_process": new_clouds,
