@@ -415,6 +415,10 @@ struct mgicp_ctx {
   DevBuf<uint32_t> vl_cell, vl_pool_pos, vl_build, vl_bcentre, vl_pend;
   DevBuf<float4> vl_pool;
   DevBuf<unsigned int> vl_ctr;
+  uint32_t vl_epoch = 0;              // sweeps run over the current lists (a cell is built on its 2nd sweep)
+  bool vl_eager = false;              // env MGICP_VLIST_EAGER: build a cell at its first query
+  DevBuf<float4> qsrc;                // the shard's (guess-applied) points in query order, w = shard position
+  const float4* qsrc_for = nullptr;   // the d_out they were taken from (nullptr: stale)
   // multi-GPU
   int nranks = 1, rank = 0;
   ncclComm_t comm = nullptr;
@@ -837,6 +841,7 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
   cl.dirty = false;
   cl.have_cov = false;
   if (&cl == &ctx->tgt) ctx->vl_valid = false;  // the 1-NN cell lists index the old target
+  if (&cl == &ctx->src) ctx->qsrc_for = nullptr;  // the query-order copy holds the old source
   if (&cl == &ctx->src || &cl == &ctx->tgt) {  // sorted positions changed
     ctx->have_corr = false;
     ctx->seed_valid = false;
@@ -1273,6 +1278,7 @@ int set_output(mgicp_ctx* ctx, const Mat4& G) {
     HIPCK(ctx->src_out.reserve(ctx->src.n));
     HIPCK(launch_xform_points(ctx->src.pts.p, ctx->src.n, G.xf(), ctx->src_out.p, ctx->stream));
     ctx->d_out = ctx->src_out.p;
+    ctx->qsrc_for = nullptr;  // src_out was rewritten
     // bbox of the transformed cloud (the Gauss-Newton expansion centre)
     const size_t n = ctx->src.n;
     const int nb = static_cast<int>(std::min<size_t>((n + 255) / 256, 1024));
@@ -1368,7 +1374,8 @@ int vl_prepare(mgicp_ctx* ctx) {
     v.nz = nd[2];
     HIPCK(ctx->vl_cell.reserve(nc));
     HIPCK(hipMemsetAsync(ctx->vl_cell.p, 0xff, nc * sizeof(uint32_t), ctx->stream));
-    const size_t cap = std::min<size_t>((size_t(1) << 26) - 1, std::max<size_t>(size_t(1) << 22, 16 * t.n));
+    // list starts are stored in units of 4 entries in 25 bits: at most 2^27 entries (20 bytes each)
+    const size_t cap = std::min<size_t>(size_t(1) << 27, std::max<size_t>(size_t(1) << 22, 32 * t.n));
     HIPCK(ctx->vl_pool.reserve(cap));
     HIPCK(ctx->vl_pool_pos.reserve(cap));
     HIPCK(ctx->vl_ctr.reserve(4));
@@ -1380,6 +1387,7 @@ int vl_prepare(mgicp_ctx* ctx) {
     v.ctr = ctx->vl_ctr.p;
     ctx->vl_ncells = nc;
     ctx->vl_valid = true;
+    ctx->vl_epoch = 0;
   }
   if (ctx->vl_off) return MGICP_OK;
   // per-sweep lists sized by the shard (one request / pending entry per query at most)
@@ -1391,6 +1399,18 @@ int vl_prepare(mgicp_ctx* ctx) {
   ctx->vl.bcentre = ctx->vl_bcentre.p;
   ctx->vl.build_cap = static_cast<uint32_t>(std::min(ctx->vl_build.cap, ctx->vl_ncells));
   ctx->vl.pend = ctx->vl_pend.p;
+  if (++ctx->vl_epoch >= 0x40000000u) {  // epochs wrap: every touched mark then reads as "earlier sweep"
+    ctx->vl_epoch = 1;
+  }
+  ctx->vl.epoch = ctx->vl_epoch;
+  ctx->vl.eager = ctx->vl_eager ? 1 : 0;
+  // the shard's points in query order (once per source cloud, shard and guess)
+  if (ctx->qsrc_for != ctx->d_out || !ctx->qperm_valid) {
+    const uint32_t* qp = query_perm(ctx);
+    HIPCK(ctx->qsrc.reserve(q));
+    HIPCK(launch_query_order_points(ctx->d_out, ctx->shard_p0(), ns, qp, ctx->qsrc.p, ctx->stream));
+    ctx->qsrc_for = ctx->qperm_valid ? ctx->d_out : nullptr;
+  }
   return MGICP_OK;
 }
 
@@ -1402,7 +1422,7 @@ hipError_t launch_sweep(mgicp_ctx* ctx, const Mat4& T, double thr, bool seeded, 
   const GridView& g = ctx->tgt.view;
   if (ctx->vlist && ctx->vl_valid && !ctx->vl_off)
     return launch_vl_sweep(g, ctx->vl, ctx->d_out, p0, p1, T.xf(), thr, seeded ? 1 : 0, ctx->prev_pos.p, ctx->flags.p,
-                           qp, ctx->cus, ctx->stream);
+                           ctx->qsrc.p, ctx->cus, ctx->stream);
   if (ctx->corr_wave && g.pairs) {
     const float rc = ctx->corr_rcap * g.h;
     void* work = nullptr;
@@ -1961,6 +1981,7 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
     if (f > 0.05f && f < 8.f) ctx->vlist_cell = f;
   }
   if (const char* vs = std::getenv("MGICP_VLIST_STATS")) ctx->vl_stats = std::atoi(vs) != 0;
+  if (const char* ve = std::getenv("MGICP_VLIST_EAGER")) ctx->vl_eager = std::atoi(ve) != 0;
   ctx->tgt.want_pairs = ctx->corr_wave;
   if (const char* cb = std::getenv("MGICP_CELL_BOXES")) ctx->tgt.want_boxes = std::atoi(cb) != 0;
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -2023,7 +2044,7 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   ctx->prev_pos.release(); ctx->flags.release(); ctx->cpos.release();
   ctx->nn_work.release(); ctx->nn_work_n.release();
   ctx->vl_cell.release(); ctx->vl_pool.release(); ctx->vl_pool_pos.release(); ctx->vl_ctr.release();
-  ctx->vl_build.release(); ctx->vl_bcentre.release(); ctx->vl_pend.release();
+  ctx->vl_build.release(); ctx->vl_bcentre.release(); ctx->vl_pend.release(); ctx->qsrc.release();
   ctx->tpart.release();
   ctx->tpart_n = 0;
   ctx->corr_f.release(); ctx->corr_d.release(); ctx->cscratch.release();
@@ -2520,6 +2541,7 @@ int mgicp_comm_init(mgicp_ctx* ctx, int nranks, int rank, const unsigned char id
   ctx->nranks = nranks;
   ctx->rank = rank;
   ctx->qperm_valid = false;
+  ctx->qsrc_for = nullptr;
   ctx->src.have_cov = false;
   ctx->have_corr = false;
   ctx->seed_valid = false;  // the shard (and its per-point match buffers) changes

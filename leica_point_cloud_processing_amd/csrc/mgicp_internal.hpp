@@ -149,12 +149,14 @@ size_t nn_work_bytes(size_t n);
 // below the gate -- a superset, pruned by the affine dominance test against 9 anchor points -- or
 // "reject" (no target point within the gate of the cell).  Lists are built the first time a sweep
 // queries the cell and persist until the target or the gate changes.
-constexpr uint32_t kVlNotBuilt = 0xFFFFFFFFu;  // no list yet (a query requests it)
+constexpr uint32_t kVlNotBuilt = 0xFFFFFFFFu;  // never queried
 constexpr uint32_t kVlRequested = 0xFFFFFFFEu; // queued for this sweep's build
 constexpr uint32_t kVlOverflow = 0xFFFFFFFDu;  // more than kVlMaxList entries / candidates / pool full
 constexpr uint32_t kVlReject = 0xFFFFFFFCu;    // no target point within the gate of the cell
-constexpr uint32_t kVlSpecial = 0xFFFFFFFCu;   // values >= this are states, below: (off << 6) | count
-constexpr int kVlMaxList = 63;
+constexpr uint32_t kVlTouched = 0x80000000u;   // | epoch: first queried in sweep `epoch` (built when queried
+                                               // again in a later sweep); values below: (off4 << 6) | count
+constexpr int kVlMaxList = 63;                 // entries per list (lists padded to a multiple of 4 with far
+                                               // sentinels; off4 = list start / 4, < 2^25)
 struct VListView {
   float ox, oy, oz;      // fine grid origin
   float c, inv_c;        // fine cell edge and its float reciprocal
@@ -170,13 +172,19 @@ struct VListView {
   uint32_t* bcentre;     // per requested cell: sorted position of the cell centre's 1-NN (or none)
   uint32_t build_cap;
   uint32_t* pend;        // shard-relative positions of this sweep's queries without a list
+  uint32_t epoch;        // this sweep's number (1 .. 2^30 - 1)
+  int eager;             // 1: build a cell's list at its first query (else at its first query in a later sweep)
 };
 // one sweep over the lists: listed queries answered at once, reject cells rejected, the others
 // queued (pend) and their cells requested; then the requested cells' lists are built and the
 // pending queries answered by the exact per-lane search (seeded like correspond_kernel)
 hipError_t launch_vl_sweep(const GridView& tgt, const VListView& vl, const float4* src, size_t p0, size_t p1,
                            Xf34 T, double thr, int seeded, uint32_t* nn_pos, uint32_t* flags,
-                           const uint32_t* qperm, int cus, hipStream_t s);
+                           const float4* qsrc /*the shard's points in query order, w = bits(shard position)*/,
+                           int cus, hipStream_t s);
+// qsrc[t] = src[p0 + qperm[t]] with w = bits(qperm[t]) (qperm nullable: identity)
+hipError_t launch_query_order_points(const float4* src, size_t p0, size_t n, const uint32_t* qperm, float4* qsrc,
+                                     hipStream_t s);
 // diagnostics (env MGICP_VLIST_STATS): per built cell list lengths histogram etc. into out[64]
 hipError_t launch_vl_stats(const VListView& vl, size_t ncells, unsigned long long* out /*device, 64*/, hipStream_t s);
 size_t     pair_count(size_t n);

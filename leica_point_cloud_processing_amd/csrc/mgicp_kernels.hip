@@ -1595,7 +1595,7 @@ __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_kernel(GridV
 // accepted queries, and a rejected query's list minimum is >= thr as well (every listed point is a
 // real point, no closer than the true 1-NN).  Queries outside the fine grid, or in a cell with no
 // target point within D(1 + 1e-5) + its half diagonal of the centre, are rejected.
-constexpr int kVlCand = 512;  // candidates a build wave keeps in LDS (more: the cell stays a fallback cell)
+constexpr int kVlCand = 1024;  // candidates a build wave keeps in LDS (more: the cell stays a fallback cell)
 
 __device__ __forceinline__ void vl_cell_xyz(const VListView& v, uint32_t ci, uint32_t& ix, uint32_t& iy, uint32_t& iz) {
   const uint32_t nx = static_cast<uint32_t>(v.nx), ny = static_cast<uint32_t>(v.ny);
@@ -1604,17 +1604,28 @@ __device__ __forceinline__ void vl_cell_xyz(const VListView& v, uint32_t ci, uin
   iz = ci / (nx * ny);
 }
 
-__global__ __launch_bounds__(256) void vl_query_kernel(GridView tg, VListView v, const float4* __restrict__ src,
-                                                       size_t p0, size_t p1, Xf34 T, double thr,
-                                                       uint32_t* __restrict__ nn_pos, uint32_t* __restrict__ flags,
-                                                       const uint32_t* __restrict__ qperm) {
+// the shard's points in the sweeps' query order (Morton), w = bits(shard position): the query kernel
+// reads them coalesced, one dependent load fewer
+__global__ void query_order_points_kernel(const float4* __restrict__ src, size_t p0, size_t n,
+                                          const uint32_t* __restrict__ qperm, float4* __restrict__ out) {
+  const size_t t = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const uint32_t k = qperm ? qperm[t] : static_cast<uint32_t>(t);
+  const float4 s = src[p0 + k];
+  out[t] = make_float4(s.x, s.y, s.z, __uint_as_float(k));
+}
+
+__global__ __launch_bounds__(256) void vl_query_kernel(VListView v, const float4* __restrict__ qsrc, size_t n, Xf34 T,
+                                                       double thr, uint32_t* __restrict__ nn_pos,
+                                                       uint32_t* __restrict__ flags) {
   const int lane = threadIdx.x & 63;
   const size_t t = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  const bool live = t < p1 - p0;
-  const uint32_t k = live ? (qperm ? qperm[t] : static_cast<uint32_t>(t)) : 0u;
+  const bool live = t < n;
   float qx = 0.f, qy = 0.f, qz = 0.f;
+  uint32_t k = 0;
   if (live) {
-    const float4 s = src[p0 + k];
+    const float4 s = qsrc[t];
+    k = __float_as_uint(s.w);
     xform(T, s.x, s.y, s.z, qx, qy, qz);
   }
   const int ix = qcell(qx, v.ox, v.inv_c), iy = qcell(qy, v.oy, v.inv_c), iz = qcell(qz, v.oz, v.inv_c);
@@ -1624,9 +1635,17 @@ __global__ __launch_bounds__(256) void vl_query_kernel(GridView tg, VListView v,
                                                                   static_cast<uint32_t>(v.ny) * static_cast<uint32_t>(iz))
                              : 0u;
   const uint32_t st = inside ? v.cell[ci] : kVlReject;
-  const bool pending = live && st >= kVlSpecial && st != kVlReject;
+  const bool pending = live && st >= kVlTouched && st != kVlReject;
+  // a cell's list is built when it is queried in a sweep after the one that first queried it (or at
+  // once, eager): cells a single sweep passes through cost one state word, not a build
   bool req = false;
-  if (pending && st == kVlNotBuilt) req = atomicCAS(&v.cell[ci], kVlNotBuilt, kVlRequested) == kVlNotBuilt;
+  const uint32_t mine = kVlTouched | v.epoch;
+  if (pending && st == kVlNotBuilt) {
+    if (v.eager) req = atomicCAS(&v.cell[ci], kVlNotBuilt, kVlRequested) == kVlNotBuilt;
+    else atomicCAS(&v.cell[ci], kVlNotBuilt, mine);
+  } else if (pending && st < kVlReject && st != mine) {  // touched in an earlier sweep
+    req = atomicCAS(&v.cell[ci], st, kVlRequested) == st;
+  }
   // the cell's build request and the query's place in the pending list: one atomic per wave each
   const unsigned long long rm = __builtin_amdgcn_ballot_w64(req);
   if (rm) {
@@ -1637,7 +1656,7 @@ __global__ __launch_bounds__(256) void vl_query_kernel(GridView tg, VListView v,
                                                      __builtin_amdgcn_mbcnt_lo(static_cast<unsigned int>(rm), 0u));
     if (req) {
       if (base + o < v.build_cap) v.build[base + o] = ci;
-      else atomicExch(&v.cell[ci], kVlNotBuilt);  // no room this sweep: requested again next time
+      else atomicExch(&v.cell[ci], kVlNotBuilt);  // no room this sweep: requested again later
     }
   }
   const unsigned long long pm = __builtin_amdgcn_ballot_w64(pending);
@@ -1652,17 +1671,21 @@ __global__ __launch_bounds__(256) void vl_query_kernel(GridView tg, VListView v,
   if (!live || pending) return;
   unsigned long long best = ~0ull;
   uint32_t bk = 0;
-  if (st < kVlSpecial) {
-    const uint32_t off = st >> 6, cnt = st & 63u;
+  const uint32_t off = (st >> 6) << 2, cnt = st & 63u;
+  if (st < kVlTouched) {
+    // lists are padded to a multiple of 4 with far sentinels (d2 = inf): 8 entries per round in flight
     const float4* e = v.pool + off;
-    for (uint32_t j = 0; j < cnt; j += 4) {
-      float4 a[4];
+    for (uint32_t j = 0; j < cnt; j += 8) {
+      float4 a[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) a[u] = e[min(j + u, cnt - 1)];
+      for (int u = 0; u < 4; ++u) a[u] = e[j + u];
+      const bool two = j + 4 < cnt;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 4; u < 8; ++u) a[u] = two ? e[j + u] : make_float4(3.0e38f, 3.0e38f, 3.0e38f, __uint_as_float(~0u));
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
         const unsigned long long key = mkkey(dist2(qx, qy, qz, a[u]), a[u].w);
-        if (j + u < cnt && key < best) {
+        if (key < best) {
           best = key;
           bk = j + u;
         }
@@ -1670,7 +1693,7 @@ __global__ __launch_bounds__(256) void vl_query_kernel(GridView tg, VListView v,
     }
   }
   const bool ok = best != ~0ull && static_cast<double>(__uint_as_float(static_cast<uint32_t>(best >> 32))) < thr;
-  nn_pos[k] = ok ? v.pool_pos[(st >> 6) + bk] : 0xffffffffu;
+  nn_pos[k] = ok ? v.pool_pos[off + bk] : 0xffffffffu;
   flags[k] = ok ? 1u : 0u;
 }
 
@@ -1704,17 +1727,29 @@ __device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long x)
   return x;
 }
 
+// affine dominance over the grown box (closed form of the minimum over its corners): does a (box-centred
+// a3, |a|^2 = a2) beat t (t3, |t|^2 = tt, largest squared distance to the box M2) at every point of the box?
+__device__ __forceinline__ bool vl_dominates(const double (&a3)[3], double a2, const double (&t3)[3], double tt,
+                                             double margin, const double (&hx)[3]) {
+  const double fmin = tt - a2 - 2.0 * (hx[0] * fabs(a3[0] - t3[0]) + hx[1] * fabs(a3[1] - t3[1]) +
+                                       hx[2] * fabs(a3[2] - t3[2]));
+  return fmin > margin;
+}
+
 // One wave per requested cell: gather S from the target grid (rows of the box grown by R, one round
 // trip for up to 64 rows' bounds, then the points), pick the anchors (the centre's 1-NN and each grown
-// corner's nearest candidate), drop every candidate an anchor dominates, append the rest to the pool.
-__global__ __launch_bounds__(256) void vl_build_kernel(GridView tg, VListView v) {
-  __shared__ float4 cand[4][kVlCand];
-  __shared__ uint32_t cpos[4][kVlCand];
-  __shared__ uint32_t rowa[4][64], rowp[4][64];
+// corner's nearest candidate), drop every candidate an anchor dominates, then every survivor another
+// survivor dominates (dominance is transitive, so the order of the drops does not matter), append the
+// rest to the pool padded to a multiple of 4 entries with far sentinels.
+constexpr int kVlWaves = 2;  // waves per build block (LDS: kVlCand x 20 bytes per wave)
+__global__ __launch_bounds__(64 * kVlWaves) void vl_build_kernel(GridView tg, VListView v) {
+  __shared__ float4 cand[kVlWaves][kVlCand];
+  __shared__ uint32_t cpos[kVlWaves][kVlCand];
+  __shared__ uint32_t rowa[kVlWaves][64], rowp[kVlWaves][64];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const unsigned int n = min(v.ctr[1], v.build_cap);
-  const unsigned int nwv = gridDim.x * 4u;
-  for (unsigned int sl = blockIdx.x * 4u + static_cast<unsigned int>(wid); sl < n; sl += nwv) {
+  const unsigned int nwv = gridDim.x * static_cast<unsigned int>(kVlWaves);
+  for (unsigned int sl = blockIdx.x * kVlWaves + static_cast<unsigned int>(wid); sl < n; sl += nwv) {
     const uint32_t ci = v.build[sl];
     const uint32_t tc = v.bcentre[sl];
     if (tc == 0xffffffffu) {
@@ -1859,11 +1894,53 @@ __global__ __launch_bounds__(256) void vl_build_kernel(GridView tg, VListView v)
     double an2[9];
 #pragma unroll
     for (int a = 0; a < 9; ++a) an2[a] = an[a][0] * an[a][0] + an[a][1] * an[a][1] + an[a][2] * an[a][2];
-    // affine dominance over the grown box (closed form of the minimum over its corners)
+    // stage 1: the anchors' dominance, survivors compacted to the front of cand (in order: a batch is
+    // read whole before its survivors are written, and they land at or before their own slots)
+    int ns = 0;
+    for (int i0 = 0; i0 < nc; i0 += 64) {
+      const int kq = i0 + lane;
+      bool keep = false;
+      float4 tp = make_float4(0.f, 0.f, 0.f, 0.f);
+      uint32_t tj = 0;
+      if (kq < nc) {
+        tp = cand[wid][kq];
+        tj = cpos[wid][kq];
+        const double t3[3] = {static_cast<double>(tp.x) - ctr[0], static_cast<double>(tp.y) - ctr[1],
+                              static_cast<double>(tp.z) - ctr[2]};
+        double M2 = 0.0, tt = 0.0;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+          const double e = fabs(t3[d]) + hx[d];
+          M2 += e * e;
+          tt += t3[d] * t3[d];
+        }
+        const double margin = 1e-5 * M2 + 1e-15;
+        bool dom = false;
+#pragma unroll
+        for (int a = 0; a < 9; ++a) dom = dom || vl_dominates(an[a], an2[a], t3, tt, margin, hx);
+        keep = !dom;
+      }
+      lds_wave_sync();
+      const unsigned long long m = __builtin_amdgcn_ballot_w64(keep);
+      const int o = static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<unsigned int>(m >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo(static_cast<unsigned int>(m), 0u)));
+      if (keep) {
+        cand[wid][ns + o] = tp;
+        cpos[wid][ns + o] = tj;
+      }
+      ns += __builtin_popcountll(m);
+      lds_wave_sync();
+    }
+    // stage 2: survivors against each other (at most 4 survivors per lane considered; more than 256
+    // survivors cannot make a list of <= 63 here: overflow)
+    if (ns > 256) {
+      if (lane == 0) v.cell[ci] = kVlOverflow;
+      continue;
+    }
     uint32_t keepm = 0;
-    for (int i = 0; i < kVlCand / 64; ++i) {
+    for (int i = 0; i < 4; ++i) {
       const int kq = lane + 64 * i;
-      if (kq >= nc) break;
+      if (kq >= ns) break;
       const float4 tp = cand[wid][kq];
       const double t3[3] = {static_cast<double>(tp.x) - ctr[0], static_cast<double>(tp.y) - ctr[1],
                             static_cast<double>(tp.z) - ctr[2]};
@@ -1876,11 +1953,13 @@ __global__ __launch_bounds__(256) void vl_build_kernel(GridView tg, VListView v)
       }
       const double margin = 1e-5 * M2 + 1e-15;
       bool dom = false;
-#pragma unroll
-      for (int a = 0; a < 9; ++a) {
-        const double fmin = tt - an2[a] - 2.0 * (hx[0] * fabs(an[a][0] - t3[0]) + hx[1] * fabs(an[a][1] - t3[1]) +
-                                                 hx[2] * fabs(an[a][2] - t3[2]));
-        dom = dom || fmin > margin;
+      for (int j = 0; j < ns && !dom; ++j) {
+        if (j == kq) continue;
+        const float4 ap = cand[wid][j];
+        const double a3[3] = {static_cast<double>(ap.x) - ctr[0], static_cast<double>(ap.y) - ctr[1],
+                              static_cast<double>(ap.z) - ctr[2]};
+        const double a2 = a3[0] * a3[0] + a3[1] * a3[1] + a3[2] * a3[2];
+        dom = vl_dominates(a3, a2, t3, tt, margin, hx);
       }
       if (!dom) keepm |= 1u << i;
     }
@@ -1892,15 +1971,16 @@ __global__ __launch_bounds__(256) void vl_build_kernel(GridView tg, VListView v)
       if (lane == 0) v.cell[ci] = kVlOverflow;
       continue;
     }
+    const unsigned int cnt4 = (cntl + 3u) & ~3u;
     unsigned int off = 0;
-    if (lane == 0) off = atomicAdd(&v.ctr[0], cntl);
+    if (lane == 0) off = atomicAdd(&v.ctr[0], cnt4);
     off = __builtin_amdgcn_readfirstlane(off);
-    if (off + cntl > v.pool_cap) {
+    if (off + cnt4 > v.pool_cap) {
       if (lane == 0) v.cell[ci] = kVlOverflow;
       continue;
     }
     unsigned int run = 0;
-    for (int i = 0; i < kVlCand / 64; ++i) {
+    for (int i = 0; i < 4; ++i) {
       const bool b = (keepm >> i) & 1u;
       const unsigned long long m = __builtin_amdgcn_ballot_w64(b);
       if (b) {
@@ -1911,7 +1991,11 @@ __global__ __launch_bounds__(256) void vl_build_kernel(GridView tg, VListView v)
       }
       run += static_cast<unsigned int>(__builtin_popcountll(m));
     }
-    if (lane == 0) v.cell[ci] = (off << 6) | cntl;
+    if (static_cast<unsigned int>(lane) < cnt4 - cntl) {  // far sentinels (d2 = inf) up to the multiple of 4
+      v.pool[off + cntl + lane] = make_float4(3.0e38f, 3.0e38f, 3.0e38f, __uint_as_float(~0u));
+      v.pool_pos[off + cntl + lane] = 0u;
+    }
+    if (lane == 0) v.cell[ci] = ((off >> 2) << 6) | cntl;
     lds_wave_sync();  // cand / cpos are rewritten for the wave's next cell
   }
 }
@@ -1945,12 +2029,12 @@ __global__ void vl_stats_kernel(const uint32_t* __restrict__ cell, size_t n, uns
        i += static_cast<size_t>(gridDim.x) * blockDim.x) {
     const uint32_t c = cell[i];
     if (c == kVlNotBuilt) continue;  // the common case: no atomics
-    if (c < kVlSpecial) {
+    if (c < kVlTouched) {
       atomicAdd(&out[0], 1ull);
       atomicAdd(&out[1], static_cast<unsigned long long>(c & 63u));
       atomicAdd(&out[8 + min(c & 63u, 55u)], 1ull);
     } else {
-      atomicAdd(&out[c == kVlReject ? 2 : c == kVlOverflow ? 3 : 4], 1ull);
+      atomicAdd(&out[c == kVlReject ? 2 : c == kVlOverflow ? 3 : c == kVlRequested ? 4 : 5], 1ull);
     }
   }
 }
@@ -3446,19 +3530,26 @@ hipError_t launch_knn_cov(const GridView& g, int k, double eps, size_t p0, size_
 bool knn_logged_enabled() { return knn_two_phase(); }
 
 hipError_t launch_vl_sweep(const GridView& tgt, const VListView& vl, const float4* src, size_t p0, size_t p1,
-                           Xf34 T, double thr, int seeded, uint32_t* nn_pos, uint32_t* flags,
-                           const uint32_t* qperm, int cus, hipStream_t s) {
+                           Xf34 T, double thr, int seeded, uint32_t* nn_pos, uint32_t* flags, const float4* qsrc,
+                           int cus, hipStream_t s) {
   if (p1 <= p0) return hipSuccess;
   hipError_t e = hipMemsetAsync(vl.ctr + 1, 0, 2 * sizeof(unsigned int), s);
   if (e != hipSuccess) return e;
-  vl_query_kernel<<<nblk(p1 - p0), 256, 0, s>>>(tgt, vl, src, p0, p1, T, thr, nn_pos, flags, qperm);
+  vl_query_kernel<<<nblk(p1 - p0), 256, 0, s>>>(vl, qsrc, p1 - p0, T, thr, nn_pos, flags);
   // requested cells: the centre's 1-NN within the gate + the grown cell's half diagonal, then the lists
   const double hd = std::sqrt(3.0) * (0.5 * static_cast<double>(vl.c) + static_cast<double>(vl.es));
   const double rc = vl.gate * (1.0 + 1e-5) + 1e-9 + hd;
   const unsigned g = static_cast<unsigned>(std::max(cus, 1));
   vl_centre_kernel<<<4 * g, 256, 0, s>>>(tgt, vl, rc * rc * (1.0 + 1e-5));
-  vl_build_kernel<<<4 * g, 256, 0, s>>>(tgt, vl);
+  vl_build_kernel<<<8 * g, 64 * kVlWaves, 0, s>>>(tgt, vl);
   vl_fallback_kernel<<<8 * g, 256, 0, s>>>(tgt, vl, src, p0, T, thr, seeded, nn_pos, flags);
+  return hipGetLastError();
+}
+
+hipError_t launch_query_order_points(const float4* src, size_t p0, size_t n, const uint32_t* qperm, float4* qsrc,
+                                     hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  query_order_points_kernel<<<nblk(n), 256, 0, s>>>(src, p0, n, qperm, qsrc);
   return hipGetLastError();
 }
 

@@ -456,22 +456,26 @@ def _vlist_cases(part_small):
     return [("part", src, tgt, Ttrue), ("fod", fsrc, ftgt, fT), ("lattice", lat.copy(), lat.copy(), np.eye(4))]
 
 
-@pytest.mark.parametrize("case", ["part", "fod", "lattice"])
-def test_vlist_sweeps_bitexact_through_builds(engine_mod, part_small, monkeypatch, case):
-    """r04 1-NN cell lists: a sweep whose cells have no list yet (exact per-lane search + list
-    builds), the SAME sweep again (every query answered from a list), then new transforms (lists
-    and builds mixed) -- every sweep's indices bit-exact against the oracle and against the r03
-    sweep (MGICP_VLIST=0), with rejections near the 4 cm gate and exact-distance ties."""
+@pytest.mark.parametrize("case,eager", [("part", 0), ("fod", 0), ("lattice", 0), ("part", 1)])
+def test_vlist_sweeps_bitexact_through_builds(engine_mod, part_small, monkeypatch, case, eager):
+    """r04 1-NN cell lists: the first sweep over cells without lists (exact per-lane search; cells
+    marked), the same sweep again (the marked cells' lists built, queries still on the per-lane
+    search), a third time (every query answered from a list), then new transforms -- every sweep's
+    indices and Mahalanobis matrices bit-exact against the oracle and against the r03 sweep
+    (MGICP_VLIST=0), with rejections near the 4 cm gate and exact-distance ties.  eager = 1
+    (MGICP_VLIST_EAGER): lists built at a cell's first query."""
     from oracle import ref
 
     name, src, tgt, Ttrue = {c[0]: c for c in _vlist_cases(part_small)}[case]
-    Ts = [np.eye(4, dtype=np.float32), np.eye(4, dtype=np.float32), np.linalg.inv(Ttrue).astype(np.float32)]
+    I = np.eye(4, dtype=np.float32)
+    Tinv = np.linalg.inv(Ttrue).astype(np.float32)
     off = np.eye(4, dtype=np.float32)
     off[:3, 3] = [0.0025, -0.0025, 0.031]
-    Ts += [off, off]
+    Ts = [I, I, I, Tinv, Tinv, Tinv, off, off, off]
     o = ref.RefGICP()
     o.set_source(src)
     o.set_target(tgt)
+    monkeypatch.setenv("MGICP_VLIST_EAGER", str(eager))
     e = engine_mod()
     e.set_source_xyz(src)
     e.set_target_xyz(tgt)
@@ -490,12 +494,17 @@ def test_vlist_sweeps_bitexact_through_builds(engine_mod, part_small, monkeypatc
         np.testing.assert_array_equal(tj, tj0)
         np.testing.assert_array_equal(M, M0)
     assert e0.vlist_stats()["cells"] == 0  # the r03 sweep really ran there
-    assert stats[0]["cells"] > 0 and stats[0]["requested"] > 0 and stats[0]["pending"] > 0
-    # the repeated sweep finds every cell listed or rejected: nothing requested, nothing pending
-    # (except cells that overflowed)
-    assert stats[1]["requested"] == 0, stats[1]
-    assert stats[1]["pending"] <= stats[1]["overflow"] * 64, stats[1]
-    assert stats[4]["requested"] == 0, stats[4]
+    assert stats[0]["cells"] > 0 and stats[0]["pending"] > 0
+    if eager:
+        assert stats[0]["requested"] > 0 and stats[1]["requested"] == 0, stats[:2]
+    else:
+        assert stats[0]["requested"] == 0 and stats[1]["requested"] > 0, stats[:2]
+    # the third identical sweep finds every cell listed or rejected: nothing requested, and only the
+    # queries of overflow cells (if any) pending
+    for k in (2, 5, 8):
+        assert stats[k]["requested"] == 0, (k, stats[k])
+        assert stats[k]["pending"] <= stats[k]["overflow"] * 64, (k, stats[k])
+    assert stats[2]["lists"] > 0
     e.close()
     e0.close()
 
