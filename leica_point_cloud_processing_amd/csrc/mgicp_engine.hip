@@ -412,13 +412,11 @@ struct mgicp_ctx {
   bool vl_off = false;                // the gate is too large for a fine grid of this target: r03 sweeps
   VListView vl{};
   size_t vl_ncells = 0;
-  DevBuf<uint32_t> vl_cell, vl_pool_pos, vl_build, vl_bcentre, vl_pend;
+  DevBuf<uint32_t> vl_cell, vl_build, vl_bcentre, vl_pend;
   DevBuf<float4> vl_pool;
   DevBuf<unsigned int> vl_ctr;
   uint32_t vl_epoch = 0;              // sweeps run over the current lists (a cell is built on its 2nd sweep)
   bool vl_eager = false;              // env MGICP_VLIST_EAGER: build a cell at its first query
-  DevBuf<float4> qsrc;                // the shard's (guess-applied) points in query order, w = shard position
-  const float4* qsrc_for = nullptr;   // the d_out they were taken from (nullptr: stale)
   // multi-GPU
   int nranks = 1, rank = 0;
   ncclComm_t comm = nullptr;
@@ -841,7 +839,6 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
   cl.dirty = false;
   cl.have_cov = false;
   if (&cl == &ctx->tgt) ctx->vl_valid = false;  // the 1-NN cell lists index the old target
-  if (&cl == &ctx->src) ctx->qsrc_for = nullptr;  // the query-order copy holds the old source
   if (&cl == &ctx->src || &cl == &ctx->tgt) {  // sorted positions changed
     ctx->have_corr = false;
     ctx->seed_valid = false;
@@ -1278,7 +1275,6 @@ int set_output(mgicp_ctx* ctx, const Mat4& G) {
     HIPCK(ctx->src_out.reserve(ctx->src.n));
     HIPCK(launch_xform_points(ctx->src.pts.p, ctx->src.n, G.xf(), ctx->src_out.p, ctx->stream));
     ctx->d_out = ctx->src_out.p;
-    ctx->qsrc_for = nullptr;  // src_out was rewritten
     // bbox of the transformed cloud (the Gauss-Newton expansion centre)
     const size_t n = ctx->src.n;
     const int nb = static_cast<int>(std::min<size_t>((n + 255) / 256, 1024));
@@ -1374,15 +1370,13 @@ int vl_prepare(mgicp_ctx* ctx) {
     v.nz = nd[2];
     HIPCK(ctx->vl_cell.reserve(nc));
     HIPCK(hipMemsetAsync(ctx->vl_cell.p, 0xff, nc * sizeof(uint32_t), ctx->stream));
-    // list starts are stored in units of 4 entries in 25 bits: at most 2^27 entries (20 bytes each)
+    // list starts are stored in units of 4 entries in 25 bits: at most 2^27 entries (16 bytes each)
     const size_t cap = std::min<size_t>(size_t(1) << 27, std::max<size_t>(size_t(1) << 22, 32 * t.n));
     HIPCK(ctx->vl_pool.reserve(cap));
-    HIPCK(ctx->vl_pool_pos.reserve(cap));
     HIPCK(ctx->vl_ctr.reserve(4));
     HIPCK(hipMemsetAsync(ctx->vl_ctr.p, 0, 4 * sizeof(unsigned int), ctx->stream));
     v.cell = ctx->vl_cell.p;
     v.pool = ctx->vl_pool.p;
-    v.pool_pos = ctx->vl_pool_pos.p;
     v.pool_cap = static_cast<uint32_t>(cap);
     v.ctr = ctx->vl_ctr.p;
     ctx->vl_ncells = nc;
@@ -1404,13 +1398,7 @@ int vl_prepare(mgicp_ctx* ctx) {
   }
   ctx->vl.epoch = ctx->vl_epoch;
   ctx->vl.eager = ctx->vl_eager ? 1 : 0;
-  // the shard's points in query order (once per source cloud, shard and guess)
-  if (ctx->qsrc_for != ctx->d_out || !ctx->qperm_valid) {
-    const uint32_t* qp = query_perm(ctx);
-    HIPCK(ctx->qsrc.reserve(q));
-    HIPCK(launch_query_order_points(ctx->d_out, ctx->shard_p0(), ns, qp, ctx->qsrc.p, ctx->stream));
-    ctx->qsrc_for = ctx->qperm_valid ? ctx->d_out : nullptr;
-  }
+  ctx->vl.tpts = ctx->tgt.pts.p;
   return MGICP_OK;
 }
 
@@ -1422,7 +1410,7 @@ hipError_t launch_sweep(mgicp_ctx* ctx, const Mat4& T, double thr, bool seeded, 
   const GridView& g = ctx->tgt.view;
   if (ctx->vlist && ctx->vl_valid && !ctx->vl_off)
     return launch_vl_sweep(g, ctx->vl, ctx->d_out, p0, p1, T.xf(), thr, seeded ? 1 : 0, ctx->prev_pos.p, ctx->flags.p,
-                           ctx->qsrc.p, ctx->cus, ctx->stream);
+                           ctx->cus, ctx->stream);
   if (ctx->corr_wave && g.pairs) {
     const float rc = ctx->corr_rcap * g.h;
     void* work = nullptr;
@@ -2043,8 +2031,8 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   ctx->chunk_base.release(); ctx->spart.release(); ctx->gath.release(); ctx->msuper.release();
   ctx->prev_pos.release(); ctx->flags.release(); ctx->cpos.release();
   ctx->nn_work.release(); ctx->nn_work_n.release();
-  ctx->vl_cell.release(); ctx->vl_pool.release(); ctx->vl_pool_pos.release(); ctx->vl_ctr.release();
-  ctx->vl_build.release(); ctx->vl_bcentre.release(); ctx->vl_pend.release(); ctx->qsrc.release();
+  ctx->vl_cell.release(); ctx->vl_pool.release(); ctx->vl_ctr.release();
+  ctx->vl_build.release(); ctx->vl_bcentre.release(); ctx->vl_pend.release();
   ctx->tpart.release();
   ctx->tpart_n = 0;
   ctx->corr_f.release(); ctx->corr_d.release(); ctx->cscratch.release();
@@ -2541,7 +2529,6 @@ int mgicp_comm_init(mgicp_ctx* ctx, int nranks, int rank, const unsigned char id
   ctx->nranks = nranks;
   ctx->rank = rank;
   ctx->qperm_valid = false;
-  ctx->qsrc_for = nullptr;
   ctx->src.have_cov = false;
   ctx->have_corr = false;
   ctx->seed_valid = false;  // the shard (and its per-point match buffers) changes

@@ -155,8 +155,10 @@ constexpr uint32_t kVlOverflow = 0xFFFFFFFDu;  // more than kVlMaxList entries /
 constexpr uint32_t kVlReject = 0xFFFFFFFCu;    // no target point within the gate of the cell
 constexpr uint32_t kVlTouched = 0x80000000u;   // | epoch: first queried in sweep `epoch` (built when queried
                                                // again in a later sweep); values below: (off4 << 6) | count
-constexpr int kVlMaxList = 63;                 // entries per list (lists padded to a multiple of 4 with far
-                                               // sentinels; off4 = list start / 4, < 2^25)
+constexpr int kVlLong = 63;                    // count field 63: a long list -- its true count in the x bits of a
+                                               // header entry at off, its entries from off + 4
+                                               // (lists padded to a multiple of 4 with far sentinels; off4 = list
+                                               // start / 4, < 2^25)
 struct VListView {
   float ox, oy, oz;      // fine grid origin
   float c, inv_c;        // fine cell edge and its float reciprocal
@@ -164,8 +166,8 @@ struct VListView {
   int nx, ny, nz;
   double gate;           // max correspondence distance the lists are built for
   uint32_t* cell;        // nx * ny * nz states / (off << 6 | count)
-  float4* pool;          // list entries {x, y, z, bits(original index)}
-  uint32_t* pool_pos;    // their sorted target positions
+  float4* pool;          // list entries {x, y, z, bits(sorted target position)}
+  const float4* tpts;    // the target's sorted points (w = original index: exact-distance ties only)
   uint32_t pool_cap;     // entries (< 2^26)
   unsigned int* ctr;     // [0] pool head (persistent), [1] cells requested, [2] queries pending (per sweep)
   uint32_t* build;       // requested cells of this sweep
@@ -179,12 +181,8 @@ struct VListView {
 // queued (pend) and their cells requested; then the requested cells' lists are built and the
 // pending queries answered by the exact per-lane search (seeded like correspond_kernel)
 hipError_t launch_vl_sweep(const GridView& tgt, const VListView& vl, const float4* src, size_t p0, size_t p1,
-                           Xf34 T, double thr, int seeded, uint32_t* nn_pos, uint32_t* flags,
-                           const float4* qsrc /*the shard's points in query order, w = bits(shard position)*/,
-                           int cus, hipStream_t s);
-// qsrc[t] = src[p0 + qperm[t]] with w = bits(qperm[t]) (qperm nullable: identity)
-hipError_t launch_query_order_points(const float4* src, size_t p0, size_t n, const uint32_t* qperm, float4* qsrc,
-                                     hipStream_t s);
+                           Xf34 T, double thr, int seeded, uint32_t* nn_pos, uint32_t* flags, int cus,
+                           hipStream_t s);
 // diagnostics (env MGICP_VLIST_STATS): per built cell list lengths histogram etc. into out[64]
 hipError_t launch_vl_stats(const VListView& vl, size_t ncells, unsigned long long* out /*device, 64*/, hipStream_t s);
 size_t     pair_count(size_t n);

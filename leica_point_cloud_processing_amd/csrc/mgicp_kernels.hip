@@ -1604,28 +1604,18 @@ __device__ __forceinline__ void vl_cell_xyz(const VListView& v, uint32_t ci, uin
   iz = ci / (nx * ny);
 }
 
-// the shard's points in the sweeps' query order (Morton), w = bits(shard position): the query kernel
-// reads them coalesced, one dependent load fewer
-__global__ void query_order_points_kernel(const float4* __restrict__ src, size_t p0, size_t n,
-                                          const uint32_t* __restrict__ qperm, float4* __restrict__ out) {
-  const size_t t = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (t >= n) return;
-  const uint32_t k = qperm ? qperm[t] : static_cast<uint32_t>(t);
-  const float4 s = src[p0 + k];
-  out[t] = make_float4(s.x, s.y, s.z, __uint_as_float(k));
-}
-
-__global__ __launch_bounds__(256) void vl_query_kernel(VListView v, const float4* __restrict__ qsrc, size_t n, Xf34 T,
-                                                       double thr, uint32_t* __restrict__ nn_pos,
+__global__ __launch_bounds__(256) void vl_query_kernel(VListView v, const float4* __restrict__ src, size_t p0,
+                                                       size_t n, Xf34 T, double thr, uint32_t* __restrict__ nn_pos,
                                                        uint32_t* __restrict__ flags) {
+  // grid order (shard positions): the source reads and the nn_pos / flags writes are coalesced, and
+  // neighbouring lanes query neighbouring cells (shared table lines and lists)
   const int lane = threadIdx.x & 63;
   const size_t t = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   const bool live = t < n;
+  const uint32_t k = static_cast<uint32_t>(t);
   float qx = 0.f, qy = 0.f, qz = 0.f;
-  uint32_t k = 0;
   if (live) {
-    const float4 s = qsrc[t];
-    k = __float_as_uint(s.w);
+    const float4 s = src[p0 + t];
     xform(T, s.x, s.y, s.z, qx, qy, qz);
   }
   const int ix = qcell(qx, v.ox, v.inv_c), iy = qcell(qy, v.oy, v.inv_c), iz = qcell(qz, v.oz, v.inv_c);
@@ -1669,10 +1659,14 @@ __global__ __launch_bounds__(256) void vl_query_kernel(VListView v, const float4
     if (pending) v.pend[base + o] = k;
   }
   if (!live || pending) return;
-  unsigned long long best = ~0ull;
-  uint32_t bk = 0;
-  const uint32_t off = (st >> 6) << 2, cnt = st & 63u;
+  float bd = INFINITY;
+  uint32_t bp = 0xffffffffu;
   if (st < kVlTouched) {
+    uint32_t off = (st >> 6) << 2, cnt = st & 63u;
+    if (cnt == static_cast<uint32_t>(kVlLong)) {  // a long list: count in the header entry
+      cnt = __float_as_uint(v.pool[off].x);
+      off += 4;
+    }
     // lists are padded to a multiple of 4 with far sentinels (d2 = inf): 8 entries per round in flight
     const float4* e = v.pool + off;
     for (uint32_t j = 0; j < cnt; j += 8) {
@@ -1681,19 +1675,24 @@ __global__ __launch_bounds__(256) void vl_query_kernel(VListView v, const float4
       for (int u = 0; u < 4; ++u) a[u] = e[j + u];
       const bool two = j + 4 < cnt;
 #pragma unroll
-      for (int u = 4; u < 8; ++u) a[u] = two ? e[j + u] : make_float4(3.0e38f, 3.0e38f, 3.0e38f, __uint_as_float(~0u));
+      for (int u = 4; u < 8; ++u) a[u] = two ? e[j + u] : make_float4(3.0e38f, 3.0e38f, 3.0e38f, 0.f);
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const unsigned long long key = mkkey(dist2(qx, qy, qz, a[u]), a[u].w);
-        if (key < best) {
-          best = key;
-          bk = j + u;
+        const float d = dist2(qx, qy, qz, a[u]);
+        const uint32_t pu = __float_as_uint(a[u].w);
+        if (d < bd) {
+          bd = d;
+          bp = pu;
+        } else if (d == bd && d < INFINITY && pu != bp) {
+          // an exact-distance tie (measure zero on scans, lattices have them): the lower original
+          // index wins, as the (d2, index) key of every other 1-NN search
+          if (__float_as_uint(v.tpts[pu].w) < __float_as_uint(v.tpts[bp].w)) bp = pu;
         }
       }
     }
   }
-  const bool ok = best != ~0ull && static_cast<double>(__uint_as_float(static_cast<uint32_t>(best >> 32))) < thr;
-  nn_pos[k] = ok ? v.pool_pos[off + bk] : 0xffffffffu;
+  const bool ok = bp != 0xffffffffu && static_cast<double>(bd) < thr;
+  nn_pos[k] = ok ? bp : 0xffffffffu;
   flags[k] = ok ? 1u : 0u;
 }
 
@@ -1931,16 +1930,17 @@ __global__ __launch_bounds__(64 * kVlWaves) void vl_build_kernel(GridView tg, VL
       ns += __builtin_popcountll(m);
       lds_wave_sync();
     }
-    // stage 2: survivors against each other (at most 4 survivors per lane considered; more than 256
-    // survivors cannot make a list of <= 63 here: overflow)
-    if (ns > 256) {
-      if (lane == 0) v.cell[ci] = kVlOverflow;
-      continue;
-    }
+    // stage 2: survivors against each other (up to 256 survivors; more are kept as they are, in a
+    // long list)
+    const bool pair = ns <= 256;
     uint32_t keepm = 0;
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < kVlCand / 64; ++i) {
       const int kq = lane + 64 * i;
       if (kq >= ns) break;
+      if (!pair) {
+        keepm |= 1u << i;
+        continue;
+      }
       const float4 tp = cand[wid][kq];
       const double t3[3] = {static_cast<double>(tp.x) - ctr[0], static_cast<double>(tp.y) - ctr[1],
                             static_cast<double>(tp.z) - ctr[2]};
@@ -1967,11 +1967,8 @@ __global__ __launch_bounds__(64 * kVlWaves) void vl_build_kernel(GridView tg, VL
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) cntl += __shfl_xor(cntl, o, 64);
     cntl = __builtin_amdgcn_readfirstlane(cntl);
-    if (cntl > static_cast<unsigned int>(kVlMaxList)) {
-      if (lane == 0) v.cell[ci] = kVlOverflow;
-      continue;
-    }
-    const unsigned int cnt4 = (cntl + 3u) & ~3u;
+    const bool lng = cntl >= static_cast<unsigned int>(kVlLong);
+    const unsigned int cnt4 = ((cntl + 3u) & ~3u) + (lng ? 4u : 0u);
     unsigned int off = 0;
     if (lane == 0) off = atomicAdd(&v.ctr[0], cnt4);
     off = __builtin_amdgcn_readfirstlane(off);
@@ -1979,23 +1976,24 @@ __global__ __launch_bounds__(64 * kVlWaves) void vl_build_kernel(GridView tg, VL
       if (lane == 0) v.cell[ci] = kVlOverflow;
       continue;
     }
+    const unsigned int e0 = off + (lng ? 4u : 0u);
+    if (lng && lane < 4) v.pool[off + lane] = make_float4(__uint_as_float(cntl), 0.f, 0.f, 0.f);
     unsigned int run = 0;
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < kVlCand / 64; ++i) {
       const bool b = (keepm >> i) & 1u;
       const unsigned long long m = __builtin_amdgcn_ballot_w64(b);
       if (b) {
         const unsigned int o = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned int>(m >> 32),
                                                          __builtin_amdgcn_mbcnt_lo(static_cast<unsigned int>(m), 0u));
-        v.pool[off + run + o] = cand[wid][lane + 64 * i];
-        v.pool_pos[off + run + o] = cpos[wid][lane + 64 * i];
+        const float4 c4 = cand[wid][lane + 64 * i];
+        v.pool[e0 + run + o] = make_float4(c4.x, c4.y, c4.z, __uint_as_float(cpos[wid][lane + 64 * i]));
       }
       run += static_cast<unsigned int>(__builtin_popcountll(m));
     }
-    if (static_cast<unsigned int>(lane) < cnt4 - cntl) {  // far sentinels (d2 = inf) up to the multiple of 4
-      v.pool[off + cntl + lane] = make_float4(3.0e38f, 3.0e38f, 3.0e38f, __uint_as_float(~0u));
-      v.pool_pos[off + cntl + lane] = 0u;
-    }
-    if (lane == 0) v.cell[ci] = ((off >> 2) << 6) | cntl;
+    const unsigned int npad = ((cntl + 3u) & ~3u) - cntl;
+    if (static_cast<unsigned int>(lane) < npad)  // far sentinels (d2 = inf) up to the multiple of 4
+      v.pool[e0 + cntl + lane] = make_float4(3.0e38f, 3.0e38f, 3.0e38f, 0.f);
+    if (lane == 0) v.cell[ci] = ((off >> 2) << 6) | (lng ? static_cast<unsigned int>(kVlLong) : cntl);
     lds_wave_sync();  // cand / cpos are rewritten for the wave's next cell
   }
 }
@@ -3530,12 +3528,12 @@ hipError_t launch_knn_cov(const GridView& g, int k, double eps, size_t p0, size_
 bool knn_logged_enabled() { return knn_two_phase(); }
 
 hipError_t launch_vl_sweep(const GridView& tgt, const VListView& vl, const float4* src, size_t p0, size_t p1,
-                           Xf34 T, double thr, int seeded, uint32_t* nn_pos, uint32_t* flags, const float4* qsrc,
-                           int cus, hipStream_t s) {
+                           Xf34 T, double thr, int seeded, uint32_t* nn_pos, uint32_t* flags, int cus,
+                           hipStream_t s) {
   if (p1 <= p0) return hipSuccess;
   hipError_t e = hipMemsetAsync(vl.ctr + 1, 0, 2 * sizeof(unsigned int), s);
   if (e != hipSuccess) return e;
-  vl_query_kernel<<<nblk(p1 - p0), 256, 0, s>>>(vl, qsrc, p1 - p0, T, thr, nn_pos, flags);
+  vl_query_kernel<<<nblk(p1 - p0), 256, 0, s>>>(vl, src, p0, p1 - p0, T, thr, nn_pos, flags);
   // requested cells: the centre's 1-NN within the gate + the grown cell's half diagonal, then the lists
   const double hd = std::sqrt(3.0) * (0.5 * static_cast<double>(vl.c) + static_cast<double>(vl.es));
   const double rc = vl.gate * (1.0 + 1e-5) + 1e-9 + hd;
@@ -3543,13 +3541,6 @@ hipError_t launch_vl_sweep(const GridView& tgt, const VListView& vl, const float
   vl_centre_kernel<<<4 * g, 256, 0, s>>>(tgt, vl, rc * rc * (1.0 + 1e-5));
   vl_build_kernel<<<8 * g, 64 * kVlWaves, 0, s>>>(tgt, vl);
   vl_fallback_kernel<<<8 * g, 256, 0, s>>>(tgt, vl, src, p0, T, thr, seeded, nn_pos, flags);
-  return hipGetLastError();
-}
-
-hipError_t launch_query_order_points(const float4* src, size_t p0, size_t n, const uint32_t* qperm, float4* qsrc,
-                                     hipStream_t s) {
-  if (n == 0) return hipSuccess;
-  query_order_points_kernel<<<nblk(n), 256, 0, s>>>(src, p0, n, qperm, qsrc);
   return hipGetLastError();
 }
 
