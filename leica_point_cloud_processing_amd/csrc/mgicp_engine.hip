@@ -415,8 +415,14 @@ struct mgicp_ctx {
   DevBuf<uint32_t> vl_cell, vl_build, vl_bcentre, vl_pend;
   DevBuf<float4> vl_pool;
   DevBuf<unsigned int> vl_ctr;
-  uint32_t vl_epoch = 0;              // sweeps run over the current lists (a cell is built on its 2nd sweep)
-  bool vl_eager = false;              // env MGICP_VLIST_EAGER: build a cell at its first query
+  uint32_t vl_epoch = 0;              // sweeps run over the current lists
+  // A cell's list is built when a sweep of the SECOND align (or debug sweep group) over the current
+  // target and gate queries it: the first align after a set_target runs the r03 sweep (no list work,
+  // the ms-to-converge of a one-off align is unchanged), the second builds the lists of every cell it
+  // queries, later aligns (GICPAlignment::iterate, the next scans of the same CAD target) read them.
+  int vl_groups = 0;                  // aligns / debug sweep groups finished over the current lists
+  bool vl_eager = true;               // env MGICP_VLIST_EAGER=0: build a cell only at its query in a later sweep
+  bool vl_cold_r03 = true;            // env MGICP_VLIST_COLD=0: the first align uses the lists too (builds them)
   // multi-GPU
   int nranks = 1, rank = 0;
   ncclComm_t comm = nullptr;
@@ -1382,6 +1388,7 @@ int vl_prepare(mgicp_ctx* ctx) {
     ctx->vl_ncells = nc;
     ctx->vl_valid = true;
     ctx->vl_epoch = 0;
+    ctx->vl_groups = 0;
   }
   if (ctx->vl_off) return MGICP_OK;
   // per-sweep lists sized by the shard (one request / pending entry per query at most)
@@ -1408,7 +1415,7 @@ int vl_prepare(mgicp_ctx* ctx) {
 hipError_t launch_sweep(mgicp_ctx* ctx, const Mat4& T, double thr, bool seeded, const uint32_t* qp) {
   const size_t p0 = ctx->shard_p0(), p1 = ctx->shard_p1();
   const GridView& g = ctx->tgt.view;
-  if (ctx->vlist && ctx->vl_valid && !ctx->vl_off)
+  if (ctx->vlist && ctx->vl_valid && !ctx->vl_off && (ctx->vl_groups > 0 || !ctx->vl_cold_r03))
     return launch_vl_sweep(g, ctx->vl, ctx->d_out, p0, p1, T.xf(), thr, seeded ? 1 : 0, ctx->prev_pos.p, ctx->flags.p,
                            ctx->cus, ctx->stream);
   if (ctx->corr_wave && g.pairs) {
@@ -1449,7 +1456,7 @@ int correspond(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
     HIPCK(launch_sweep(ctx, T, thr, seeded, qp));
   }
   ctx->seed_valid = true;
-  if (ctx->vl_stats && ctx->vlist && !ctx->vl_off) {
+  if (ctx->vl_stats && ctx->vlist && !ctx->vl_off && (ctx->vl_groups > 0 || !ctx->vl_cold_r03)) {
     unsigned int c3[3];
     HIPCK(hipMemcpyAsync(c3, ctx->vl_ctr.p, 3 * sizeof(unsigned int), hipMemcpyDeviceToHost, s));
     HIPCK(ctx->u64.reserve(64));
@@ -1970,6 +1977,7 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
   }
   if (const char* vs = std::getenv("MGICP_VLIST_STATS")) ctx->vl_stats = std::atoi(vs) != 0;
   if (const char* ve = std::getenv("MGICP_VLIST_EAGER")) ctx->vl_eager = std::atoi(ve) != 0;
+  if (const char* vc = std::getenv("MGICP_VLIST_COLD")) ctx->vl_cold_r03 = std::atoi(vc) != 0;
   ctx->tgt.want_pairs = ctx->corr_wave;
   if (const char* cb = std::getenv("MGICP_CELL_BOXES")) ctx->tgt.want_boxes = std::atoi(cb) != 0;
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -2141,6 +2149,7 @@ int mgicp_align(mgicp_ctx* ctx, const float guess_cm[16], float out_T_cm[16], mg
   }
   // polled passes leave their kernels' completion unobserved: drain the stream once
   if ((rc = sync(ctx))) return rc;
+  if (ctx->vl_valid) ctx->vl_groups++;
   if (ctx->h_gtrace) {
     // diagnostics of the gated passes of this align: device-side gate wait and spread, host-side
     // decision time (sums seen -> command published); device wall clock in 10 ns ticks (100 MHz)
@@ -2686,6 +2695,7 @@ static int debug_corr(mgicp_ctx* ctx, const float T_cm[16], bool seeded, int* ou
   const Mat4 G = Mat4::identity();
   if ((rc = set_output(ctx, G))) return rc;
   if ((rc = correspond(ctx, Mat4::from_cm(T_cm), G, seeded))) return rc;
+  if (ctx->vl_valid) ctx->vl_groups++;
   const size_t p0 = ctx->shard_p0(), p1 = ctx->shard_p1(), ns = p1 - p0;
   std::vector<uint32_t> nn(ns), flag(ns), slot(ns + 1), perm(n), tperm(ctx->tgt.n);
   std::vector<uint32_t> cbase(static_cast<size_t>(chunk_count(ns)) + 1);

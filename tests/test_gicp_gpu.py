@@ -458,12 +458,13 @@ def _vlist_cases(part_small):
 
 @pytest.mark.parametrize("case,eager", [("part", 0), ("fod", 0), ("lattice", 0), ("part", 1)])
 def test_vlist_sweeps_bitexact_through_builds(engine_mod, part_small, monkeypatch, case, eager):
-    """r04 1-NN cell lists: the first sweep over cells without lists (exact per-lane search; cells
-    marked), the same sweep again (the marked cells' lists built, queries still on the per-lane
-    search), a third time (every query answered from a list), then new transforms -- every sweep's
-    indices and Mahalanobis matrices bit-exact against the oracle and against the r03 sweep
-    (MGICP_VLIST=0), with rejections near the 4 cm gate and exact-distance ties.  eager = 1
-    (MGICP_VLIST_EAGER): lists built at a cell's first query."""
+    """r04 1-NN cell lists: the first sweep group after set_target runs the r03 sweep, the second
+    builds the lists of the cells it queries (those queries take the exact per-lane search), the
+    third finds every cell listed (every query answered from a list), then new transforms (lists
+    and builds mixed) -- every sweep's indices and Mahalanobis matrices bit-exact against the
+    oracle and against the r03 sweep (MGICP_VLIST=0), with rejections near the 4 cm gate and
+    exact-distance ties.  eager = 0 (MGICP_VLIST_EAGER=0, MGICP_VLIST_COLD=0): lists used from the
+    first sweep, a cell built only when a later sweep queries it again."""
     from oracle import ref
 
     name, src, tgt, Ttrue = {c[0]: c for c in _vlist_cases(part_small)}[case]
@@ -476,6 +477,7 @@ def test_vlist_sweeps_bitexact_through_builds(engine_mod, part_small, monkeypatc
     o.set_source(src)
     o.set_target(tgt)
     monkeypatch.setenv("MGICP_VLIST_EAGER", str(eager))
+    monkeypatch.setenv("MGICP_VLIST_COLD", str(eager))
     e = engine_mod()
     e.set_source_xyz(src)
     e.set_target_xyz(tgt)
@@ -494,11 +496,11 @@ def test_vlist_sweeps_bitexact_through_builds(engine_mod, part_small, monkeypatc
         np.testing.assert_array_equal(tj, tj0)
         np.testing.assert_array_equal(M, M0)
     assert e0.vlist_stats()["cells"] == 0  # the r03 sweep really ran there
-    assert stats[0]["cells"] > 0 and stats[0]["pending"] > 0
-    if eager:
-        assert stats[0]["requested"] > 0 and stats[1]["requested"] == 0, stats[:2]
-    else:
-        assert stats[0]["requested"] == 0 and stats[1]["requested"] > 0, stats[:2]
+    if eager:  # sweep 0: r03 sweep (no list state); sweep 1 builds every cell it queries
+        assert stats[0]["lists"] == 0 and stats[0]["requested"] == 0, stats[0]
+        assert stats[1]["requested"] > 0 and stats[1]["pending"] > 0, stats[1]
+    else:  # lists from the first sweep; a cell is built when a later sweep queries it again
+        assert stats[0]["requested"] == 0 and stats[0]["pending"] > 0 and stats[1]["requested"] > 0, stats[:2]
     # the third identical sweep finds every cell listed or rejected: nothing requested, and only the
     # queries of overflow cells (if any) pending
     for k in (2, 5, 8):
