@@ -400,6 +400,15 @@ struct mgicp_ctx {
   DevBuf<unsigned char> scratch;
   DevBuf<unsigned long long> u64;
   bool split_target_cov = true;     // multi-GPU: target covariances split + all-gathered (env MGICP_SPLIT_TARGET_COV)
+  // lazy source covariances (r04, env MGICP_LAZY_SRC_COV): a source point's covariance is computed the
+  // first time a sweep accepts it -- every consumer (Mahalanobis of the compaction, GN moments) reads
+  // accepted points only, so points the gate never accepts (clutter, debris far off the part) never
+  // pay PCL's exact 20-NN search; the values are the eager ones bit for bit
+  bool lazy_src_cov = true;
+  bool src_lazy_ready = false;      // cov arrays sized and cov_ok cleared for the current shard
+  size_t src_lazy_p0 = 0, src_lazy_p1 = 0;
+  DevBuf<uint8_t> cov_ok;           // per shard point: covariance computed
+  DevBuf<uint32_t> cov_need;        // this sweep's accepted points without a covariance (absolute positions)
   bool knn_logged = true;           // env MGICP_KNN2 at create: logged k-NN kernel, else register-list
   DevBuf<uint32_t> knn_fb;          // points the logged k-NN kernel leaves to the register-list one
   unsigned int knn_fallbacks = 0;   // their count in the last covariance launch
@@ -845,6 +854,7 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
   cl.dirty = false;
   cl.have_cov = false;
   if (&cl == &ctx->tgt) ctx->vl_valid = false;  // the 1-NN cell lists index the old target
+  if (&cl == &ctx->src) ctx->src_lazy_ready = false;  // lazy covariances: none computed for this cloud
   if (&cl == &ctx->src || &cl == &ctx->tgt) {  // sorted positions changed
     ctx->have_corr = false;
     ctx->seed_valid = false;
@@ -973,8 +983,67 @@ int prepare(mgicp_ctx* ctx, bool need_cov) {
   if (ctx->src.dirty && (rc = build_grid(ctx, ctx->src))) return rc;
   if (!need_cov) return MGICP_OK;
   if (!ctx->tgt.have_cov && (rc = target_cov(ctx))) return rc;
-  if (!ctx->src.have_cov || ctx->src.cov_p0 != ctx->shard_p0() || ctx->src.cov_p1 != ctx->shard_p1())
+  const bool src_cur = ctx->src.have_cov && ctx->src.cov_p0 == ctx->shard_p0() && ctx->src.cov_p1 == ctx->shard_p1();
+  if (ctx->lazy_src_cov && !src_cur) {
+    // computed per sweep for the points it accepts (src_cov_lazy); here only sized and marked empty
+    if (!ctx->src_lazy_ready || ctx->src_lazy_p0 != ctx->shard_p0() || ctx->src_lazy_p1 != ctx->shard_p1()) {
+      Cloud& c = ctx->src;
+      const size_t ns = ctx->shard_p1() - ctx->shard_p0();
+      HIPCK(c.cov.reserve(3 * c.n));
+      c.cov_stride = c.n;
+      HIPCK(ctx->cov_ok.reserve(std::max<size_t>(ns, 1)));
+      HIPCK(ctx->cov_need.reserve(std::max<size_t>(ns, 1)));
+      HIPCK(hipMemsetAsync(ctx->cov_ok.p, 0, std::max<size_t>(ns, 1), ctx->stream));
+      ctx->src_lazy_ready = true;
+      ctx->src_lazy_p0 = ctx->shard_p0();
+      ctx->src_lazy_p1 = ctx->shard_p1();
+    }
+    return MGICP_OK;
+  }
+  if (!src_cur)
     if ((rc = compute_cov(ctx, ctx->src, ctx->shard_p0(), ctx->shard_p1()))) return rc;
+  return MGICP_OK;
+}
+
+// the source covariances a sweep needs (lazy mode): its accepted points without one, computed by the
+// same kernels as the eager pass (listed queries, the register-list hand-off for the rest)
+int src_cov_lazy(mgicp_ctx* ctx) {
+  if (!ctx->lazy_src_cov || ctx->src.have_cov) return MGICP_OK;
+  const size_t p0 = ctx->shard_p0(), ns = ctx->shard_p1() - p0;
+  unsigned int* cnt = reinterpret_cast<unsigned int*>(ctx->u64.p);
+  HIPCK(ctx->u64.reserve(1));
+  cnt = reinterpret_cast<unsigned int*>(ctx->u64.p);
+  HIPCK(launch_cov_need(ctx->flags.p, ctx->cov_ok.p, p0, ns, ctx->cov_need.p, cnt, ctx->stream));
+  HIPCK(hipMemcpyAsync(ctx->h_small, cnt, sizeof(unsigned int), hipMemcpyDeviceToHost, ctx->stream));
+  int rc = sync(ctx);
+  if (rc) return rc;
+  unsigned int need = 0;
+  std::memcpy(&need, ctx->h_small, sizeof(need));
+  if (!need) return MGICP_OK;
+  Cloud& cl = ctx->src;
+  const bool logged = ctx->knn_logged;
+  unsigned int* fb_count = cnt;
+  if (logged) {
+    HIPCK(ctx->knn_fb.reserve(need));
+    HIPCK(hipMemsetAsync(fb_count, 0, sizeof(unsigned int), ctx->stream));
+  }
+  {
+    ProfScope ps(ctx, kFamCov);
+    HIPCK(launch_knn_cov(cl.view, ctx->prm.k, ctx->prm.gicp_eps, 0, need, cl.cov3(), ctx->cov_need.p,
+                         logged ? ctx->knn_fb.p : nullptr, logged ? fb_count : nullptr, ctx->stream));
+  }
+  if (logged) {
+    HIPCK(hipMemcpyAsync(ctx->h_small, fb_count, sizeof(unsigned int), hipMemcpyDeviceToHost, ctx->stream));
+    if ((rc = sync(ctx))) return rc;
+    unsigned int nfb = 0;
+    std::memcpy(&nfb, ctx->h_small, sizeof(nfb));
+    ctx->knn_fallbacks = nfb;
+    if (nfb) {
+      ProfScope ps(ctx, kFamCov);
+      HIPCK(launch_knn_cov(cl.view, ctx->prm.k, ctx->prm.gicp_eps, 0, nfb, cl.cov3(), ctx->knn_fb.p, nullptr, nullptr,
+                           ctx->stream));
+    }
+  }
   return MGICP_OK;
 }
 
@@ -1505,6 +1574,10 @@ int correspond(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
                    st[1] ? double(st[5]) / st[1] : 0.0, st[2] ? double(st[6]) / st[2] : 0.0);
   }
 #endif
+  {
+    int rc = src_cov_lazy(ctx);  // covariances of newly accepted source points (lazy mode)
+    if (rc) return rc;
+  }
   const size_t sb = scan_scratch_bytes(ns + 1);
   HIPCK(launch_exclusive_scan(ctx->cscratch.p, sb, ctx->flags.p, ctx->cpos.p, ns + 1, s));
   {
@@ -1818,6 +1891,8 @@ int correspond_gn(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
   }
   ctx->seed_valid = true;
   ctx->have_corr = false;  // the SoA streams of the BFGS mode are not refreshed
+  int rc = src_cov_lazy(ctx);
+  if (rc) return rc;
   return moments_pass(ctx, T, G);
 }
 
@@ -1978,6 +2053,7 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
   if (const char* vs = std::getenv("MGICP_VLIST_STATS")) ctx->vl_stats = std::atoi(vs) != 0;
   if (const char* ve = std::getenv("MGICP_VLIST_EAGER")) ctx->vl_eager = std::atoi(ve) != 0;
   if (const char* vc = std::getenv("MGICP_VLIST_COLD")) ctx->vl_cold_r03 = std::atoi(vc) != 0;
+  if (const char* lc = std::getenv("MGICP_LAZY_SRC_COV")) ctx->lazy_src_cov = std::atoi(lc) != 0;
   ctx->tgt.want_pairs = ctx->corr_wave;
   if (const char* cb = std::getenv("MGICP_CELL_BOXES")) ctx->tgt.want_boxes = std::atoi(cb) != 0;
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -2009,6 +2085,7 @@ int mgicp_set_params(mgicp_ctx* ctx, const mgicp_params* p) {
   if (cov_change) {
     ctx->src.have_cov = false;
     ctx->tgt.have_cov = false;
+    ctx->src_lazy_ready = false;
   }
   return MGICP_OK;
 }
@@ -2041,6 +2118,7 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   ctx->nn_work.release(); ctx->nn_work_n.release();
   ctx->vl_cell.release(); ctx->vl_pool.release(); ctx->vl_ctr.release();
   ctx->vl_build.release(); ctx->vl_bcentre.release(); ctx->vl_pend.release();
+  ctx->cov_ok.release(); ctx->cov_need.release();
   ctx->tpart.release();
   ctx->tpart_n = 0;
   ctx->corr_f.release(); ctx->corr_d.release(); ctx->cscratch.release();
@@ -2538,6 +2616,7 @@ int mgicp_comm_init(mgicp_ctx* ctx, int nranks, int rank, const unsigned char id
   ctx->nranks = nranks;
   ctx->rank = rank;
   ctx->qperm_valid = false;
+  ctx->src_lazy_ready = false;
   ctx->src.have_cov = false;
   ctx->have_corr = false;
   ctx->seed_valid = false;  // the shard (and its per-point match buffers) changes
@@ -2667,6 +2746,11 @@ int mgicp_debug_covariances(mgicp_ctx* ctx, int which, double* out_c6) {
   HIPCK(hipSetDevice(ctx->device));
   int rc = prepare(ctx, true);
   if (rc) return rc;
+  if (which == 0 && !(ctx->src.have_cov && ctx->src.cov_p0 == ctx->shard_p0() && ctx->src.cov_p1 == ctx->shard_p1())) {
+    // every source covariance (lazy mode computes only the accepted points' ones)
+    if ((rc = compute_cov(ctx, ctx->src, ctx->shard_p0(), ctx->shard_p1()))) return rc;
+    if (ctx->src_lazy_ready) HIPCK(hipMemsetAsync(ctx->cov_ok.p, 1, ctx->shard_p1() - ctx->shard_p0(), ctx->stream));
+  }
   Cloud& cl = which ? ctx->tgt : ctx->src;
   const size_t n = cl.n;
   const size_t st = cl.cov_stride;

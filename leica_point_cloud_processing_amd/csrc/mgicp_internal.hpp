@@ -183,6 +183,10 @@ struct VListView {
 hipError_t launch_vl_sweep(const GridView& tgt, const VListView& vl, const float4* src, size_t p0, size_t p1,
                            Xf34 T, double thr, int seeded, uint32_t* nn_pos, uint32_t* flags, int cus,
                            hipStream_t s);
+// lazy source covariances (r04): shard positions k with flags[k] && !cov_ok[k] -> list (absolute
+// positions p0 + k, *count of them), cov_ok[k] = 1
+hipError_t launch_cov_need(const uint32_t* flags, uint8_t* cov_ok, size_t p0, size_t n, uint32_t* list,
+                           unsigned int* count, hipStream_t s);
 // diagnostics (env MGICP_VLIST_STATS): per built cell list lengths histogram etc. into out[64]
 hipError_t launch_vl_stats(const VListView& vl, size_t ncells, unsigned long long* out /*device, 64*/, hipStream_t s);
 size_t     pair_count(size_t n);

@@ -3544,6 +3544,33 @@ hipError_t launch_vl_sweep(const GridView& tgt, const VListView& vl, const float
   return hipGetLastError();
 }
 
+// lazy source covariances: the accepted points of a sweep whose covariance was never computed
+__global__ void cov_need_kernel(const uint32_t* __restrict__ flags, uint8_t* __restrict__ cov_ok, size_t p0, size_t n,
+                                uint32_t* __restrict__ list, unsigned int* __restrict__ count) {
+  const size_t k = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const bool need = k < n && flags[k] && !cov_ok[k];
+  const unsigned long long m = __builtin_amdgcn_ballot_w64(need);
+  if (!m) return;
+  const int lane = threadIdx.x & 63;
+  unsigned int base = 0;
+  if (lane == 0) base = atomicAdd(count, static_cast<unsigned int>(__builtin_popcountll(m)));
+  base = __builtin_amdgcn_readfirstlane(base);
+  if (need) {
+    const unsigned int o = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned int>(m >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo(static_cast<unsigned int>(m), 0u));
+    list[base + o] = static_cast<uint32_t>(p0 + k);
+    cov_ok[k] = 1;
+  }
+}
+
+hipError_t launch_cov_need(const uint32_t* flags, uint8_t* cov_ok, size_t p0, size_t n, uint32_t* list,
+                           unsigned int* count, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(count, 0, sizeof(unsigned int), s);
+  if (e != hipSuccess || n == 0) return e;
+  cov_need_kernel<<<nblk(n), 256, 0, s>>>(flags, cov_ok, p0, n, list, count);
+  return hipGetLastError();
+}
+
 hipError_t launch_vl_stats(const VListView& vl, size_t ncells, unsigned long long* out, hipStream_t s) {
   hipError_t e = hipMemsetAsync(out, 0, 64 * sizeof(unsigned long long), s);
   if (e != hipSuccess) return e;

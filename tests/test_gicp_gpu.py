@@ -541,3 +541,32 @@ def test_vlist_invalidated_by_new_target_and_gate(engine_mod, part_small):
         f2.close()
     e.close()
     f.close()
+
+
+def test_lazy_source_covariances_match_eager(engine_mod, monkeypatch):
+    """r04 lazy source covariances: a source point's covariance is computed the first time a sweep
+    accepts it (clutter the gate never accepts never pays the 20-NN search).  On a scan with 4 %
+    clutter and debris the align -- T, iterations, passes, the last correspondences and their
+    Mahalanobis matrices -- is bitwise the eager computation's (MGICP_LAZY_SRC_COV=0)."""
+    from leica_point_cloud_processing_amd import synth
+
+    scan, cad, _ = synth.scan_vs_cad(60_000, 60_000, clutter=0.04, debris=600)
+    res = {}
+    for lazy in (1, 0):
+        monkeypatch.setenv("MGICP_LAZY_SRC_COV", str(lazy))
+        e = engine_mod()
+        e.set_source_xyz(scan)
+        e.set_target_xyz(cad)
+        T = e.align()
+        r = dict(e.last_result)
+        T2 = e.align()  # iterate(): cached state
+        m, tj, M = e.debug_correspondences(T, len(scan))
+        res[lazy] = (T, T2, r["iterations"], r["n_evals"], r["n_corr"], m, tj, M)
+        e.close()
+    a, b = res[1], res[0]
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1], b[1])
+    assert a[2:6] == b[2:6]
+    assert a[4] < len(scan)  # the clutter is rejected
+    np.testing.assert_array_equal(a[6], b[6])
+    np.testing.assert_array_equal(a[7], b[7])
