@@ -560,10 +560,9 @@ void cancel_gated(mgicp_ctx* ctx) {
     // host-row passes leave the tickets as multiples of their supers' sizes: re-arm them for the
     // launched passes (stream order: after the server has exited)
     (void)hipMemsetAsync(ctx->tickets.p, 0, ctx->tickets_n * sizeof(unsigned int), ctx->stream);
-    if (ctx->srv_locked) {  // the device's server slot is free for the next BFGS run (any context)
-      g_srv_busy[ctx->device & 63].store(0, std::memory_order_release);
-      ctx->srv_locked = false;
-    }
+    // the device's server slot stays with this context until its stream has drained (sync): a
+    // cancelled server may still be finishing, and another context's server must not start beside
+    // it; this context's next BFGS run re-launches behind it in stream order
   }
   if (!ctx->gated_seq) return;
   publish_cmd(ctx, ctx->gated_seq, kPassCancel, 0, nullptr);
@@ -589,6 +588,10 @@ void srv_resolve(mgicp_ctx* ctx) {
 int sync(mgicp_ctx* ctx) {
   cancel_gated(ctx);  // a queued gated pass would otherwise hold the stream until its timeout
   HIPCK(hipStreamSynchronize(ctx->stream));
+  if (ctx->srv_locked && !ctx->srv_live) {  // the stream drained: no server of this context is running
+    g_srv_busy[ctx->device & 63].store(0, std::memory_order_release);
+    ctx->srv_locked = false;
+  }
   if (ctx->profiling) prof_resolve(ctx);
   if (!ctx->srv_ev.empty()) srv_resolve(ctx);
   return MGICP_OK;
@@ -1638,7 +1641,7 @@ struct DeviceFunctor {
     // the host rows first: a failure here (e.g. a source larger than the shared segment) must not
     // leave the device's server slot taken
     if (!ctx->srv_live && (shm_rows || (nsrv > 0 && ctx->host_rows)) && (rc = ensure_rows(ctx))) return rc;
-    if (nsrv > 0 && !ctx->srv_live) {
+    if (nsrv > 0 && !ctx->srv_live && !ctx->srv_locked) {
       int idle = 0;  // one server per device and process (g_srv_busy)
       ctx->srv_locked = g_srv_busy[ctx->device & 63].compare_exchange_strong(idle, 1, std::memory_order_acq_rel);
       if (!ctx->srv_locked) {

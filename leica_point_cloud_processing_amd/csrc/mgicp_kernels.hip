@@ -2639,7 +2639,7 @@ __device__ __forceinline__ double lane_from(double x, int q) {  // lane v < 16: 
 
 __device__ __forceinline__ bool super_sum_tagged(const unsigned long long* __restrict__ tpart, int sj, int nch,
                                                  int lane, unsigned int rstamp, const PassCmd* cmd, unsigned int cur,
-                                                 unsigned long long limit, double& a) {
+                                                 unsigned long long limit, double& a, bool cmd_host = true) {
   const int c0 = sj * kSuperChunks, nin = min(kSuperChunks, nch - c0);
   const int v = lane & 15, qb = 8 * (lane >> 4);
   const unsigned long long t0 = wall_clock64();
@@ -2656,7 +2656,8 @@ __device__ __forceinline__ bool super_sum_tagged(const unsigned long long* __res
     if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
     if (cmd) {
       unsigned long long c[16];
-      read_cmd<true>(cmd, c);
+      if (cmd_host) read_cmd<true>(cmd, c);
+      else read_cmd<false>(cmd, c);
       const unsigned int st = __builtin_amdgcn_readfirstlane(static_cast<unsigned int>(c[0] >> 32));
       if (static_cast<int>(st - cur) > 0) return false;  // a newer command: the host took the pass over
     }
@@ -3036,8 +3037,13 @@ __global__ __launch_bounds__(64 * kWaves, 1) void fdf_server_kernel(
     if (tagged) {
       if (w0 < nsup) {
         double a = 0.0;
-        const PassCmd* watch = !kBench && host_pollers >= static_cast<int>(gridDim.x) ? cmd : nullptr;
-        if (super_sum_tagged(tpart, w0, nch, lane, rstamp, watch, static_cast<unsigned int>(seq), timeout >> 3, a)) {
+        // a newer command means the host took this pass over: with the BAR command block every block
+        // polls it; otherwise the mailbox block 0 forwards the host's commands to (without
+        // a watch the reducers of a cancelled server spun until their timeout)
+        const bool bar_cmd = host_pollers >= static_cast<int>(gridDim.x);
+        const PassCmd* watch = kBench ? nullptr : (bar_cmd ? cmd : mail);
+        if (super_sum_tagged(tpart, w0, nch, lane, rstamp, watch, static_cast<unsigned int>(seq), timeout >> 3, a,
+                             bar_cmd)) {
           // the super's row, as wave_tickets writes it: lane l < 32 stores half l & 1 of value l >> 1
           const long long bits = __double_as_longlong(__shfl(a, lane >> 1, 64));
           const unsigned int half = static_cast<unsigned int>((lane & 1) ? (bits >> 32) : bits);
