@@ -415,7 +415,7 @@ struct mgicp_ctx {
   DevBuf<float> fpartial;
   // the target's 1-NN cell lists (r04, DESIGN.md "1-NN cell lists"; env MGICP_VLIST=0: the r03 sweeps)
   bool vlist = true;
-  float vlist_cell = 0.75f;           // fine cell edge / the target grid's cell edge (env MGICP_VLIST_CELL)
+  float vlist_cell = 0.6f;            // fine cell edge / the target grid's cell edge (env MGICP_VLIST_CELL)
   bool vl_stats = false;              // env MGICP_VLIST_STATS: per-sweep list diagnostics on stderr
   bool vl_valid = false;              // lists belong to the current target grid and gate
   bool vl_off = false;                // the gate is too large for a fine grid of this target: r03 sweeps
@@ -585,13 +585,18 @@ void srv_resolve(mgicp_ctx* ctx) {
   ctx->srv_ev.clear();
 }
 
-int sync(mgicp_ctx* ctx) {
-  cancel_gated(ctx);  // a queued gated pass would otherwise hold the stream until its timeout
-  HIPCK(hipStreamSynchronize(ctx->stream));
-  if (ctx->srv_locked && !ctx->srv_live) {  // the stream drained: no server of this context is running
+// after a stream drain: no server of this context is running, the device's slot is free again
+void srv_release(mgicp_ctx* ctx) {
+  if (ctx->srv_locked && !ctx->srv_live) {
     g_srv_busy[ctx->device & 63].store(0, std::memory_order_release);
     ctx->srv_locked = false;
   }
+}
+
+int sync(mgicp_ctx* ctx) {
+  cancel_gated(ctx);  // a queued gated pass would otherwise hold the stream until its timeout
+  HIPCK(hipStreamSynchronize(ctx->stream));
+  srv_release(ctx);
   if (ctx->profiling) prof_resolve(ctx);
   if (!ctx->srv_ev.empty()) srv_resolve(ctx);
   return MGICP_OK;
@@ -2100,6 +2105,7 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   cancel_gated(ctx);
   (void)hipStreamSynchronize(ctx->stream);
+  srv_release(ctx);
   ctx->f_flags.release(); ctx->f_pos.release(); ctx->f_rgba_in.release(); ctx->f_rgba.release();
   ctx->f_rgba2.release(); ctx->f_vox.release(); ctx->f_vox2.release(); ctx->f_keep.release();
   ctx->f_count.release();
@@ -3040,6 +3046,7 @@ int mgicp_set_profiling(mgicp_ctx* ctx, int on) {
   (void)hipSetDevice(ctx->device);
   cancel_gated(ctx);
   (void)hipStreamSynchronize(ctx->stream);
+  srv_release(ctx);
   prof_resolve(ctx);
   ctx->profiling = on != 0;
   ctx->prof_tick = 0;

@@ -1596,6 +1596,10 @@ __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_kernel(GridV
 // real point, no closer than the true 1-NN).  Queries outside the fine grid, or in a cell with no
 // target point within D(1 + 1e-5) + its half diagonal of the centre, are rejected.
 constexpr int kVlCand = 1024;  // candidates a build wave keeps in LDS (more: the cell stays a fallback cell)
+#ifndef MGICP_VLIST_BATCH
+#define MGICP_VLIST_BATCH 4  // list entries a query loads per round (a multiple of 4)
+#endif
+constexpr int kVlBatch = MGICP_VLIST_BATCH;
 
 __device__ __forceinline__ void vl_cell_xyz(const VListView& v, uint32_t ci, uint32_t& ix, uint32_t& iy, uint32_t& iz) {
   const uint32_t nx = static_cast<uint32_t>(v.nx), ny = static_cast<uint32_t>(v.ny);
@@ -1667,17 +1671,18 @@ __global__ __launch_bounds__(256) void vl_query_kernel(VListView v, const float4
       cnt = __float_as_uint(v.pool[off].x);
       off += 4;
     }
-    // lists are padded to a multiple of 4 with far sentinels (d2 = inf): 8 entries per round in flight
+    // lists are padded to a multiple of 4 with far sentinels (d2 = inf): kVlBatch entries per round in
+    // flight (groups of 4 past the list's end are not loaded)
     const float4* e = v.pool + off;
-    for (uint32_t j = 0; j < cnt; j += 8) {
-      float4 a[8];
+    for (uint32_t j = 0; j < cnt; j += kVlBatch) {
+      float4 a[kVlBatch];
 #pragma unroll
       for (int u = 0; u < 4; ++u) a[u] = e[j + u];
-      const bool two = j + 4 < cnt;
 #pragma unroll
-      for (int u = 4; u < 8; ++u) a[u] = two ? e[j + u] : make_float4(3.0e38f, 3.0e38f, 3.0e38f, 0.f);
+      for (int u = 4; u < kVlBatch; ++u)
+        a[u] = j + (u & ~3) < cnt ? e[j + u] : make_float4(3.0e38f, 3.0e38f, 3.0e38f, 0.f);
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < kVlBatch; ++u) {
         const float d = dist2(qx, qy, qz, a[u]);
         const uint32_t pu = __float_as_uint(a[u].w);
         if (d < bd) {
