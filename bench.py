@@ -458,10 +458,15 @@ def main():
         # pass server off), then the covariance kernels' times from a profiled repeat
         eng2 = GICPEngine(device=local, max_iter=args.max_iter, fixed_iterations=int(args.fixed))
         t_n = time.perf_counter()
-        eng2.set_target_xyz(cad)
-        eng2.set_source_xyz(scan)
+        eng2.set_target_xyz(cad)  # r04: uploads, builds the grid, starts the covariances (2nd stream)
+        t_t = time.perf_counter()
+        eng2.set_source_xyz(scan)  # the same for the source, beside the target's covariances
+        t_s = time.perf_counter()
         eng2.align()
-        new_clouds = {"ms_wall": round(1e3 * (time.perf_counter() - t_n), 3),
+        t_a = time.perf_counter()
+        new_clouds = {"ms_wall": round(1e3 * (t_a - t_n), 3),
+                      "ms_set_target": round(1e3 * (t_t - t_n), 3), "ms_set_source": round(1e3 * (t_s - t_t), 3),
+                      "ms_align": round(1e3 * (t_a - t_s), 3),
                       **{k: round(eng2.last_result[k], 3) for k in ("ms_upload", "ms_prep", "ms_loop")}}
         eng2.set_profiling(True)
         eng2.set_target_xyz(cad)  # new clouds: the covariances are recomputed under events

@@ -409,6 +409,25 @@ struct mgicp_ctx {
   size_t src_lazy_p0 = 0, src_lazy_p1 = 0;
   DevBuf<uint8_t> cov_ok;           // per shard point: covariance computed
   DevBuf<uint32_t> cov_need;        // this sweep's accepted points without a covariance (absolute positions)
+  // lazy target covariances (r04, single rank; env MGICP_LAZY_TGT_COV=1, default off): the first align after
+  // a set_target computes the covariances of the target points its sweeps match; the next align
+  // computes the rest, so later sweeps run without any check
+  bool lazy_tgt_cov = false;         // measured at C4: no gain (the matched set grows every sweep), DESIGN.md
+  bool tgt_lazy = false;            // the target's covariances are being computed per sweep
+  int tgt_lazy_aligns = 0;          // aligns run since the lazy target was set up
+  DevBuf<uint8_t> tcov_ok;          // per target sorted position: 0 none, 2 matched this sweep, 1 computed
+  DevBuf<uint32_t> tcov_need;       // this sweep's target points to compute (sorted positions)
+  // r04: set_target builds the target's grid and starts its k-NN covariances on a second stream, so
+  // they run while the caller uploads the source; prepare joins them (env MGICP_ASYNC_COV=0: off)
+  bool async_tgt = true;
+  // (and set_source the source's: single rank, same stream; with the lazy source mode these cover
+  // every point, computed while the first sweep runs)
+  bool tgt_cov_pending = false;     // the aux stream's covariance launches not joined yet
+  bool src_cov_pending = false;
+  hipStream_t aux_stream = nullptr;
+  hipEvent_t aux_ev[2] = {nullptr, nullptr};  // completion of the target's [0] / source's [1] launch
+  DevBuf<unsigned int> aux_cnt;     // their hand-off counts: [0] target, [1] source
+  DevBuf<uint32_t> knn_fb2;         // the source's hand-off list
   bool knn_logged = true;           // env MGICP_KNN2 at create: logged k-NN kernel, else register-list
   DevBuf<uint32_t> knn_fb;          // points the logged k-NN kernel leaves to the register-list one
   unsigned int knn_fallbacks = 0;   // their count in the last covariance launch
@@ -620,12 +639,73 @@ int reset_stamps(mgicp_ctx* ctx) {
 }
 
 // Upload strided host records (or copy device records) and pack to float4 (original order).
+int build_grid(mgicp_ctx* ctx, Cloud& cl);
+
+// the covariances started by cov_prep_async: wait for the aux stream, then hand the points the
+// logged kernel left (log overflow, ties at the k-th distance) to the register-list kernel on the
+// main stream -- the same two launches as compute_cov
+int cov_join(mgicp_ctx* ctx, bool tgt) {
+  bool& pending = tgt ? ctx->tgt_cov_pending : ctx->src_cov_pending;
+  if (!pending) return MGICP_OK;
+  pending = false;
+  Cloud& c = tgt ? ctx->tgt : ctx->src;
+  HIPCK(hipEventSynchronize(ctx->aux_ev[tgt ? 0 : 1]));  // this cloud's launch only
+  if (ctx->knn_logged) {
+    unsigned int nfb = 0;
+    HIPCK(hipMemcpy(&nfb, ctx->aux_cnt.p + (tgt ? 0 : 1), sizeof(nfb), hipMemcpyDeviceToHost));
+    ctx->knn_fallbacks = nfb;
+    if (nfb) {
+      ProfScope ps(ctx, kFamCov);
+      HIPCK(launch_knn_cov(c.view, ctx->prm.k, ctx->prm.gicp_eps, 0, nfb, c.cov3(), tgt ? ctx->knn_fb.p : ctx->knn_fb2.p,
+                           nullptr, nullptr, ctx->stream));
+    }
+  }
+  c.have_cov = true;
+  c.cov_p0 = 0;
+  c.cov_p1 = c.n;
+  return MGICP_OK;
+}
+int cov_join_all(mgicp_ctx* ctx) {
+  const int rc = cov_join(ctx, true);
+  return rc ? rc : cov_join(ctx, false);
+}
+
+// set_target's / set_source's head start (single rank, eager target covariances, not profiling): the
+// cloud's grid now (its host round trips), then its k-NN covariances on the aux stream -- the
+// target's overlap the source's upload and grid build, the source's the first 1-NN sweep.  Any
+// failure leaves the cloud for prepare, which reports it as before.
+int cov_prep_async(mgicp_ctx* ctx, bool tgt) {
+  Cloud& c = tgt ? ctx->tgt : ctx->src;
+  if (!ctx->async_tgt || !ctx->aux_stream || ctx->nranks != 1 || ctx->comm || ctx->have_shm || ctx->profiling ||
+      (tgt && ctx->lazy_tgt_cov) || static_cast<size_t>(ctx->prm.k) > c.n)
+    return MGICP_OK;
+  if (build_grid(ctx, c) != MGICP_OK || c.n < static_cast<size_t>(ctx->prm.k)) return MGICP_OK;
+  HIPCK(c.cov.reserve(3 * c.n));
+  c.cov_stride = c.n;
+  if (ctx->knn_logged) {
+    HIPCK((tgt ? ctx->knn_fb : ctx->knn_fb2).reserve(c.n));
+    HIPCK(ctx->aux_cnt.reserve(2));
+    HIPCK(hipMemsetAsync(ctx->aux_cnt.p + (tgt ? 0 : 1), 0, sizeof(unsigned int), ctx->stream));
+  }
+  HIPCK(hipStreamSynchronize(ctx->stream));  // the grid (and the count) before the aux stream reads them
+  HIPCK(launch_knn_cov(c.view, ctx->prm.k, ctx->prm.gicp_eps, 0, c.n, c.cov3(), nullptr,
+                       ctx->knn_logged ? (tgt ? ctx->knn_fb.p : ctx->knn_fb2.p) : nullptr,
+                       ctx->knn_logged ? ctx->aux_cnt.p + (tgt ? 0 : 1) : nullptr, ctx->aux_stream));
+  HIPCK(hipEventRecord(ctx->aux_ev[tgt ? 0 : 1], ctx->aux_stream));
+  (tgt ? ctx->tgt_cov_pending : ctx->src_cov_pending) = true;
+  return MGICP_OK;
+}
+
 int upload_cloud(mgicp_ctx* ctx, Cloud& cl, const float* xyz, size_t n, size_t stride,
                  bool device_ptr) {
   if (n == 0 || !xyz || stride < 12 || (stride % 4) != 0)
     return fail(ctx, MGICP_E_INVALID, "invalid cloud (null, empty or stride not a multiple of 4 >= 12)");
   if (n >= (size_t(1) << 31) - 1)  // 32-bit point indices / hipcub item counts
     return fail(ctx, MGICP_E_INVALID, "cloud too large: at most 2^31 - 2 points per cloud");
+  if (&cl == &ctx->tgt || &cl == &ctx->src) {  // an async covariance launch still reads the old cloud
+    const int rj = cov_join(ctx, &cl == &ctx->tgt);
+    if (rj) return rj;
+  }
   const double t0 = now_ms();
   MGICP_TRACE_AT("upload: begin");
   HIPCK(cl.orig.reserve(n));
@@ -863,6 +943,7 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
   cl.have_cov = false;
   if (&cl == &ctx->tgt) ctx->vl_valid = false;  // the 1-NN cell lists index the old target
   if (&cl == &ctx->src) ctx->src_lazy_ready = false;  // lazy covariances: none computed for this cloud
+  if (&cl == &ctx->tgt) ctx->tgt_lazy = false;
   if (&cl == &ctx->src || &cl == &ctx->tgt) {  // sorted positions changed
     ctx->have_corr = false;
     ctx->seed_valid = false;
@@ -989,11 +1070,30 @@ int prepare(mgicp_ctx* ctx, bool need_cov) {
   int rc;
   if (ctx->tgt.dirty && (rc = build_grid(ctx, ctx->tgt))) return rc;
   if (ctx->src.dirty && (rc = build_grid(ctx, ctx->src))) return rc;
+  if ((rc = cov_join(ctx, true))) return rc;  // set_target's covariances (after the source grid: overlapped)
   if (!need_cov) return MGICP_OK;
-  if (!ctx->tgt.have_cov && (rc = target_cov(ctx))) return rc;
-  const bool src_cur = ctx->src.have_cov && ctx->src.cov_p0 == ctx->shard_p0() && ctx->src.cov_p1 == ctx->shard_p1();
+  if (!ctx->tgt.have_cov && !ctx->tgt_lazy) {
+    if (ctx->lazy_tgt_cov && ctx->nranks == 1 && !ctx->comm && !ctx->have_shm) {
+      // computed per sweep for the target points the first align's sweeps match (cov_lazy)
+      Cloud& t = ctx->tgt;
+      HIPCK(t.cov.reserve(3 * t.n));
+      t.cov_stride = t.n;
+      t.cov_p0 = 0;
+      t.cov_p1 = t.n;
+      HIPCK(ctx->tcov_ok.reserve(t.n));
+      HIPCK(ctx->tcov_need.reserve(t.n));
+      HIPCK(hipMemsetAsync(ctx->tcov_ok.p, 0, t.n, ctx->stream));
+      ctx->tgt_lazy = true;
+      ctx->tgt_lazy_aligns = 0;
+    } else if ((rc = target_cov(ctx))) {
+      return rc;
+    }
+  }
+  // set_source's covariances still running count as current: the sweep joins them (overlapped)
+  const bool src_cur = ctx->src_cov_pending ||
+                       (ctx->src.have_cov && ctx->src.cov_p0 == ctx->shard_p0() && ctx->src.cov_p1 == ctx->shard_p1());
   if (ctx->lazy_src_cov && !src_cur) {
-    // computed per sweep for the points it accepts (src_cov_lazy); here only sized and marked empty
+    // computed per sweep for the points it accepts (cov_lazy); here only sized and marked empty
     if (!ctx->src_lazy_ready || ctx->src_lazy_p0 != ctx->shard_p0() || ctx->src_lazy_p1 != ctx->shard_p1()) {
       Cloud& c = ctx->src;
       const size_t ns = ctx->shard_p1() - ctx->shard_p0();
@@ -1013,44 +1113,58 @@ int prepare(mgicp_ctx* ctx, bool need_cov) {
   return MGICP_OK;
 }
 
-// the source covariances a sweep needs (lazy mode): its accepted points without one, computed by the
-// same kernels as the eager pass (listed queries, the register-list hand-off for the rest)
-int src_cov_lazy(mgicp_ctx* ctx) {
-  if (!ctx->lazy_src_cov || ctx->src.have_cov) return MGICP_OK;
+// the covariances a sweep needs (lazy modes): its accepted source points without one, and the
+// target points they matched without one (tgt_rest: every target point still without one), computed
+// by the same kernels as the eager passes (logged k-NN, the register-list hand-off for the rest)
+int cov_lazy(mgicp_ctx* ctx, bool tgt_rest = false) {
+  const bool do_src = ctx->lazy_src_cov && !ctx->src.have_cov && !tgt_rest;
+  const bool do_tgt = ctx->tgt_lazy;
+  if (!do_src && !do_tgt) return MGICP_OK;
   const size_t p0 = ctx->shard_p0(), ns = ctx->shard_p1() - p0;
-  unsigned int* cnt = reinterpret_cast<unsigned int*>(ctx->u64.p);
-  HIPCK(ctx->u64.reserve(1));
-  cnt = reinterpret_cast<unsigned int*>(ctx->u64.p);
-  HIPCK(launch_cov_need(ctx->flags.p, ctx->cov_ok.p, p0, ns, ctx->cov_need.p, cnt, ctx->stream));
-  HIPCK(hipMemcpyAsync(ctx->h_small, cnt, sizeof(unsigned int), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCK(ctx->u64.reserve(2));
+  unsigned int* cnt = reinterpret_cast<unsigned int*>(ctx->u64.p);  // [0] source, [1] target, [2..3] hand-offs
+  HIPCK(hipMemsetAsync(cnt, 0, 4 * sizeof(unsigned int), ctx->stream));
+  if (do_src) HIPCK(launch_cov_need(ctx->flags.p, ctx->cov_ok.p, p0, ns, ctx->cov_need.p, cnt, ctx->stream));
+  if (do_tgt)
+    HIPCK(launch_tgt_cov_need(ctx->flags.p, ctx->prev_pos.p, tgt_rest ? 0 : ns, ctx->tcov_ok.p, ctx->tgt.n,
+                              tgt_rest ? 1 : 0, ctx->tcov_need.p, cnt + 1, ctx->stream));
+  HIPCK(hipMemcpyAsync(ctx->h_small, cnt, 2 * sizeof(unsigned int), hipMemcpyDeviceToHost, ctx->stream));
   int rc = sync(ctx);
   if (rc) return rc;
-  unsigned int need = 0;
-  std::memcpy(&need, ctx->h_small, sizeof(need));
-  if (!need) return MGICP_OK;
-  Cloud& cl = ctx->src;
+  unsigned int need[2] = {0, 0};
+  std::memcpy(need, ctx->h_small, sizeof(need));
   const bool logged = ctx->knn_logged;
-  unsigned int* fb_count = cnt;
-  if (logged) {
-    HIPCK(ctx->knn_fb.reserve(need));
-    HIPCK(hipMemsetAsync(fb_count, 0, sizeof(unsigned int), ctx->stream));
-  }
-  {
-    ProfScope ps(ctx, kFamCov);
-    HIPCK(launch_knn_cov(cl.view, ctx->prm.k, ctx->prm.gicp_eps, 0, need, cl.cov3(), ctx->cov_need.p,
-                         logged ? ctx->knn_fb.p : nullptr, logged ? fb_count : nullptr, ctx->stream));
-  }
-  if (logged) {
-    HIPCK(hipMemcpyAsync(ctx->h_small, fb_count, sizeof(unsigned int), hipMemcpyDeviceToHost, ctx->stream));
-    if ((rc = sync(ctx))) return rc;
-    unsigned int nfb = 0;
-    std::memcpy(&nfb, ctx->h_small, sizeof(nfb));
-    ctx->knn_fallbacks = nfb;
-    if (nfb) {
+  if (need[0] || need[1]) {
+    if (logged) HIPCK(ctx->knn_fb.reserve(static_cast<size_t>(need[0]) + need[1]));
+    {
       ProfScope ps(ctx, kFamCov);
-      HIPCK(launch_knn_cov(cl.view, ctx->prm.k, ctx->prm.gicp_eps, 0, nfb, cl.cov3(), ctx->knn_fb.p, nullptr, nullptr,
-                           ctx->stream));
+      if (need[0])
+        HIPCK(launch_knn_cov(ctx->src.view, ctx->prm.k, ctx->prm.gicp_eps, 0, need[0], ctx->src.cov3(),
+                             ctx->cov_need.p, logged ? ctx->knn_fb.p : nullptr, logged ? cnt + 2 : nullptr,
+                             ctx->stream));
+      if (need[1])
+        HIPCK(launch_knn_cov(ctx->tgt.view, ctx->prm.k, ctx->prm.gicp_eps, 0, need[1], ctx->tgt.cov3(),
+                             ctx->tcov_need.p, logged ? ctx->knn_fb.p + need[0] : nullptr,
+                             logged ? cnt + 3 : nullptr, ctx->stream));
     }
+    if (logged) {
+      HIPCK(hipMemcpyAsync(ctx->h_small, cnt + 2, 2 * sizeof(unsigned int), hipMemcpyDeviceToHost, ctx->stream));
+      if ((rc = sync(ctx))) return rc;
+      unsigned int nfb[2] = {0, 0};
+      std::memcpy(nfb, ctx->h_small, sizeof(nfb));
+      ctx->knn_fallbacks = nfb[0] + nfb[1];
+      ProfScope ps(ctx, kFamCov);
+      if (nfb[0])
+        HIPCK(launch_knn_cov(ctx->src.view, ctx->prm.k, ctx->prm.gicp_eps, 0, nfb[0], ctx->src.cov3(), ctx->knn_fb.p,
+                             nullptr, nullptr, ctx->stream));
+      if (nfb[1])
+        HIPCK(launch_knn_cov(ctx->tgt.view, ctx->prm.k, ctx->prm.gicp_eps, 0, nfb[1], ctx->tgt.cov3(),
+                             ctx->knn_fb.p + need[0], nullptr, nullptr, ctx->stream));
+    }
+  }
+  if (tgt_rest) {  // every target covariance is computed: later sweeps skip the checks
+    ctx->tgt_lazy = false;
+    ctx->tgt.have_cov = true;
   }
   return MGICP_OK;
 }
@@ -1583,7 +1697,9 @@ int correspond(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
   }
 #endif
   {
-    int rc = src_cov_lazy(ctx);  // covariances of newly accepted source points (lazy mode)
+    int rc = cov_join(ctx, false);  // set_source's covariances (they ran beside this sweep)
+    if (rc) return rc;
+    rc = cov_lazy(ctx);  // covariances of newly accepted source points / matched target points (lazy modes)
     if (rc) return rc;
   }
   const size_t sb = scan_scratch_bytes(ns + 1);
@@ -1899,8 +2015,9 @@ int correspond_gn(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
   }
   ctx->seed_valid = true;
   ctx->have_corr = false;  // the SoA streams of the BFGS mode are not refreshed
-  int rc = src_cov_lazy(ctx);
+  int rc = cov_join(ctx, false);
   if (rc) return rc;
+  if ((rc = cov_lazy(ctx))) return rc;
   return moments_pass(ctx, T, G);
 }
 
@@ -2062,6 +2179,8 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
   if (const char* ve = std::getenv("MGICP_VLIST_EAGER")) ctx->vl_eager = std::atoi(ve) != 0;
   if (const char* vc = std::getenv("MGICP_VLIST_COLD")) ctx->vl_cold_r03 = std::atoi(vc) != 0;
   if (const char* lc = std::getenv("MGICP_LAZY_SRC_COV")) ctx->lazy_src_cov = std::atoi(lc) != 0;
+  if (const char* lc = std::getenv("MGICP_LAZY_TGT_COV")) ctx->lazy_tgt_cov = std::atoi(lc) != 0;
+  if (const char* at = std::getenv("MGICP_ASYNC_COV")) ctx->async_tgt = std::atoi(at) != 0;
   ctx->tgt.want_pairs = ctx->corr_wave;
   if (const char* cb = std::getenv("MGICP_CELL_BOXES")) ctx->tgt.want_boxes = std::atoi(cb) != 0;
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -2078,6 +2197,16 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
     delete ctx;
     return MGICP_E_HIP;
   }
+  // the second stream of set_target's covariance head start (created here: a stream's creation costs
+  // milliseconds of host time, which set_target would otherwise pay before the launch)
+  if (ctx->async_tgt && (hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking) != hipSuccess ||
+                         hipEventCreateWithFlags(&ctx->aux_ev[0], hipEventDisableTiming) != hipSuccess ||
+                         hipEventCreateWithFlags(&ctx->aux_ev[1], hipEventDisableTiming) != hipSuccess)) {
+    if (ctx->aux_stream) (void)hipStreamDestroy(ctx->aux_stream);
+    for (hipEvent_t& e : ctx->aux_ev)
+      if (e) (void)hipEventDestroy(e), e = nullptr;
+    ctx->aux_stream = nullptr;
+  }
   *out = ctx;
   return MGICP_OK;
 }
@@ -2086,6 +2215,7 @@ int mgicp_set_params(mgicp_ctx* ctx, const mgicp_params* p) {
   if (!ctx || !p) return MGICP_E_INVALID;
   int rc = check_params(ctx, *p);
   if (rc) return rc;
+  if ((rc = cov_join_all(ctx))) return rc;  // a pending covariance launch uses the old k / eps
   const bool cov_change = p->k != ctx->prm.k || p->gicp_eps != ctx->prm.gicp_eps;
   const int dev = ctx->device;
   ctx->prm = *p;
@@ -2093,6 +2223,7 @@ int mgicp_set_params(mgicp_ctx* ctx, const mgicp_params* p) {
   if (cov_change) {
     ctx->src.have_cov = false;
     ctx->tgt.have_cov = false;
+    ctx->tgt_lazy = false;
     ctx->src_lazy_ready = false;
   }
   return MGICP_OK;
@@ -2104,6 +2235,8 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   cancel_gated(ctx);
+  if (ctx->aux_stream) (void)hipStreamSynchronize(ctx->aux_stream);
+  ctx->tgt_cov_pending = ctx->src_cov_pending = false;
   (void)hipStreamSynchronize(ctx->stream);
   srv_release(ctx);
   ctx->f_flags.release(); ctx->f_pos.release(); ctx->f_rgba_in.release(); ctx->f_rgba.release();
@@ -2127,7 +2260,8 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   ctx->nn_work.release(); ctx->nn_work_n.release();
   ctx->vl_cell.release(); ctx->vl_pool.release(); ctx->vl_ctr.release();
   ctx->vl_build.release(); ctx->vl_bcentre.release(); ctx->vl_pend.release();
-  ctx->cov_ok.release(); ctx->cov_need.release();
+  ctx->cov_ok.release(); ctx->cov_need.release(); ctx->tcov_ok.release(); ctx->tcov_need.release();
+  ctx->aux_cnt.release(); ctx->knn_fb2.release();
   ctx->tpart.release();
   ctx->tpart_n = 0;
   ctx->corr_f.release(); ctx->corr_d.release(); ctx->cscratch.release();
@@ -2150,28 +2284,35 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   for (hipEvent_t e : ctx->pool) (void)hipEventDestroy(e);
   if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  if (ctx->aux_stream) (void)hipStreamDestroy(ctx->aux_stream);
+  for (hipEvent_t e : ctx->aux_ev)
+    if (e) (void)hipEventDestroy(e);
   delete ctx;
 }
 
 int mgicp_set_target(mgicp_ctx* ctx, const float* xyz, size_t n, size_t stride) {
   if (!ctx) return MGICP_E_INVALID;
   HIPCK(hipSetDevice(ctx->device));
-  return upload_cloud(ctx, ctx->tgt, xyz, n, stride, false);
+  const int rc = upload_cloud(ctx, ctx->tgt, xyz, n, stride, false);
+  return rc ? rc : cov_prep_async(ctx, true);
 }
 int mgicp_set_source(mgicp_ctx* ctx, const float* xyz, size_t n, size_t stride) {
   if (!ctx) return MGICP_E_INVALID;
   HIPCK(hipSetDevice(ctx->device));
-  return upload_cloud(ctx, ctx->src, xyz, n, stride, false);
+  const int rc = upload_cloud(ctx, ctx->src, xyz, n, stride, false);
+  return rc ? rc : cov_prep_async(ctx, false);
 }
 int mgicp_set_target_device(mgicp_ctx* ctx, const float* d_xyz, size_t n, size_t stride) {
   if (!ctx) return MGICP_E_INVALID;
   HIPCK(hipSetDevice(ctx->device));
-  return upload_cloud(ctx, ctx->tgt, d_xyz, n, stride, true);
+  const int rc = upload_cloud(ctx, ctx->tgt, d_xyz, n, stride, true);
+  return rc ? rc : cov_prep_async(ctx, true);
 }
 int mgicp_set_source_device(mgicp_ctx* ctx, const float* d_xyz, size_t n, size_t stride) {
   if (!ctx) return MGICP_E_INVALID;
   HIPCK(hipSetDevice(ctx->device));
-  return upload_cloud(ctx, ctx->src, d_xyz, n, stride, true);
+  const int rc = upload_cloud(ctx, ctx->src, d_xyz, n, stride, true);
+  return rc ? rc : cov_prep_async(ctx, false);
 }
 
 int mgicp_align(mgicp_ctx* ctx, const float guess_cm[16], float out_T_cm[16], mgicp_result* res) {
@@ -2185,6 +2326,7 @@ int mgicp_align(mgicp_ctx* ctx, const float guess_cm[16], float out_T_cm[16], mg
   MGICP_TRACE_AT("align: begin");
   int rc = prepare(ctx, true);
   if (rc) return rc;
+  if (ctx->tgt_lazy && ctx->tgt_lazy_aligns > 0 && (rc = cov_lazy(ctx, true))) return rc;  // the rest, once
   MGICP_TRACE_AT("align: prepared");
   rc = ensure_iter_buffers(ctx);
   if (rc) return rc;
@@ -2237,6 +2379,7 @@ int mgicp_align(mgicp_ctx* ctx, const float guess_cm[16], float out_T_cm[16], mg
   // polled passes leave their kernels' completion unobserved: drain the stream once
   if ((rc = sync(ctx))) return rc;
   if (ctx->vl_valid) ctx->vl_groups++;
+  if (ctx->tgt_lazy) ctx->tgt_lazy_aligns++;
   if (ctx->h_gtrace) {
     // diagnostics of the gated passes of this align: device-side gate wait and spread, host-side
     // decision time (sums seen -> command published); device wall clock in 10 ns ticks (100 MHz)
@@ -2611,6 +2754,7 @@ int mgicp_get_unique_id(unsigned char id[128]) {
 int mgicp_comm_init(mgicp_ctx* ctx, int nranks, int rank, const unsigned char id[128]) {
   if (!ctx || nranks < 1 || rank < 0 || rank >= nranks) return MGICP_E_INVALID;
   HIPCK(hipSetDevice(ctx->device));
+  if (int rj = cov_join_all(ctx)) return rj;  // the shard changes under them
   if (ctx->comm) {
     (void)ncclCommDestroy(ctx->comm);
     ctx->comm = nullptr;
@@ -2644,7 +2788,9 @@ int mgicp_comm_init(mgicp_ctx* ctx, int nranks, int rank, const unsigned char id
 int mgicp_comm_attach_shm(mgicp_ctx* ctx, const char* name, size_t max_source_points) {
   if (!ctx) return MGICP_E_INVALID;
   HIPCK(hipSetDevice(ctx->device));
-  int rc = reset_stamps(ctx);  // the stamp count restarts with the transport on every rank
+  int rc = cov_join_all(ctx);  // the shard changes under them
+  if (rc) return rc;
+  rc = reset_stamps(ctx);  // the stamp count restarts with the transport on every rank
   if (rc) return rc;
   if (ctx->have_shm) {
     (void)hipHostUnregister(ctx->shm.base);
@@ -2708,6 +2854,7 @@ int mgicp_debug_target_cov_slice(mgicp_ctx* ctx, int nranks, int rank, double* o
   // target_cov's slice call, verbatim: the same range, the same N * cnt array layout
   if ((rc = compute_cov(ctx, t, a, b, N * cnt))) return rc;
   t.have_cov = false;  // only a slice is current: the next align recomputes the target's covariances
+  ctx->tgt_lazy = false;
   const size_t st = t.cov_stride, m = b - a;
   std::vector<double2> h(3 * std::max<size_t>(m, 1));
   if (m) {
@@ -2755,11 +2902,13 @@ int mgicp_debug_covariances(mgicp_ctx* ctx, int which, double* out_c6) {
   HIPCK(hipSetDevice(ctx->device));
   int rc = prepare(ctx, true);
   if (rc) return rc;
+  if ((rc = cov_join(ctx, false))) return rc;
   if (which == 0 && !(ctx->src.have_cov && ctx->src.cov_p0 == ctx->shard_p0() && ctx->src.cov_p1 == ctx->shard_p1())) {
     // every source covariance (lazy mode computes only the accepted points' ones)
     if ((rc = compute_cov(ctx, ctx->src, ctx->shard_p0(), ctx->shard_p1()))) return rc;
     if (ctx->src_lazy_ready) HIPCK(hipMemsetAsync(ctx->cov_ok.p, 1, ctx->shard_p1() - ctx->shard_p0(), ctx->stream));
   }
+  if (which == 1 && ctx->tgt_lazy && (rc = cov_lazy(ctx, true))) return rc;  // every target covariance
   Cloud& cl = which ? ctx->tgt : ctx->src;
   const size_t n = cl.n;
   const size_t st = cl.cov_stride;

@@ -187,6 +187,11 @@ hipError_t launch_vl_sweep(const GridView& tgt, const VListView& vl, const float
 // positions p0 + k, *count of them), cov_ok[k] = 1
 hipError_t launch_cov_need(const uint32_t* flags, uint8_t* cov_ok, size_t p0, size_t n, uint32_t* list,
                            unsigned int* count, hipStream_t s);
+// lazy target covariances (r04): rest = 0 -- the target points matched by the sweep's accepted
+// queries (nn_pos) without a covariance; rest = 1 -- every target point without one.  Listed
+// (sorted positions, *count of them) and marked done in ok
+hipError_t launch_tgt_cov_need(const uint32_t* flags, const uint32_t* nn_pos, size_t ns, uint8_t* ok, size_t nt,
+                               int rest, uint32_t* list, unsigned int* count, hipStream_t s);
 // diagnostics (env MGICP_VLIST_STATS): per built cell list lengths histogram etc. into out[64]
 hipError_t launch_vl_stats(const VListView& vl, size_t ncells, unsigned long long* out /*device, 64*/, hipStream_t s);
 size_t     pair_count(size_t n);

@@ -677,29 +677,44 @@ __global__ void empty_init_kernel(const uint32_t* __restrict__ cs, size_t nc, ui
 }
 
 // one separable pass of the Chebyshev (L-inf) distance transform along an axis of extent n and
-// element stride `stride`: out(c) = min_{|d| <= cap} max(|d|, in(c + d*stride)), capped at cap+1.
-// With seeds, the seed of the winning cell travels along (first winner in |d|, minus side first),
-// so the final seed lies in a Chebyshev-nearest non-empty cell
-__global__ void empty_pass_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
-                                  size_t nc, int n, size_t stride, int cap, const uint32_t* __restrict__ sin,
-                                  uint32_t* __restrict__ sout) {
+// element stride `stride`: out(c) = min_{|d| <= kEmptyCap} max(|d|, in(c + d*stride)), capped at
+// kEmptyCap + 1.  With seeds, the seed of the winning cell travels along (first winner in |d|, minus
+// side first), so the final seed lies in a Chebyshev-nearest non-empty cell.  r04: all 2 kEmptyCap
+// neighbours are loaded up front (clamped addresses, out-of-line slots read as empty) and the
+// candidates are then taken in the original order from registers -- the loop of r01 issued its loads
+// one |d| at a time behind the early exit (~275 us per pass at C4's 19.5M target cells)
+__global__ __launch_bounds__(256) void empty_pass_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                         size_t nc, int n, size_t stride,
+                                                         const uint32_t* __restrict__ sin,
+                                                         uint32_t* __restrict__ sout) {
+  constexpr int cap = kEmptyCap;
   const size_t c = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (c >= nc) return;
   const int x = static_cast<int>((c / stride) % static_cast<size_t>(n));
+  int vm[cap], vp[cap];
+#pragma unroll
+  for (int d = 1; d <= cap; ++d) {
+    const int am = min(d, x), ap = min(d, n - 1 - x);  // clamped: an in-line address
+    const int lm = in[c - static_cast<size_t>(am) * stride], lp = in[c + static_cast<size_t>(ap) * stride];
+    vm[d - 1] = am == d ? lm : 255;
+    vp[d - 1] = ap == d ? lp : 255;
+  }
   int best = min(static_cast<int>(in[c]), cap + 1);
-  size_t arg = c;
-  for (int d = 1; d <= cap && d < best; ++d) {
-    if (x - d >= 0) {
-      const int v = max(d, static_cast<int>(in[c - d * stride]));
-      if (v < best) { best = v; arg = c - d * stride; }
-    }
-    if (x + d < n) {
-      const int v = max(d, static_cast<int>(in[c + d * stride]));
-      if (v < best) { best = v; arg = c + d * stride; }
+  int dbest = 0;  // signed offset of the winner
+#pragma unroll
+  for (int d = 1; d <= cap; ++d) {
+    if (d < best) {
+      const int v = max(d, vm[d - 1]);
+      if (v < best) { best = v; dbest = -d; }
+      const int w = max(d, vp[d - 1]);
+      if (w < best) { best = w; dbest = d; }
     }
   }
   out[c] = static_cast<uint8_t>(min(best, cap + 1));
-  if (sout) sout[c] = best <= cap ? sin[arg] : 0xffffffffu;
+  if (sout) {
+    const size_t arg = dbest < 0 ? c - static_cast<size_t>(-dbest) * stride : c + static_cast<size_t>(dbest) * stride;
+    sout[c] = best <= cap ? sin[arg] : 0xffffffffu;
+  }
 }
 
 // per-cell point boxes: boxes[2c] = (min x, min y, min z, bits(start)), boxes[2c + 1] =
@@ -3462,9 +3477,9 @@ hipError_t launch_empty_map(const uint32_t* cell_start, int nx, int ny, int nz, 
   uint32_t* s2 = seed ? seed_scratch : nullptr;
   empty_init_kernel<<<nblk(nc), 256, 0, s>>>(cell_start, nc, out, seed, g ? g->pts : nullptr, nx, ny,
                                              g ? g->ox : 0.f, g ? g->oy : 0.f, g ? g->oz : 0.f, g ? g->h : 0.f);
-  empty_pass_kernel<<<nblk(nc), 256, 0, s>>>(out, scratch, nc, nx, 1, kEmptyCap, seed, s2);
-  empty_pass_kernel<<<nblk(nc), 256, 0, s>>>(scratch, out, nc, ny, static_cast<size_t>(nx), kEmptyCap, s2, seed);
-  empty_pass_kernel<<<nblk(nc), 256, 0, s>>>(out, scratch, nc, nz, static_cast<size_t>(nx) * ny, kEmptyCap, seed,
+  empty_pass_kernel<<<nblk(nc), 256, 0, s>>>(out, scratch, nc, nx, 1, seed, s2);
+  empty_pass_kernel<<<nblk(nc), 256, 0, s>>>(scratch, out, nc, ny, static_cast<size_t>(nx), s2, seed);
+  empty_pass_kernel<<<nblk(nc), 256, 0, s>>>(out, scratch, nc, nz, static_cast<size_t>(nx) * ny, seed,
                                              s2);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
@@ -3556,21 +3571,52 @@ hipError_t launch_vl_sweep(const GridView& tgt, const VListView& vl, const float
 }
 
 // lazy source covariances: the accepted points of a sweep whose covariance was never computed
-__global__ void cov_need_kernel(const uint32_t* __restrict__ flags, uint8_t* __restrict__ cov_ok, size_t p0, size_t n,
-                                uint32_t* __restrict__ list, unsigned int* __restrict__ count) {
-  const size_t k = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  const bool need = k < n && flags[k] && !cov_ok[k];
-  const unsigned long long m = __builtin_amdgcn_ballot_w64(need);
-  if (!m) return;
-  const int lane = threadIdx.x & 63;
-  unsigned int base = 0;
-  if (lane == 0) base = atomicAdd(count, static_cast<unsigned int>(__builtin_popcountll(m)));
-  base = __builtin_amdgcn_readfirstlane(base);
-  if (need) {
-    const unsigned int o = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned int>(m >> 32),
-                                                     __builtin_amdgcn_mbcnt_lo(static_cast<unsigned int>(m), 0u));
-    list[base + o] = static_cast<uint32_t>(p0 + k);
-    cov_ok[k] = 1;
+// the accepted points of a sweep without a covariance, listed (any order) and marked.  One block of
+// 256 threads takes kCovNeedPer consecutive points per thread round, counts its points, and takes its
+// list slots with ONE atomic (one per wave saturated the counter's memory-side atomics in the first
+// sweep of a cloud: ~0.3 ms at 5M, profiles/r04/prep4)
+constexpr int kCovNeedPer = 16;
+// flags == nullptr (lazy target covariances): the points marked 2 by cov_mark_kernel, or (rest) every
+// point not marked 1
+__global__ __launch_bounds__(256) void cov_need_kernel(const uint32_t* __restrict__ flags, uint8_t* __restrict__ cov_ok,
+                                                       size_t p0, size_t n, uint32_t* __restrict__ list,
+                                                       unsigned int* __restrict__ count, int rest) {
+  __shared__ unsigned int s_w[4];
+  __shared__ unsigned int s_base;
+  const size_t k0 = static_cast<size_t>(blockIdx.x) * (256 * kCovNeedPer);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  unsigned long long m[kCovNeedPer];
+  unsigned int mine = 0;
+#pragma unroll
+  for (int u = 0; u < kCovNeedPer; ++u) {
+    const size_t k = k0 + static_cast<size_t>(u) * 256 + threadIdx.x;
+    bool need = false;
+    if (k < n) {
+      if (flags) need = flags[k] && !cov_ok[k];
+      else need = rest ? cov_ok[k] != 1 : cov_ok[k] == 2;
+    }
+    m[u] = __builtin_amdgcn_ballot_w64(need);
+    mine += static_cast<unsigned int>(__builtin_popcountll(m[u]));
+  }
+  if (lane == 0) s_w[wid] = mine;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned int tot = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    s_base = tot ? atomicAdd(count, tot) : 0u;
+  }
+  __syncthreads();
+  unsigned int o = s_base;
+  for (int w = 0; w < wid; ++w) o += s_w[w];
+#pragma unroll
+  for (int u = 0; u < kCovNeedPer; ++u) {
+    const size_t k = k0 + static_cast<size_t>(u) * 256 + threadIdx.x;
+    if ((m[u] >> lane) & 1ull) {
+      const unsigned int r = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned int>(m[u] >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo(static_cast<unsigned int>(m[u]), 0u));
+      list[o + r] = static_cast<uint32_t>(p0 + k);
+      cov_ok[k] = 1;
+    }
+    o += static_cast<unsigned int>(__builtin_popcountll(m[u]));
   }
 }
 
@@ -3578,7 +3624,27 @@ hipError_t launch_cov_need(const uint32_t* flags, uint8_t* cov_ok, size_t p0, si
                            unsigned int* count, hipStream_t s) {
   hipError_t e = hipMemsetAsync(count, 0, sizeof(unsigned int), s);
   if (e != hipSuccess || n == 0) return e;
-  cov_need_kernel<<<nblk(n), 256, 0, s>>>(flags, cov_ok, p0, n, list, count);
+  cov_need_kernel<<<nblk(n, 256 * kCovNeedPer), 256, 0, s>>>(flags, cov_ok, p0, n, list, count, 0);
+  return hipGetLastError();
+}
+
+// the matched target points of a sweep: ok[nn_pos[k]] 0 -> 2 for every accepted k (plain stores:
+// racing writers store the same value)
+__global__ __launch_bounds__(256) void cov_mark_kernel(const uint32_t* __restrict__ flags,
+                                                       const uint32_t* __restrict__ nn_pos, size_t n,
+                                                       uint8_t* __restrict__ ok) {
+  const size_t k = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (k >= n || !flags[k]) return;
+  const uint32_t j = nn_pos[k];
+  if (ok[j] == 0) ok[j] = 2;
+}
+
+hipError_t launch_tgt_cov_need(const uint32_t* flags, const uint32_t* nn_pos, size_t ns, uint8_t* ok, size_t nt,
+                               int rest, uint32_t* list, unsigned int* count, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(count, 0, sizeof(unsigned int), s);
+  if (e != hipSuccess || nt == 0) return e;
+  if (!rest && ns) cov_mark_kernel<<<nblk(ns), 256, 0, s>>>(flags, nn_pos, ns, ok);
+  cov_need_kernel<<<nblk(nt, 256 * kCovNeedPer), 256, 0, s>>>(nullptr, ok, 0, nt, list, count, rest);
   return hipGetLastError();
 }
 
