@@ -286,12 +286,12 @@ struct mgicp_ctx {
   const float4* d_out = nullptr;
   // compacted accepted correspondences of the current outer iteration (shard-relative)
   DevBuf<uint32_t> prev_pos;  // matched target sorted position per shard point (also the next 1-NN seed)
-  DevBuf<uint32_t> flags, cpos;
+  DevBuf<uint32_t> flags;
   DevBuf<unsigned char> nn_work;      // NnWork list of the wave sweep's stragglers (r03)
   DevBuf<unsigned int> nn_work_n;
   DevBuf<float> corr_f;    // 6 streams
   DevBuf<double> corr_d;   // 6 streams
-  DevBuf<unsigned char> cscratch;
+
   size_t corr_cap = 0;     // elements per stream (multiple of 4)
   bool seed_valid = false;
   // query order of the 1-NN sweeps (Morton order of the shard; env MGICP_QUERY_ORDER)
@@ -300,7 +300,7 @@ struct mgicp_ctx {
   DevBuf<uint32_t> qperm;
   // the fixed reduction tree (internal.hpp kChunkPts / kSuperChunks): chunk layout of the streams,
   // chunk and super partials of this shard, the all-gathered supers of every rank, the total
-  DevBuf<uint32_t> chunk_base;  // chunk_count(ns) + 1
+  DevBuf<uint32_t> ccnt;  // chunk_count(ns): correspondences per chunk (fixed-slot layout, r04)
   DevBuf<double> partial;       // chunk partials, kRedVals each
   DevBuf<unsigned long long> tpart;  // the server's stamped chunk partials, 32 words each (r03; 0xff.. = no stamp)
   size_t tpart_n = 0;
@@ -434,6 +434,8 @@ struct mgicp_ctx {
   DevBuf<float> fpartial;
   // the target's 1-NN cell lists (r04, DESIGN.md "1-NN cell lists"; env MGICP_VLIST=0: the r03 sweeps)
   bool vlist = true;
+  bool fuse_compact = true;           // r04: compaction fused into listed sweeps (env MGICP_FUSE_COMPACT)
+  DevBuf<uint32_t> vl_defer;          // chunks a fused sweep deferred to the compaction launch
   float vlist_cell = 0.6f;            // fine cell edge / the target grid's cell edge (env MGICP_VLIST_CELL)
   bool vl_stats = false;              // env MGICP_VLIST_STATS: per-sweep list diagnostics on stderr
   bool vl_valid = false;              // lists belong to the current target grid and gate
@@ -654,6 +656,8 @@ int cov_join(mgicp_ctx* ctx, bool tgt) {
     unsigned int nfb = 0;
     HIPCK(hipMemcpy(&nfb, ctx->aux_cnt.p + (tgt ? 0 : 1), sizeof(nfb), hipMemcpyDeviceToHost));
     ctx->knn_fallbacks = nfb;
+    if (std::getenv("MGICP_KNN_STATS"))  // as compute_cov reports it
+      std::fprintf(stderr, "[knn] %zu points, %u left to the register-list kernel\n", c.n, nfb);
     if (nfb) {
       ProfScope ps(ctx, kFamCov);
       HIPCK(launch_knn_cov(c.view, ctx->prm.k, ctx->prm.gicp_eps, 0, nfb, c.cov3(), tgt ? ctx->knn_fb.p : ctx->knn_fb2.p,
@@ -694,6 +698,18 @@ int cov_prep_async(mgicp_ctx* ctx, bool tgt) {
   HIPCK(hipEventRecord(ctx->aux_ev[tgt ? 0 : 1], ctx->aux_stream));
   (tgt ? ctx->tgt_cov_pending : ctx->src_cov_pending) = true;
   return MGICP_OK;
+}
+
+// after a set_*: the head start for every cloud that can have it, in prepare's order -- the target
+// first, the source only once the target's grid exists (the source grid starts from the target's
+// cell size, so the grids, and with them every sorted order and sum, are those of the synchronous
+// path whatever the order of the set_* calls; the reference calls setInputSource first,
+// GICPAlignment.cpp:89-90)
+int cov_prep_async_all(mgicp_ctx* ctx) {
+  int rc = MGICP_OK;
+  if (ctx->tgt.dirty && (rc = cov_prep_async(ctx, true))) return rc;
+  if (ctx->src.dirty && !ctx->tgt.dirty && ctx->tgt.n_built > 0) rc = cov_prep_async(ctx, false);
+  return rc;
 }
 
 int upload_cloud(mgicp_ctx* ctx, Cloud& cl, const float* xyz, size_t n, size_t stride,
@@ -1312,7 +1328,7 @@ int take_over(mgicp_ctx* ctx, unsigned int rstamp, const Xf34& A) {
   ctx->st[kStTakeover]++;
   ctx->st[kStLaunchedPass]++;
   const size_t ns = ctx->shard_p1() - ctx->shard_p0();
-  HIPCK(launch_fdf_soa(corr_soa(ctx), ctx->cpos.p, ctx->chunk_base.p, ns, A, ctx->partial.p, ctx->spart.p,
+  HIPCK(launch_fdf_soa(corr_soa(ctx), ctx->ccnt.p, ns, A, ctx->partial.p, ctx->spart.p,
                        fdf_grid_blocks(ns, ctx->fdf_max_blocks), ctx->tickets.p, nullptr, 0, nullptr, 0, ctx->stream,
                        row_view(ctx).dev_rows(rstamp), rstamp));
   // host-row passes leave the tickets as multiples of their supers' sizes: re-arm them for whatever
@@ -1389,7 +1405,7 @@ int ensure_iter_buffers(mgicp_ctx* ctx) {
     ctx->tpart_n = ctx->tpart.cap;
   }
   HIPCK(ctx->spart.reserve(std::max<size_t>(msup, 1) * kRedVals));
-  HIPCK(ctx->chunk_base.reserve(nch + 1));
+  HIPCK(ctx->ccnt.reserve(std::max<size_t>(nch, 1)));
   HIPCK(ctx->red.reserve(kRedVals));
   if (ctx->tickets_n < msup + 1) {  // zero between passes: every finishing wave re-arms its own
     HIPCK(ctx->tickets.reserve(msup + 1));
@@ -1398,17 +1414,15 @@ int ensure_iter_buffers(mgicp_ctx* ctx) {
   }
   int rc = ensure_host_red(ctx);
   if (rc) return rc;
-  // every chunk's run is padded to a multiple of 4 slots
-  const size_t cap = (ns + 3 * nch + 3) / 4 * 4 + 4;
+  // fixed slots: chunk c's run starts at c * kChunkPts (padded to a multiple of 4 within the chunk)
+  const size_t cap = std::max<size_t>(nch, 1) * kChunkPts;
   HIPCK(ctx->prev_pos.reserve(ns + 1));
   HIPCK(ctx->flags.reserve(ns + 1));
-  HIPCK(ctx->cpos.reserve(ns + 1));
   if (ctx->corr_cap < cap) {
     HIPCK(ctx->corr_f.reserve(6 * cap));
     HIPCK(ctx->corr_d.reserve(6 * cap));
     ctx->corr_cap = cap;
   }
-  HIPCK(ctx->cscratch.reserve(scan_scratch_bytes(ns + 1)));
   return MGICP_OK;
 }
 
@@ -1603,12 +1617,18 @@ int vl_prepare(mgicp_ctx* ctx) {
 // The 1-NN sweep kernel of one correspondence phase: the target's cell lists (r04, default), else the
 // wave-uniform scan when the target has its pair copy, else the per-lane search (env MGICP_VLIST=0,
 // MGICP_CORR_WAVE=0); all exact, same results.
-hipError_t launch_sweep(mgicp_ctx* ctx, const Mat4& T, double thr, bool seeded, const uint32_t* qp) {
+bool sweep_listed(const mgicp_ctx* ctx) {
+  return ctx->vlist && ctx->vl_valid && !ctx->vl_off && (ctx->vl_groups > 0 || !ctx->vl_cold_r03);
+}
+
+// fc (nullable, listed sweeps only): the compaction fused into the sweep
+hipError_t launch_sweep(mgicp_ctx* ctx, const Mat4& T, double thr, bool seeded, const uint32_t* qp,
+                        const FusedCompact* fc = nullptr) {
   const size_t p0 = ctx->shard_p0(), p1 = ctx->shard_p1();
   const GridView& g = ctx->tgt.view;
-  if (ctx->vlist && ctx->vl_valid && !ctx->vl_off && (ctx->vl_groups > 0 || !ctx->vl_cold_r03))
+  if (sweep_listed(ctx))
     return launch_vl_sweep(g, ctx->vl, ctx->d_out, p0, p1, T.xf(), thr, seeded ? 1 : 0, ctx->prev_pos.p, ctx->flags.p,
-                           ctx->cus, ctx->stream);
+                           ctx->cus, ctx->stream, fc);
   if (ctx->corr_wave && g.pairs) {
     const float rc = ctx->corr_rcap * g.h;
     void* work = nullptr;
@@ -1642,9 +1662,25 @@ int correspond(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
     int rc = vl_prepare(ctx);
     if (rc) return rc;
   }
+  // the compaction fused into a listed sweep: both clouds' covariances must be complete (or, lazy
+  // source mode, marked per point) -- not on the first align after set_*, which runs the r03 sweep
+  const bool fused = ctx->fuse_compact && sweep_listed(ctx) && ctx->tgt.have_cov && !ctx->tgt_lazy &&
+                     !ctx->tgt_cov_pending && !ctx->src_cov_pending &&
+                     (ctx->src.have_cov || (ctx->lazy_src_cov && ctx->src_lazy_ready));
+  FusedCompact fc{};
+  if (fused) {
+    HIPCK(ctx->vl_defer.reserve(std::max(chunk_count(ns), 1)));
+    fc.cov_s = ctx->src.cov3();
+    fc.cov_t = ctx->tgt.cov3();
+    fc.R = rot_of(T, G);
+    fc.cov_ok = ctx->src.have_cov ? nullptr : ctx->cov_ok.p;
+    fc.ccnt = ctx->ccnt.p;
+    fc.defer = ctx->vl_defer.p;
+    fc.out = corr_soa(ctx);
+  }
   {
     ProfScope ps(ctx, kFamCorr);
-    HIPCK(launch_sweep(ctx, T, thr, seeded, qp));
+    HIPCK(launch_sweep(ctx, T, thr, seeded, qp, fused ? &fc : nullptr));
   }
   ctx->seed_valid = true;
   if (ctx->vl_stats && ctx->vlist && !ctx->vl_off && (ctx->vl_groups > 0 || !ctx->vl_cold_r03)) {
@@ -1702,14 +1738,12 @@ int correspond(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
     rc = cov_lazy(ctx);  // covariances of newly accepted source points / matched target points (lazy modes)
     if (rc) return rc;
   }
-  const size_t sb = scan_scratch_bytes(ns + 1);
-  HIPCK(launch_exclusive_scan(ctx->cscratch.p, sb, ctx->flags.p, ctx->cpos.p, ns + 1, s));
   {
     ProfScope ps(ctx, kFamCompact);
-    HIPCK(launch_chunk_base(ctx->cpos.p, ns, ctx->chunk_base.p, corr_soa(ctx), s));
-    HIPCK(launch_compact(ctx->d_out, ctx->tgt.view.pts, ctx->src.cov3(), ctx->tgt.cov3(),
-                         rot_of(T, G), ctx->prev_pos.p, ctx->flags.p, ctx->cpos.p, ctx->chunk_base.p, p0, p1,
-                         corr_soa(ctx), s));
+    // fused: only the chunks the sweep deferred (pending queries, lazy covariances computed above)
+    HIPCK(launch_compact(ctx->d_out, ctx->tgt.view.pts, ctx->src.cov3(), ctx->tgt.cov3(), rot_of(T, G),
+                         ctx->prev_pos.p, ctx->flags.p, p0, p1, ctx->ccnt.p, corr_soa(ctx), s,
+                         fused ? ctx->vl_defer.p : nullptr, fused ? ctx->vl_ctr.p + 3 : nullptr, ctx->cus));
   }
   // no host round trip here: the correspondence count arrives with the first objective pass (its
   // count lane) and every consumer of the streams runs on the same stream
@@ -1783,7 +1817,7 @@ struct DeviceFunctor {
         {
           ProfScope ps(ctx, kFamFdf);
           if (e == hipSuccess)
-            e = launch_fdf_server(c, ctx->cpos.p, ctx->chunk_base.p, ns, ctx->partial.p, ctx->spart.p, ctx->tickets.p,
+            e = launch_fdf_server(c, ctx->ccnt.p, ns, ctx->partial.p, ctx->spart.p, ctx->tickets.p,
                                   out, ctx->d_flag, seq, ctx->bar_cmd ? ctx->bar_cmd : ctx->d_cmd, ctx->mail,
                                   ctx->gate_timeout, ctx->d_ptimes, 0, Ax, rows ? rv.dev_rows(0) : nullptr, rv.stride,
                                   nsrv, ctx->srv_waves, ctx->bar_cmd ? nsrv : 1, ctx->stall_pass,
@@ -1836,7 +1870,7 @@ struct DeviceFunctor {
       cancel_gated(ctx);
       {
         ProfScope ps(ctx, kFamFdf);
-        HIPCK(launch_fdf_soa(c, ctx->cpos.p, ctx->chunk_base.p, ns, Ax, ctx->partial.p, ctx->spart.p, nb,
+        HIPCK(launch_fdf_soa(c, ctx->ccnt.p, ns, Ax, ctx->partial.p, ctx->spart.p, nb,
                              ctx->tickets.p, nullptr, reverse, nullptr, seq, ctx->stream,
                              row_view(ctx).dev_rows(rstamp), rstamp));
       }
@@ -1852,14 +1886,14 @@ struct DeviceFunctor {
     } else {
       cancel_gated(ctx);
       ProfScope ps(ctx, kFamFdf);
-      HIPCK(launch_fdf_soa(c, ctx->cpos.p, ctx->chunk_base.p, ns, Ax, ctx->partial.p, ctx->spart.p, nb,
+      HIPCK(launch_fdf_soa(c, ctx->ccnt.p, ns, Ax, ctx->partial.p, ctx->spart.p, nb,
                            ctx->tickets.p, out, reverse, (poll && inlaunch) ? ctx->d_flag : nullptr, seq,
                            ctx->stream));
     }
     if (gate) {
       // queue pass seq + 1 now (its launch overlaps this pass); it runs once the BFGS step has
       // published x_{k+1}, or exits on cancel when the BFGS run ends
-      HIPCK(launch_fdf_soa_gated(c, ctx->cpos.p, ctx->chunk_base.p, ns, ctx->partial.p, ctx->spart.p, nb,
+      HIPCK(launch_fdf_soa_gated(c, ctx->ccnt.p, ns, ctx->partial.p, ctx->spart.p, nb,
                                  ctx->tickets.p, out, ctx->d_flag, seq + 1, ctx->d_cmd, ctx->mail,
                                  ctx->gate_timeout, ctx->d_gtrace, ctx->gate_pollers, ctx->stream));
       ctx->gated_seq = seq + 1;
@@ -2181,6 +2215,7 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
   if (const char* lc = std::getenv("MGICP_LAZY_SRC_COV")) ctx->lazy_src_cov = std::atoi(lc) != 0;
   if (const char* lc = std::getenv("MGICP_LAZY_TGT_COV")) ctx->lazy_tgt_cov = std::atoi(lc) != 0;
   if (const char* at = std::getenv("MGICP_ASYNC_COV")) ctx->async_tgt = std::atoi(at) != 0;
+  if (const char* fc = std::getenv("MGICP_FUSE_COMPACT")) ctx->fuse_compact = std::atoi(fc) != 0;
   ctx->tgt.want_pairs = ctx->corr_wave;
   if (const char* cb = std::getenv("MGICP_CELL_BOXES")) ctx->tgt.want_boxes = std::atoi(cb) != 0;
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -2255,16 +2290,16 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   ctx->knn_fb.release();
   ctx->tickets.release();
   ctx->tickets_n = 0;
-  ctx->chunk_base.release(); ctx->spart.release(); ctx->gath.release(); ctx->msuper.release();
-  ctx->prev_pos.release(); ctx->flags.release(); ctx->cpos.release();
+  ctx->ccnt.release(); ctx->spart.release(); ctx->gath.release(); ctx->msuper.release();
+  ctx->prev_pos.release(); ctx->flags.release();
   ctx->nn_work.release(); ctx->nn_work_n.release();
   ctx->vl_cell.release(); ctx->vl_pool.release(); ctx->vl_ctr.release();
-  ctx->vl_build.release(); ctx->vl_bcentre.release(); ctx->vl_pend.release();
+  ctx->vl_build.release(); ctx->vl_bcentre.release(); ctx->vl_pend.release(); ctx->vl_defer.release();
   ctx->cov_ok.release(); ctx->cov_need.release(); ctx->tcov_ok.release(); ctx->tcov_need.release();
   ctx->aux_cnt.release(); ctx->knn_fb2.release();
   ctx->tpart.release();
   ctx->tpart_n = 0;
-  ctx->corr_f.release(); ctx->corr_d.release(); ctx->cscratch.release();
+  ctx->corr_f.release(); ctx->corr_d.release();
   ctx->xyz_dev.release();
   if (ctx->mail) (void)hipFree(ctx->mail);
   if (ctx->h_red) (void)hipHostFree(ctx->h_red);
@@ -2294,25 +2329,25 @@ int mgicp_set_target(mgicp_ctx* ctx, const float* xyz, size_t n, size_t stride) 
   if (!ctx) return MGICP_E_INVALID;
   HIPCK(hipSetDevice(ctx->device));
   const int rc = upload_cloud(ctx, ctx->tgt, xyz, n, stride, false);
-  return rc ? rc : cov_prep_async(ctx, true);
+  return rc ? rc : cov_prep_async_all(ctx);
 }
 int mgicp_set_source(mgicp_ctx* ctx, const float* xyz, size_t n, size_t stride) {
   if (!ctx) return MGICP_E_INVALID;
   HIPCK(hipSetDevice(ctx->device));
   const int rc = upload_cloud(ctx, ctx->src, xyz, n, stride, false);
-  return rc ? rc : cov_prep_async(ctx, false);
+  return rc ? rc : cov_prep_async_all(ctx);
 }
 int mgicp_set_target_device(mgicp_ctx* ctx, const float* d_xyz, size_t n, size_t stride) {
   if (!ctx) return MGICP_E_INVALID;
   HIPCK(hipSetDevice(ctx->device));
   const int rc = upload_cloud(ctx, ctx->tgt, d_xyz, n, stride, true);
-  return rc ? rc : cov_prep_async(ctx, true);
+  return rc ? rc : cov_prep_async_all(ctx);
 }
 int mgicp_set_source_device(mgicp_ctx* ctx, const float* d_xyz, size_t n, size_t stride) {
   if (!ctx) return MGICP_E_INVALID;
   HIPCK(hipSetDevice(ctx->device));
   const int rc = upload_cloud(ctx, ctx->src, d_xyz, n, stride, true);
-  return rc ? rc : cov_prep_async(ctx, false);
+  return rc ? rc : cov_prep_async_all(ctx);
 }
 
 int mgicp_align(mgicp_ctx* ctx, const float guess_cm[16], float out_T_cm[16], mgicp_result* res) {
@@ -2939,13 +2974,12 @@ static int debug_corr(mgicp_ctx* ctx, const float T_cm[16], bool seeded, int* ou
   if ((rc = correspond(ctx, Mat4::from_cm(T_cm), G, seeded))) return rc;
   if (ctx->vl_valid) ctx->vl_groups++;
   const size_t p0 = ctx->shard_p0(), p1 = ctx->shard_p1(), ns = p1 - p0;
-  std::vector<uint32_t> nn(ns), flag(ns), slot(ns + 1), perm(n), tperm(ctx->tgt.n);
-  std::vector<uint32_t> cbase(static_cast<size_t>(chunk_count(ns)) + 1);
+  std::vector<uint32_t> nn(ns), flag(ns), perm(n), tperm(ctx->tgt.n);
+  std::vector<uint32_t> ccnt(static_cast<size_t>(chunk_count(ns)));
   HIPCK(hipMemcpyAsync(nn.data(), ctx->prev_pos.p, ns * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
   HIPCK(hipMemcpyAsync(flag.data(), ctx->flags.p, ns * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
-  HIPCK(hipMemcpyAsync(slot.data(), ctx->cpos.p, (ns + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
-  HIPCK(hipMemcpyAsync(cbase.data(), ctx->chunk_base.p, cbase.size() * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                       ctx->stream));
+  if (!ccnt.empty())
+    HIPCK(hipMemcpyAsync(ccnt.data(), ctx->ccnt.p, ccnt.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
   HIPCK(hipMemcpyAsync(perm.data(), ctx->src.perm.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
   HIPCK(hipMemcpyAsync(tperm.data(), ctx->tgt.perm.p, ctx->tgt.n * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
   const size_t cap = ctx->corr_cap;
@@ -2953,17 +2987,26 @@ static int debug_corr(mgicp_ctx* ctx, const float T_cm[16], bool seeded, int* ou
   HIPCK(hipMemcpyAsync(M.data(), ctx->corr_d.p, 6 * cap * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
   if ((rc = sync(ctx))) return rc;
   int cnt = 0;
+  size_t rank = 0;  // accepted before k in k's chunk
   for (size_t p = p0; p < p1; ++p) {
     const size_t i = perm[p], k = p - p0;
+    if (k % kChunkPts == 0) rank = 0;
     const bool ok = flag[k] != 0;
     if (out_tgt) out_tgt[i] = ok ? static_cast<int>(tperm[nn[k]]) : -1;
-    if (ok) cnt++;
     if (out_M6) {
       double* o = out_M6 + 6 * i;
-      const size_t ch = k / kChunkPts;  // the chunk's run of the streams
-      const size_t at = cbase[ch] + slot[k] - slot[ch * kChunkPts];
+      const size_t at = (k / kChunkPts) * kChunkPts + rank;  // the chunk's run of the streams
       for (int v = 0; v < 6; ++v) o[v] = ok ? M[v * cap + at] : 0.0;
     }
+    if (ok) {
+      cnt++;
+      rank++;
+    }
+  }
+  for (size_t c = 0; c < ccnt.size(); ++c) {  // the compaction's counts agree with the flags
+    size_t m = 0;
+    for (size_t k = c * kChunkPts; k < std::min(ns, (c + 1) * kChunkPts); ++k) m += flag[k] != 0;
+    if (m != ccnt[c]) return fail(ctx, MGICP_E_HIP, "chunk counts disagree with the sweep's flags");
   }
   return cnt;
 }
@@ -3035,7 +3078,7 @@ int mgicp_debug_pass_bench(mgicp_ctx* ctx, const double x[6], int npasses, int m
     }
     const unsigned long long seq0 = ++ctx->pass_seq;
     const RowView rv = row_view(ctx);
-    e = launch_fdf_server(c, ctx->cpos.p, ctx->chunk_base.p, ns, ctx->partial.p, ctx->spart.p, ctx->tickets.p,
+    e = launch_fdf_server(c, ctx->ccnt.p, ns, ctx->partial.p, ctx->spart.p, ctx->tickets.p,
                           ctx->d_h_red, ctx->d_flag, seq0, ctx->d_cmd, ctx->mail, ctx->gate_timeout, ctx->d_ptimes,
                           npasses, A, rows ? rv.dev_rows(0) : nullptr, rv.stride, nb, ctx->srv_waves, 1, -1,
                           ctx->srv_tagged ? ctx->tpart.p : nullptr, ctx->stream);
@@ -3043,7 +3086,7 @@ int mgicp_debug_pass_bench(mgicp_ctx* ctx, const double x[6], int npasses, int m
   } else {
     const int nb = fdf_grid_blocks(ns, ctx->fdf_max_blocks);
     for (int k = 0; k < npasses && e == hipSuccess; ++k)
-      e = launch_fdf_soa(c, ctx->cpos.p, ctx->chunk_base.p, ns, A, ctx->partial.p, ctx->spart.p, nb, ctx->tickets.p,
+      e = launch_fdf_soa(c, ctx->ccnt.p, ns, A, ctx->partial.p, ctx->spart.p, nb, ctx->tickets.p,
                          ctx->d_h_red, ctx->alt_sweep ? (k & 1) : 0, ctx->d_flag, ++ctx->pass_seq, ctx->stream);
   }
   if (e == hipSuccess) e = hipEventRecord(b, ctx->stream);
@@ -3115,7 +3158,7 @@ int mgicp_debug_supers(mgicp_ctx* ctx, int kind, const double* arg, double* out,
     const size_t ns = ctx->shard_p1() - ctx->shard_p0();
     // host-row passes leave the tickets as multiples of their supers' sizes
     HIPCK(hipMemsetAsync(ctx->tickets.p, 0, ctx->tickets_n * sizeof(unsigned int), ctx->stream));
-    HIPCK(launch_fdf_soa(corr_soa(ctx), ctx->cpos.p, ctx->chunk_base.p, ns, apply_state(x).xf(), ctx->partial.p,
+    HIPCK(launch_fdf_soa(corr_soa(ctx), ctx->ccnt.p, ns, apply_state(x).xf(), ctx->partial.p,
                          ctx->spart.p, fdf_grid_blocks(ns, ctx->fdf_max_blocks), ctx->tickets.p, nullptr, 0,
                          nullptr, 0, ctx->stream));
   } else if (kind == 1) {

@@ -180,9 +180,20 @@ struct VListView {
 // one sweep over the lists: listed queries answered at once, reject cells rejected, the others
 // queued (pend) and their cells requested; then the requested cells' lists are built and the
 // pending queries answered by the exact per-lane search (seeded like correspond_kernel)
+// the compaction fused into a listed sweep (vl_query_compact_kernel): its inputs; chunks it cannot
+// finish (a pending query, a lazy source covariance not computed yet) are listed in `defer`, count
+// in VListView::ctr[3], for launch_compact(..., defer, ctr + 3)
+struct FusedCompact {
+  Cov3 cov_s, cov_t;
+  Rot33d R;
+  const uint8_t* cov_ok;  // lazy source mode: per shard point, covariance computed (nullptr: all are)
+  uint32_t* ccnt;
+  uint32_t* defer;
+  CorrSoA out;
+};
 hipError_t launch_vl_sweep(const GridView& tgt, const VListView& vl, const float4* src, size_t p0, size_t p1,
                            Xf34 T, double thr, int seeded, uint32_t* nn_pos, uint32_t* flags, int cus,
-                           hipStream_t s);
+                           hipStream_t s, const FusedCompact* fc = nullptr);
 // lazy source covariances (r04): shard positions k with flags[k] && !cov_ok[k] -> list (absolute
 // positions p0 + k, *count of them), cov_ok[k] = 1
 hipError_t launch_cov_need(const uint32_t* flags, uint8_t* cov_ok, size_t p0, size_t n, uint32_t* list,
@@ -199,15 +210,14 @@ hipError_t launch_pairs(const float4* pts, size_t n, float4* out, hipStream_t s)
 // Morton keys (30 bit, bbox lo, 1024 / extent = inv) of points [p0, p0 + n) and values 0..n-1
 hipError_t launch_morton_keys(const float4* pts, size_t p0, size_t n, const float lo[3], float inv,
                               uint32_t* keys, uint32_t* vals, hipStream_t s);
-// chunk layout of the compacted streams: base[c] (chunk_count(ns) + 1 entries, multiples of 4) from
-// pos = exclusive scan of the ns + 1 flags; zeroes each chunk's <= 3 pad slots
-hipError_t launch_chunk_base(const uint32_t* pos, size_t ns, uint32_t* base, CorrSoA out, hipStream_t s);
-// accepted correspondences -> their chunk's run of the streams, computing the Mahalanobis
-// matrices on the way
+// accepted correspondences -> their chunk's run of the streams (fixed slots: chunk c at c *
+// kChunkPts, ccnt[c] of them, pads to a multiple of 4 zeroed), computing the Mahalanobis matrices
+// on the way
+// defer (nullable): only the chunks a fused listed sweep deferred (list + device count)
 hipError_t launch_compact(const float4* src, const float4* tpts, const Cov3& cov_s,
                           const Cov3& cov_t, Rot33d R, const uint32_t* nn_pos,
-                          const uint32_t* flags, const uint32_t* pos, const uint32_t* chunk_base, size_t p0,
-                          size_t p1, CorrSoA out, hipStream_t s);
+                          const uint32_t* flags, size_t p0, size_t p1, uint32_t* ccnt, CorrSoA out, hipStream_t s,
+                          const uint32_t* defer = nullptr, const unsigned int* defer_count = nullptr, int cus = 0);
 // objective pass over the shard's chunks (ns source positions): chunk partials (partial,
 // chunk_count(ns) x kRedVals), super partials (spart), and with `out` the total (in-launch).
 // tickets: one per super + one, zero between passes.  done_flag (nullable, mapped host memory):
@@ -215,14 +225,14 @@ hipError_t launch_compact(const float4* src, const float4* tpts, const Cov3& cov
 // poll instead of synchronising the stream
 // host_rows (nullable): super partials as stamped host rows (stamp rstamp, this pass's parity buffer
 // at the rank's first super; tickets counted modulo the supers' sizes) instead of spart / out
-hipError_t launch_fdf_soa(const CorrSoA& c, const uint32_t* pos, const uint32_t* base, size_t ns, Xf34 A,
+hipError_t launch_fdf_soa(const CorrSoA& c, const uint32_t* ccnt, size_t ns, Xf34 A,
                           double* partial, double* spart, int nb, unsigned int* tickets, double* out, int reverse,
                           unsigned long long* done_flag, unsigned long long seq, hipStream_t s,
                           unsigned long long* host_rows = nullptr, unsigned int rstamp = 0);
 // the same pass pre-launched before its state is known: block 0 waits for cmd->seq == seq (or for
 // `timeout_ticks` of wall_clock64) and forwards the command to `mail` (device memory) for the other
 // blocks; then every block runs with its A / reverse, or exits on a cancel
-hipError_t launch_fdf_soa_gated(const CorrSoA& c, const uint32_t* pos, const uint32_t* base, size_t ns,
+hipError_t launch_fdf_soa_gated(const CorrSoA& c, const uint32_t* ccnt, size_t ns,
                                 double* partial, double* spart, int nb, unsigned int* tickets, double* out,
                                 unsigned long long* done_flag, unsigned long long seq, const PassCmd* cmd,
                                 PassCmd* mail, unsigned long long timeout_ticks,
@@ -234,7 +244,7 @@ int        fdf_grid_blocks(size_t ns, int max_blocks = 2048);
 // (timing): that many passes of A back to back without commands.  fdf_server_blocks: its grid for a
 // shard of ns positions on `cus` CUs (0: not servable, use the launched passes)
 int        fdf_server_blocks(size_t ns, int cus, int waves /*4 or 8 per CU*/);
-hipError_t launch_fdf_server(const CorrSoA& c, const uint32_t* pos, const uint32_t* base, size_t ns, double* partial,
+hipError_t launch_fdf_server(const CorrSoA& c, const uint32_t* ccnt, size_t ns, double* partial,
                              double* spart, unsigned int* tickets, double* out, unsigned long long* done_flag,
                              unsigned long long seq0, const PassCmd* cmd, PassCmd* mail,
                              unsigned long long timeout_ticks, unsigned long long* ptimes /*nullable*/,

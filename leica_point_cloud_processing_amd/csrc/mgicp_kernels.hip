@@ -1623,18 +1623,22 @@ __device__ __forceinline__ void vl_cell_xyz(const VListView& v, uint32_t ci, uin
   iz = ci / (nx * ny);
 }
 
-__global__ __launch_bounds__(256) void vl_query_kernel(VListView v, const float4* __restrict__ src, size_t p0,
-                                                       size_t n, Xf34 T, double thr, uint32_t* __restrict__ nn_pos,
-                                                       uint32_t* __restrict__ flags) {
-  // grid order (shard positions): the source reads and the nn_pos / flags writes are coalesced, and
-  // neighbouring lanes query neighbouring cells (shared table lines and lists)
-  const int lane = threadIdx.x & 63;
-  const size_t t = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+// (defined with the compaction below)
+__device__ __forceinline__ void mahalanobis(const Rot33d& R, const double (&C1)[3][3],
+                                            const double (&C2)[3][3], double (&m6)[6]);
+
+// One query of a listed sweep (every lane of the wave calls it: the request / pending lists take one
+// atomic per wave).  Returns 1 accepted (nn / winner coordinates in bp / w), 0 rejected or not live,
+// 2 pending (the cell has no list yet: vl_fallback_kernel answers it); s = the source point.
+__device__ __forceinline__ int vl_query_point(const VListView& v, const float4* __restrict__ src, size_t p0, size_t n,
+                                              const Xf34& T, double thr, size_t t, int lane, float4& s, uint32_t& bp,
+                                              float4& w) {
   const bool live = t < n;
   const uint32_t k = static_cast<uint32_t>(t);
   float qx = 0.f, qy = 0.f, qz = 0.f;
+  s = make_float4(0.f, 0.f, 0.f, 0.f);
   if (live) {
-    const float4 s = src[p0 + t];
+    s = src[p0 + t];
     xform(T, s.x, s.y, s.z, qx, qy, qz);
   }
   const int ix = qcell(qx, v.ox, v.inv_c), iy = qcell(qy, v.oy, v.inv_c), iz = qcell(qz, v.oz, v.inv_c);
@@ -1677,9 +1681,11 @@ __global__ __launch_bounds__(256) void vl_query_kernel(VListView v, const float4
                                                      __builtin_amdgcn_mbcnt_lo(static_cast<unsigned int>(pm), 0u));
     if (pending) v.pend[base + o] = k;
   }
-  if (!live || pending) return;
+  bp = 0xffffffffu;
+  w = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (!live) return 0;
+  if (pending) return 2;
   float bd = INFINITY;
-  uint32_t bp = 0xffffffffu;
   if (st < kVlTouched) {
     uint32_t off = (st >> 6) << 2, cnt = st & 63u;
     if (cnt == static_cast<uint32_t>(kVlLong)) {  // a long list: count in the header entry
@@ -1703,17 +1709,109 @@ __global__ __launch_bounds__(256) void vl_query_kernel(VListView v, const float4
         if (d < bd) {
           bd = d;
           bp = pu;
+          w = a[u];
         } else if (d == bd && d < INFINITY && pu != bp) {
           // an exact-distance tie (measure zero on scans, lattices have them): the lower original
           // index wins, as the (d2, index) key of every other 1-NN search
-          if (__float_as_uint(v.tpts[pu].w) < __float_as_uint(v.tpts[bp].w)) bp = pu;
+          if (__float_as_uint(v.tpts[pu].w) < __float_as_uint(v.tpts[bp].w)) {
+            bp = pu;
+            w = a[u];
+          }
         }
       }
     }
   }
   const bool ok = bp != 0xffffffffu && static_cast<double>(bd) < thr;
-  nn_pos[k] = ok ? bp : 0xffffffffu;
-  flags[k] = ok ? 1u : 0u;
+  if (!ok) bp = 0xffffffffu;
+  return ok ? 1 : 0;
+}
+
+__global__ __launch_bounds__(256) void vl_query_kernel(VListView v, const float4* __restrict__ src, size_t p0,
+                                                       size_t n, Xf34 T, double thr, uint32_t* __restrict__ nn_pos,
+                                                       uint32_t* __restrict__ flags) {
+  // grid order (shard positions): the source reads and the nn_pos / flags writes are coalesced, and
+  // neighbouring lanes query neighbouring cells (shared table lines and lists)
+  const size_t t = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  float4 s, w;
+  uint32_t bp;
+  const int r = vl_query_point(v, src, p0, n, T, thr, t, threadIdx.x & 63, s, bp, w);
+  if (t >= n || r == 2) return;
+  nn_pos[t] = bp;
+  flags[t] = r == 1 ? 1u : 0u;
+}
+
+// r04: the listed sweep with the compaction fused in (DESIGN.md "Fixed-slot compaction").  One
+// 256-thread block per chunk takes its 1024 points in 4 rounds of 256 (grid order); after each
+// round's queries a block scan ranks the accepted ones and they go straight into the chunk's fixed
+// slots with their Mahalanobis matrices -- the winner's coordinates come from its list entry, the
+// source point from the query, so the compaction re-reads neither.  A chunk with a pending query
+// (its cell had no list) or, in the lazy source mode, an accepted point without a covariance yet is
+// DEFERRED: listed in `defer` (count in v.ctr[3]) and compacted whole by chunk_compact_list_kernel
+// once the fallback and the covariances are done.  Results are those of vl_query_kernel +
+// chunk_compact_kernel bit for bit (same per-point arithmetic, same slots).
+__global__ __launch_bounds__(256, 6) void vl_query_compact_kernel(VListView v, const float4* __restrict__ src, size_t p0,
+                                                               size_t n, Xf34 T, double thr,
+                                                               uint32_t* __restrict__ nn_pos,
+                                                               uint32_t* __restrict__ flags, Cov3 cov_s, Cov3 cov_t,
+                                                               Rot33d R, const uint8_t* __restrict__ cov_ok,
+                                                               uint32_t* __restrict__ ccnt, uint32_t* __restrict__ defer,
+                                                               CorrSoA o) {
+  __shared__ uint32_t s_w[2][4];
+  __shared__ uint32_t s_defer[2];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const size_t k0 = static_cast<size_t>(blockIdx.x) * kChunkPts;
+  uint32_t run = 0;
+  bool deferred = false;
+#pragma unroll 1
+  for (int u = 0; u < kChunkPts / 256; ++u) {
+    const size_t t = k0 + static_cast<size_t>(u) * 256 + threadIdx.x;
+    float4 s, w;
+    uint32_t bp;
+    const int r = vl_query_point(v, src, p0, n, T, thr, t, lane, s, bp, w);
+    if (t < n && r != 2) {
+      nn_pos[t] = bp;
+      flags[t] = r == 1 ? 1u : 0u;
+    }
+    const bool acc = r == 1;
+    const bool hold = r == 2 || (acc && cov_ok && !cov_ok[t]);
+    const unsigned long long m = __builtin_amdgcn_ballot_w64(acc);
+    const unsigned long long hm = __builtin_amdgcn_ballot_w64(hold);
+    if (lane == 0) {
+      s_w[u & 1][wid] = static_cast<uint32_t>(__builtin_popcountll(m));
+      s_defer[u & 1] = 0u;  // (every wave stores 0 before the barrier, then the holders set it)
+    }
+    __syncthreads();
+    if (lane == 0 && hm) s_defer[u & 1] = 1u;
+    __syncthreads();
+    deferred = deferred || s_defer[u & 1] != 0u;
+    uint32_t before = run;
+    for (int q = 0; q < wid; ++q) before += s_w[u & 1][q];
+    run += s_w[u & 1][0] + s_w[u & 1][1] + s_w[u & 1][2] + s_w[u & 1][3];
+    if (acc && !deferred) {
+      const uint32_t rk = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned int>(m >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo(static_cast<unsigned int>(m), 0u));
+      const size_t i = k0 + before + rk;
+      double C1[3][3], C2[3][3], m6[6];
+      load_cov(cov_s, p0 + t, C1);
+      load_cov(cov_t, bp, C2);
+      mahalanobis(R, C1, C2, m6);
+      o.m00[i] = m6[0]; o.m01[i] = m6[1]; o.m02[i] = m6[2];
+      o.m11[i] = m6[3]; o.m12[i] = m6[4]; o.m22[i] = m6[5];
+      o.sx[i] = s.x; o.sy[i] = s.y; o.sz[i] = s.z;
+      o.qx[i] = w.x; o.qy[i] = w.y; o.qz[i] = w.z;
+    }
+  }
+  if (deferred) {
+    if (threadIdx.x == 0) defer[atomicAdd(&v.ctr[3], 1u)] = blockIdx.x;
+    return;
+  }
+  if (threadIdx.x == 0) ccnt[blockIdx.x] = run;
+  const uint32_t pad = ((run + 3u) & ~3u) - run;
+  if (threadIdx.x < pad) {
+    const size_t i = k0 + run + threadIdx.x;
+    o.sx[i] = 0.f; o.sy[i] = 0.f; o.sz[i] = 0.f; o.qx[i] = 0.f; o.qy[i] = 0.f; o.qz[i] = 0.f;
+    o.m00[i] = 0.0; o.m01[i] = 0.0; o.m02[i] = 0.0; o.m11[i] = 0.0; o.m12[i] = 0.0; o.m22[i] = 0.0;
+  }
 }
 
 // the requested cells' centres: exact 1-NN within sqrt(thr_c) (none: every point is farther than the
@@ -2138,73 +2236,91 @@ __device__ __forceinline__ void mahalanobis(const Rot33d& R, const double (&C1)[
 #undef COF
 }
 
-// Accepted correspondence p -> its slot in its chunk's run of the streams (chunk c = (p - p0) /
-// kChunkPts starts at chunk_base[c], a multiple of 4; within a chunk, grid-sorted order): the
-// matched target point and its Mahalanobis matrix, written straight into the SoA streams.
-__global__ __launch_bounds__(256) void compact_kernel(const float4* __restrict__ src,
-                                                      const float4* __restrict__ tpts, Cov3 cov_s,
-                                                      Cov3 cov_t, Rot33d R,
-                                                      const uint32_t* __restrict__ nn_pos,
-                                                      const uint32_t* __restrict__ flags,
-                                                      const uint32_t* __restrict__ pos,
-                                                      const uint32_t* __restrict__ chunk_base, size_t p0,
-                                                      size_t p1, CorrSoA o) {
-  const size_t k = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  const size_t p = p0 + k;
-  if (p >= p1 || !flags[k]) return;
-  const uint32_t j = nn_pos[k];
-  const size_t c = k / kChunkPts;
-  const size_t i = chunk_base[c] + (pos[k] - pos[c * kChunkPts]);
-  const float4 s = src[p], t = tpts[j];
-  double C1[3][3], C2[3][3], m6[6];
-  load_cov(cov_s, p, C1);
-  load_cov(cov_t, j, C2);
-  mahalanobis(R, C1, C2, m6);
-  o.m00[i] = m6[0]; o.m01[i] = m6[1]; o.m02[i] = m6[2];
-  o.m11[i] = m6[3]; o.m12[i] = m6[4]; o.m22[i] = m6[5];
-  o.sx[i] = s.x; o.sy[i] = s.y; o.sz[i] = s.z;
-  o.qx[i] = t.x; o.qy[i] = t.y; o.qz[i] = t.z;
+// Fixed-slot chunk layout of the compacted streams (r04): chunk c of the shard (source positions
+// [c * kChunkPts, (c + 1) * kChunkPts) of the shard, a fixed global partition -- shards start on
+// super boundaries) keeps its cnt_c accepted correspondences, in grid-sorted order, at slots
+// [c * kChunkPts, c * kChunkPts + cnt_c) and zeroes the <= 3 pad slots up to a multiple of 4 (M = 0:
+// they add signed zeros only); ccnt[c] = cnt_c.  Slots past a chunk's run are never read.  One
+// 256-thread block per chunk takes its points in 4 rounds of 256 (coalesced, in order): a block
+// scan of the round's flags ranks them, so no global scan and no chunk-base pass (r01-r03: an
+// exclusive scan of the ns flags, chunk_base_kernel, then the scatter).  The matched target point and
+// the Mahalanobis matrix of every accepted correspondence go straight into the SoA streams.
+__device__ __forceinline__ void chunk_compact_body(int c, const float4* __restrict__ src,
+                                                   const float4* __restrict__ tpts, const Cov3& cov_s,
+                                                   const Cov3& cov_t, const Rot33d& R,
+                                                   const uint32_t* __restrict__ nn_pos,
+                                                   const uint32_t* __restrict__ flags, size_t p0, size_t p1,
+                                                   uint32_t* __restrict__ ccnt, const CorrSoA& o) {
+  __shared__ uint32_t s_w[2][4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const size_t k0 = static_cast<size_t>(c) * kChunkPts;
+  const size_t ns = p1 - p0;
+  uint32_t run = 0;  // accepted in the earlier rounds
+#pragma unroll 1
+  for (int u = 0; u < kChunkPts / 256; ++u) {
+    const size_t k = k0 + static_cast<size_t>(u) * 256 + threadIdx.x;
+    const bool acc = k < ns && flags[k] != 0u;
+    const unsigned long long m = __builtin_amdgcn_ballot_w64(acc);
+    if (lane == 0) s_w[u & 1][wid] = static_cast<uint32_t>(__builtin_popcountll(m));
+    __syncthreads();  // (double-buffered counts: the next round writes the other half)
+    uint32_t before = run;
+    for (int w = 0; w < wid; ++w) before += s_w[u & 1][w];
+    run += s_w[u & 1][0] + s_w[u & 1][1] + s_w[u & 1][2] + s_w[u & 1][3];
+    if (acc) {
+      const uint32_t r = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned int>(m >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo(static_cast<unsigned int>(m), 0u));
+      const size_t i = k0 + before + r;
+      const size_t p = p0 + k;
+      const uint32_t j = nn_pos[k];
+      const float4 s = src[p], t = tpts[j];
+      double C1[3][3], C2[3][3], m6[6];
+      load_cov(cov_s, p, C1);
+      load_cov(cov_t, j, C2);
+      mahalanobis(R, C1, C2, m6);
+      o.m00[i] = m6[0]; o.m01[i] = m6[1]; o.m02[i] = m6[2];
+      o.m11[i] = m6[3]; o.m12[i] = m6[4]; o.m22[i] = m6[5];
+      o.sx[i] = s.x; o.sy[i] = s.y; o.sz[i] = s.z;
+      o.qx[i] = t.x; o.qy[i] = t.y; o.qz[i] = t.z;
+    }
+  }
+  if (threadIdx.x == 0) ccnt[c] = run;
+  const uint32_t pad = ((run + 3u) & ~3u) - run;
+  if (threadIdx.x < pad) {
+    const size_t i = k0 + run + threadIdx.x;
+    o.sx[i] = 0.f; o.sy[i] = 0.f; o.sz[i] = 0.f; o.qx[i] = 0.f; o.qy[i] = 0.f; o.qz[i] = 0.f;
+    o.m00[i] = 0.0; o.m01[i] = 0.0; o.m02[i] = 0.0; o.m11[i] = 0.0; o.m12[i] = 0.0; o.m22[i] = 0.0;
+  }
 }
 
-// Chunk layout of the compacted streams (one 1024-thread block): chunk c of the shard (source
-// positions [c * kChunkPts, (c + 1) * kChunkPts) of the shard, a fixed global partition -- shards
-// start on super boundaries) holds cnt_c = pos[end] - pos[start] correspondences at
-// base[c] = sum_{c' < c} round_up_4(cnt_c'); base[nch] is the stream length.  The <= 3 pad slots
-// after each chunk's run are zeroed (M = 0: they add signed zeros only).
-__global__ __launch_bounds__(1024) void chunk_base_kernel(const uint32_t* __restrict__ pos, size_t ns, int nch,
-                                                          uint32_t* __restrict__ base, CorrSoA o) {
-  __shared__ uint32_t wsum[16];
-  const int per = (nch + 1023) / 1024;
-  const int c0 = min(nch, static_cast<int>(threadIdx.x) * per), c1 = min(nch, c0 + per);
-  auto count = [&](int c) {
-    const size_t e = min(static_cast<size_t>(c + 1) * kChunkPts, ns);
-    return pos[e] - pos[static_cast<size_t>(c) * kChunkPts];
-  };
-  uint32_t loc = 0;
-  for (int c = c0; c < c1; ++c) loc += (count(c) + 3u) & ~3u;
-  // block exclusive scan of loc
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  uint32_t inc = loc;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t u = __shfl_up(inc, off, 64);
-    if (lane >= off) inc += u;
+__global__ __launch_bounds__(256, 6) void chunk_compact_kernel(const float4* __restrict__ src,
+                                                            const float4* __restrict__ tpts, Cov3 cov_s,
+                                                            Cov3 cov_t, Rot33d R,
+                                                            const uint32_t* __restrict__ nn_pos,
+                                                            const uint32_t* __restrict__ flags, size_t p0,
+                                                            size_t p1, uint32_t* __restrict__ ccnt, CorrSoA o) {
+  chunk_compact_body(static_cast<int>(blockIdx.x), src, tpts, cov_s, cov_t, R, nn_pos, flags, p0, p1, ccnt, o);
+}
+
+// the chunks a fused listed sweep deferred (list `defer`, *count of them): compacted whole
+__global__ __launch_bounds__(256, 6) void chunk_compact_list_kernel(const float4* __restrict__ src,
+                                                                 const float4* __restrict__ tpts, Cov3 cov_s,
+                                                                 Cov3 cov_t, Rot33d R,
+                                                                 const uint32_t* __restrict__ nn_pos,
+                                                                 const uint32_t* __restrict__ flags, size_t p0,
+                                                                 size_t p1, uint32_t* __restrict__ ccnt,
+                                                                 const uint32_t* __restrict__ defer,
+                                                                 const unsigned int* __restrict__ count, CorrSoA o) {
+  const unsigned int nd = *count;
+  for (unsigned int i = blockIdx.x; i < nd; i += gridDim.x) {
+    chunk_compact_body(static_cast<int>(defer[i]), src, tpts, cov_s, cov_t, R, nn_pos, flags, p0, p1, ccnt, o);
+    __syncthreads();  // the next chunk reuses the block's LDS counts
   }
-  if (lane == 63) wsum[wid] = inc;
-  __syncthreads();
-  uint32_t before = 0;
-  for (int w = 0; w < wid; ++w) before += wsum[w];
-  uint32_t run = before + inc - loc;
-  for (int c = c0; c < c1; ++c) {
-    base[c] = run;
-    const uint32_t cnt = count(c), pad = (cnt + 3u) & ~3u;
-    for (uint32_t i = run + cnt; i < run + pad; ++i) {
-      o.sx[i] = 0.f; o.sy[i] = 0.f; o.sz[i] = 0.f; o.qx[i] = 0.f; o.qy[i] = 0.f; o.qz[i] = 0.f;
-      o.m00[i] = 0.0; o.m01[i] = 0.0; o.m02[i] = 0.0; o.m11[i] = 0.0; o.m12[i] = 0.0; o.m22[i] = 0.0;
-    }
-    run += pad;
-  }
-  if (threadIdx.x == 1023) base[nch] = before + inc;
+}
+
+// chunk j's groups of 4 slots in the fixed-slot layout: [chunk_g0(j), chunk_g1(ccnt, j))
+__device__ __forceinline__ uint32_t chunk_g0(int j) { return static_cast<uint32_t>(j) * (kChunkPts / 4); }
+__device__ __forceinline__ uint32_t chunk_g1(const uint32_t* __restrict__ ccnt, int j) {
+  return chunk_g0(j) + ((ccnt[j] + 3u) >> 2);
 }
 
 // ------------------------------------------------------------------------------------
@@ -2579,12 +2695,11 @@ __device__ __forceinline__ bool pass_gate(unsigned long long seq, const PassCmd*
   return true;
 }
 
-// chunk j's partial (wave_sum's shuffle tree of the lanes' in-order sums) and its exact count from
-// the scan (pad slots are not counted), stored write-through (sc1)
-__device__ __forceinline__ void chunk_store(int j, double (&acc)[kRedVals], const uint32_t* __restrict__ pos,
-                                            size_t ns, double* __restrict__ partial, int lane) {
-  const size_t e = min(static_cast<size_t>(j + 1) * kChunkPts, ns);
-  const double cnt = static_cast<double>(pos[e] - pos[static_cast<size_t>(j) * kChunkPts]);
+// chunk j's partial (wave_sum's shuffle tree of the lanes' in-order sums) and its exact count
+// (ccnt: pad slots are not counted), stored write-through (sc1)
+__device__ __forceinline__ void chunk_store(int j, double (&acc)[kRedVals], const uint32_t* __restrict__ ccnt,
+                                            double* __restrict__ partial, int lane) {
+  const double cnt = static_cast<double>(ccnt[j]);
   double* pj = partial + static_cast<size_t>(j) * kRedVals;
 #if MGICP_CHUNK_SHFL
   // r02 form (A/B): 13 wave_sum shuffle trees, lane 0 stores
@@ -2615,11 +2730,10 @@ __device__ __forceinline__ void chunk_store(int j, double (&acc)[kRedVals], cons
 // (rstamp << 32) | half and written whole by one write-through store (the 8-byte {data, tag}
 // granule of MI355X_MICROARCH "Valid forms"): a reader needs no ticket, drain or fence -- a word is
 // current when it carries this pass's stamp.
-__device__ __forceinline__ void chunk_store_tagged(int j, double (&acc)[kRedVals], const uint32_t* __restrict__ pos,
-                                                   size_t ns, unsigned long long* __restrict__ tpart, int lane,
+__device__ __forceinline__ void chunk_store_tagged(int j, double (&acc)[kRedVals], const uint32_t* __restrict__ ccnt,
+                                                   unsigned long long* __restrict__ tpart, int lane,
                                                    unsigned int rstamp) {
-  const size_t e = min(static_cast<size_t>(j + 1) * kChunkPts, ns);
-  const double cnt = static_cast<double>(pos[e] - pos[static_cast<size_t>(j) * kChunkPts]);
+  const double cnt = static_cast<double>(ccnt[j]);
   wave_sum16(acc, lane);
   if ((lane & 7) == 0) {  // lane 8k: values 2k, 2k + 1 -> words 4k .. 4k + 3
     const double v1 = lane == 48 ? cnt : acc[1];
@@ -2811,8 +2925,7 @@ __device__ __forceinline__ bool wave_tickets(int w0, int nw, int nch, int revers
 // rstamp, tickets counted modulo the supers' sizes) instead of a device total -- the form of the
 // server's passes, used when a server pass is taken over (missed deadline) or cannot run.
 template <bool kGated>
-__device__ __forceinline__ void fdf_soa_body(CorrSoA c, const uint32_t* __restrict__ pos,
-                                             const uint32_t* __restrict__ base, size_t ns, int nch, Xf34 A,
+__device__ __forceinline__ void fdf_soa_body(CorrSoA c, const uint32_t* __restrict__ ccnt, int nch, Xf34 A,
                                              double* __restrict__ partial, double* __restrict__ spart,
                                              unsigned int* __restrict__ tickets, double* __restrict__ out,
                                              int reverse, unsigned long long* done_flag,
@@ -2832,8 +2945,8 @@ __device__ __forceinline__ void fdf_soa_body(CorrSoA c, const uint32_t* __restri
     double acc[kRedVals];
 #pragma unroll
     for (int v = 0; v < kRedVals; ++v) acc[v] = 0.0;
-    const uint32_t g1 = base[j + 1] >> 2;
-    for (uint32_t i = (base[j] >> 2) + lane; i < g1; i += 64) {
+    const uint32_t g1 = chunk_g1(ccnt, j);
+    for (uint32_t i = chunk_g0(j) + lane; i < g1; i += 64) {
       CorrGroup g;
       load_group(c, i, g);
       fdf_group(A, g, acc);
@@ -2849,7 +2962,7 @@ __device__ __forceinline__ void fdf_soa_body(CorrSoA c, const uint32_t* __restri
         for (int v = 0; v < 13; ++v) partial[static_cast<size_t>(j) * kRedVals + v] = acc[v];
       continue;
     }
-    chunk_store(j, acc, pos, ns, partial, lane);
+    chunk_store(j, acc, ccnt, partial, lane);
   }
   if (w0 >= nch || (reverse & 6)) return;
   wave_tickets(w0, nw, nch, reverse, tickets, partial, spart, out, done_flag, seq, lane, host_rows, false, rstamp);
@@ -2894,8 +3007,7 @@ struct SrvShape<8> {
 // that pass (relative to seq0) entirely, so the host must take it over.
 template <bool kBench, int kWaves>
 __global__ __launch_bounds__(64 * kWaves, 1) void fdf_server_kernel(
-    CorrSoA c, const uint32_t* __restrict__ pos, const uint32_t* __restrict__ base, size_t ns, int nch,
-    double* __restrict__ partial, double* __restrict__ spart, unsigned int* __restrict__ tickets,
+    CorrSoA c, const uint32_t* __restrict__ ccnt, int nch, double* __restrict__ partial, double* __restrict__ spart, unsigned int* __restrict__ tickets,
     double* __restrict__ out, unsigned long long* done_flag, unsigned long long seq0, const PassCmd* cmd,
     PassCmd* mail, unsigned long long timeout, unsigned long long* ptimes, int bench_passes, Xf34 Abench,
     unsigned long long* host_rows, size_t rows_stride, int pollers, int stall_pass,
@@ -2914,12 +3026,12 @@ __global__ __launch_bounds__(64 * kWaves, 1) void fdf_server_kernel(
   CorrGroup R[kR];
   uint32_t rb = 0, re = 0, lb = 0, le = 0;
   if (w0 < nch) {
-    rb = base[w0] >> 2;
-    re = base[w0 + 1] >> 2;
+    rb = chunk_g0(w0);
+    re = chunk_g1(ccnt, w0);
   }
   if (kR == 4 && w1 < nch) {
-    lb = base[w1] >> 2;
-    le = base[w1 + 1] >> 2;
+    lb = chunk_g0(w1);
+    le = chunk_g1(ccnt, w1);
   } else if (kR < 4) {
     lb = rb + 64 * kR;
     le = re;
@@ -2967,8 +3079,8 @@ __global__ __launch_bounds__(64 * kWaves, 1) void fdf_server_kernel(
     const int nsup = (nch + kSuperChunks - 1) / kSuperChunks;
     const bool tagged = tpart != nullptr && rows != nullptr && nsup <= nw;
     auto store = [&](int j, double (&acc)[kRedVals]) {
-      if (tagged) chunk_store_tagged(j, acc, pos, ns, tpart, lane, rstamp);
-      else chunk_store(j, acc, pos, ns, partial, lane);
+      if (tagged) chunk_store_tagged(j, acc, ccnt, tpart, lane, rstamp);
+      else chunk_store(j, acc, ccnt, partial, lane);
     };
     // odd waves take their streamed chunks first and their resident ones last, even waves the
     // reverse: the CU's memory pipe is never left idle while all its waves compute resident data
@@ -2979,8 +3091,8 @@ __global__ __launch_bounds__(64 * kWaves, 1) void fdf_server_kernel(
         double acc[kRedVals];
 #pragma unroll
         for (int v = 0; v < kRedVals; ++v) acc[v] = 0.0;
-        const uint32_t g1 = base[w + 1] >> 2;
-        for (uint32_t i = (base[w] >> 2) + lane; i < g1; i += 64) {
+        const uint32_t g1 = chunk_g1(ccnt, w);
+        for (uint32_t i = chunk_g0(w) + lane; i < g1; i += 64) {
           CorrGroup g;
           load_group(c, i, g);
           fdf_group(A, g, acc);
@@ -3018,14 +3130,14 @@ __global__ __launch_bounds__(64 * kWaves, 1) void fdf_server_kernel(
       double acc[kRedVals];
 #pragma unroll
       for (int v = 0; v < kRedVals; ++v) acc[v] = 0.0;
-      uint32_t i0 = (base[w1] >> 2) + lane;
+      uint32_t i0 = chunk_g0(w1) + lane;
       if (kR == 4) {
 #pragma unroll
         for (int k = 0; k < kL; ++k)
           if (lb + lane + 64 * k < le) lds_group(k, A, acc);
         i0 = lb + lane + 64 * kL;
       }
-      const uint32_t g1 = base[w1 + 1] >> 2;
+      const uint32_t g1 = chunk_g1(ccnt, w1);
       for (uint32_t i = i0; i < g1; i += 64) {
         CorrGroup g;
         load_group(c, i, g);
@@ -3106,26 +3218,24 @@ __global__ __launch_bounds__(64 * kWaves, 1) void fdf_server_kernel(
   }
 }
 
-__global__ __launch_bounds__(256) void fdf_soa_kernel(CorrSoA c, const uint32_t* __restrict__ pos,
-                                                      const uint32_t* __restrict__ base, size_t ns, int nch, Xf34 A,
+__global__ __launch_bounds__(256) void fdf_soa_kernel(CorrSoA c, const uint32_t* __restrict__ ccnt, int nch, Xf34 A,
                                                       double* __restrict__ partial, double* __restrict__ spart,
                                                       unsigned int* __restrict__ tickets, double* __restrict__ out,
                                                       int reverse, unsigned long long* done_flag,
                                                       unsigned long long seq, unsigned long long* host_rows,
                                                       unsigned int rstamp) {
-  fdf_soa_body<false>(c, pos, base, ns, nch, A, partial, spart, tickets, out, reverse, done_flag, seq, nullptr,
+  fdf_soa_body<false>(c, ccnt, nch, A, partial, spart, tickets, out, reverse, done_flag, seq, nullptr,
                       nullptr, 0, nullptr, 0, host_rows, rstamp);
 }
 
-__global__ __launch_bounds__(256) void fdf_soa_gated_kernel(CorrSoA c, const uint32_t* __restrict__ pos,
-                                                            const uint32_t* __restrict__ base, size_t ns, int nch,
+__global__ __launch_bounds__(256) void fdf_soa_gated_kernel(CorrSoA c, const uint32_t* __restrict__ ccnt, int nch,
                                                             double* __restrict__ partial, double* __restrict__ spart,
                                                             unsigned int* __restrict__ tickets,
                                                             double* __restrict__ out, unsigned long long* done_flag,
                                                             unsigned long long seq, const PassCmd* cmd,
                                                             PassCmd* mail, unsigned long long timeout,
                                                             unsigned long long* gtrace, int host_pollers) {
-  fdf_soa_body<true>(c, pos, base, ns, nch, Xf34{}, partial, spart, tickets, out, 0, done_flag, seq, cmd, mail,
+  fdf_soa_body<true>(c, ccnt, nch, Xf34{}, partial, spart, tickets, out, 0, done_flag, seq, cmd, mail,
                      timeout, gtrace, host_pollers, nullptr, 0);
 }
 
@@ -3555,11 +3665,16 @@ bool knn_logged_enabled() { return knn_two_phase(); }
 
 hipError_t launch_vl_sweep(const GridView& tgt, const VListView& vl, const float4* src, size_t p0, size_t p1,
                            Xf34 T, double thr, int seeded, uint32_t* nn_pos, uint32_t* flags, int cus,
-                           hipStream_t s) {
+                           hipStream_t s, const FusedCompact* fc) {
   if (p1 <= p0) return hipSuccess;
-  hipError_t e = hipMemsetAsync(vl.ctr + 1, 0, 2 * sizeof(unsigned int), s);
+  hipError_t e = hipMemsetAsync(vl.ctr + 1, 0, 3 * sizeof(unsigned int), s);
   if (e != hipSuccess) return e;
-  vl_query_kernel<<<nblk(p1 - p0), 256, 0, s>>>(vl, src, p0, p1 - p0, T, thr, nn_pos, flags);
+  if (fc)
+    vl_query_compact_kernel<<<chunk_count(p1 - p0), 256, 0, s>>>(vl, src, p0, p1 - p0, T, thr, nn_pos, flags, fc->cov_s,
+                                                                  fc->cov_t, fc->R, fc->cov_ok, fc->ccnt, fc->defer,
+                                                                  fc->out);
+  else
+    vl_query_kernel<<<nblk(p1 - p0), 256, 0, s>>>(vl, src, p0, p1 - p0, T, thr, nn_pos, flags);
   // requested cells: the centre's 1-NN within the gate + the grown cell's half diagonal, then the lists
   const double hd = std::sqrt(3.0) * (0.5 * static_cast<double>(vl.c) + static_cast<double>(vl.es));
   const double rc = vl.gate * (1.0 + 1e-5) + 1e-9 + hd;
@@ -3704,41 +3819,39 @@ hipError_t launch_morton_keys(const float4* pts, size_t p0, size_t n, const floa
   return hipGetLastError();
 }
 
-hipError_t launch_chunk_base(const uint32_t* pos, size_t ns, uint32_t* base, CorrSoA out, hipStream_t s) {
-  const int nch = chunk_count(ns);
-  if (nch == 0) return hipSuccess;
-  chunk_base_kernel<<<1, 1024, 0, s>>>(pos, ns, nch, base, out);
-  return hipGetLastError();
-}
 hipError_t launch_compact(const float4* src, const float4* tpts, const Cov3& cov_s,
                           const Cov3& cov_t, Rot33d R, const uint32_t* nn_pos,
-                          const uint32_t* flags, const uint32_t* pos, const uint32_t* chunk_base, size_t p0,
-                          size_t p1, CorrSoA out, hipStream_t s) {
-  if (p1 <= p0) return hipSuccess;
-  compact_kernel<<<nblk(p1 - p0), 256, 0, s>>>(src, tpts, cov_s, cov_t, R, nn_pos, flags, pos, chunk_base,
-                                               p0, p1, out);
+                          const uint32_t* flags, size_t p0, size_t p1, uint32_t* ccnt, CorrSoA out, hipStream_t s,
+                          const uint32_t* defer, const unsigned int* defer_count, int cus) {
+  const int nch = chunk_count(p1 - p0);
+  if (nch == 0) return hipSuccess;
+  if (defer)
+    chunk_compact_list_kernel<<<std::min(nch, 2 * std::max(cus, 1)), 256, 0, s>>>(
+        src, tpts, cov_s, cov_t, R, nn_pos, flags, p0, p1, ccnt, defer, defer_count, out);
+  else
+    chunk_compact_kernel<<<nch, 256, 0, s>>>(src, tpts, cov_s, cov_t, R, nn_pos, flags, p0, p1, ccnt, out);
   return hipGetLastError();
 }
 
-hipError_t launch_fdf_soa(const CorrSoA& c, const uint32_t* pos, const uint32_t* base, size_t ns, Xf34 A,
+hipError_t launch_fdf_soa(const CorrSoA& c, const uint32_t* ccnt, size_t ns, Xf34 A,
                           double* partial, double* spart, int nb, unsigned int* tickets, double* out, int reverse,
                           unsigned long long* done_flag, unsigned long long seq, hipStream_t s,
                           unsigned long long* host_rows, unsigned int rstamp) {
   const int nch = chunk_count(ns);
   if (nch == 0) return hipSuccess;
-  fdf_soa_kernel<<<nb, 256, 0, s>>>(c, pos, base, ns, nch, A, partial, spart, tickets, out, reverse, done_flag,
+  fdf_soa_kernel<<<nb, 256, 0, s>>>(c, ccnt, nch, A, partial, spart, tickets, out, reverse, done_flag,
                                     seq, host_rows, rstamp);
   return hipGetLastError();
 }
 
-hipError_t launch_fdf_soa_gated(const CorrSoA& c, const uint32_t* pos, const uint32_t* base, size_t ns,
+hipError_t launch_fdf_soa_gated(const CorrSoA& c, const uint32_t* ccnt, size_t ns,
                                 double* partial, double* spart, int nb, unsigned int* tickets, double* out,
                                 unsigned long long* done_flag, unsigned long long seq, const PassCmd* cmd,
                                 PassCmd* mail, unsigned long long timeout_ticks, unsigned long long* gtrace,
                                 int host_pollers, hipStream_t s) {
   const int nch = chunk_count(ns);
   if (nch == 0) return hipSuccess;
-  fdf_soa_gated_kernel<<<nb, 256, 0, s>>>(c, pos, base, ns, nch, partial, spart, tickets, out, done_flag, seq,
+  fdf_soa_gated_kernel<<<nb, 256, 0, s>>>(c, ccnt, nch, partial, spart, tickets, out, done_flag, seq,
                                           cmd, mail, timeout_ticks, gtrace, host_pollers);
   return hipGetLastError();
 }
@@ -3753,7 +3866,7 @@ int fdf_server_blocks(size_t ns, int cus, int waves) {
   return nb;
 }
 
-hipError_t launch_fdf_server(const CorrSoA& c, const uint32_t* pos, const uint32_t* base, size_t ns, double* partial,
+hipError_t launch_fdf_server(const CorrSoA& c, const uint32_t* ccnt, size_t ns, double* partial,
                              double* spart, unsigned int* tickets, double* out, unsigned long long* done_flag,
                              unsigned long long seq0, const PassCmd* cmd, PassCmd* mail,
                              unsigned long long timeout_ticks, unsigned long long* ptimes, int bench_passes,
@@ -3779,7 +3892,7 @@ hipError_t launch_fdf_server(const CorrSoA& c, const uint32_t* pos, const uint32
   if (e != hipSuccess) return e;
   if (per_cu < 1 || static_cast<long long>(per_cu) * cus < nb) return hipErrorCooperativeLaunchTooLarge;
 #define MGICP_SRV_LAUNCH(B, W)                                                                                  \
-  fdf_server_kernel<B, W><<<nb, 64 * (W), 0, s>>>(c, pos, base, ns, nch, partial, spart, tickets, out, done_flag, \
+  fdf_server_kernel<B, W><<<nb, 64 * (W), 0, s>>>(c, ccnt, nch, partial, spart, tickets, out, done_flag, \
                                                   seq0, cmd, mail, timeout_ticks, ptimes, bench_passes, A, host_rows, \
                                                   rows_stride, pollers, stall_pass, tpart)
   if (waves == 4) {
@@ -4000,7 +4113,9 @@ hipError_t preload_kernels(void* pinned, size_t pinned_bytes, hipStream_t s) {
       reinterpret_cast<const void*>(&knn_cov2_kernel<32>),
       reinterpret_cast<const void*>(&correspond_kernel),
       reinterpret_cast<const void*>(&morton_key_kernel),
-      reinterpret_cast<const void*>(&compact_kernel),
+      reinterpret_cast<const void*>(&chunk_compact_kernel),
+      reinterpret_cast<const void*>(&chunk_compact_list_kernel),
+      reinterpret_cast<const void*>(&vl_query_compact_kernel),
       reinterpret_cast<const void*>(&fdf_soa_kernel),
       reinterpret_cast<const void*>(&fdf_soa_gated_kernel),
       reinterpret_cast<const void*>(&fdf_server_kernel<false, 4>),
@@ -4013,7 +4128,6 @@ hipError_t preload_kernels(void* pinned, size_t pinned_bytes, hipStream_t s) {
       reinterpret_cast<const void*>(&reduce_finish_kernel),
       reinterpret_cast<const void*>(&gn_moments_kernel),
       reinterpret_cast<const void*>(&publish_kernel),
-      reinterpret_cast<const void*>(&chunk_base_kernel),
       reinterpret_cast<const void*>(&super_reduce_kernel<kRedVals>),
       reinterpret_cast<const void*>(&super_reduce_kernel<kMomVals>),
       reinterpret_cast<const void*>(&finish_supers_kernel<kRedVals>),

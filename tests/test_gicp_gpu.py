@@ -418,12 +418,14 @@ def test_covariances_any_k(engine_mod, part_small, k):
 
 
 @pytest.mark.gpu
-def test_async_covariance_prep_matches_sync(engine_mod, monkeypatch, part_small):
+@pytest.mark.parametrize("source_first", [False, True])
+def test_async_covariance_prep_matches_sync(engine_mod, monkeypatch, part_small, source_first):
     """r04: set_target / set_source build the cloud's grid and start its k-NN covariances on a
     second stream (the target's overlap the source's upload, the source's the first sweep); prepare
     and the first sweep join them.  Aligns, covariances, a k change while launches may still run,
     back-to-back set_* calls and a destroy with launches pending all match the synchronous path
-    (MGICP_ASYNC_COV=0) bit for bit."""
+    (MGICP_ASYNC_COV=0) bit for bit -- with the set_* calls in either order (the reference sets the
+    source first, GICPAlignment.cpp:89-90; the source grid must still start from the target's)."""
     scan, cad, _ = part_small
     cad2 = np.ascontiguousarray(cad[::-1])
     scan2 = np.ascontiguousarray(scan[::-1])
@@ -431,8 +433,12 @@ def test_async_covariance_prep_matches_sync(engine_mod, monkeypatch, part_small)
     for a in (1, 0):
         monkeypatch.setenv("MGICP_ASYNC_COV", str(a))
         e = engine_mod()
-        e.set_target_xyz(cad)
-        e.set_source_xyz(scan)
+        if source_first:
+            e.set_source_xyz(scan)
+            e.set_target_xyz(cad)
+        else:
+            e.set_target_xyz(cad)
+            e.set_source_xyz(scan)
         T = e.align()
         it = (e.last_result["iterations"], e.last_result["n_evals"])
         C = (e.debug_covariances("target", len(cad)), e.debug_covariances("source", len(scan)))
@@ -539,6 +545,43 @@ def _vlist_cases(part_small):
     lat = np.stack(np.meshgrid(g, g, np.float32([0.0, 0.005]), indexing="ij"), -1).reshape(-1, 3)
     lat = np.ascontiguousarray(lat + np.float32(1.5), np.float32)
     return [("part", src, tgt, Ttrue), ("fod", fsrc, ftgt, fT), ("lattice", lat.copy(), lat.copy(), np.eye(4))]
+
+
+@pytest.mark.parametrize("lazy", [0, 1])
+def test_fused_compaction_matches_unfused(engine_mod, part_small, monkeypatch, lazy):
+    """r04 fixed-slot compaction fused into the listed sweeps (vl_query_compact_kernel): chunks with
+    a pending query (cells being built) or, lazy = 1, an accepted point whose source covariance is
+    not computed yet (synchronous lazy source mode) are deferred to the compaction launch.  Every
+    sweep's indices and Mahalanobis matrices (cold, building, listed, new transforms that accept new
+    points) and three aligns equal the unfused path (MGICP_FUSE_COMPACT=0) bit for bit."""
+    name, src, tgt, Ttrue = _vlist_cases(part_small)[1]  # clutter + debris: gate rejections
+    Tinv = np.linalg.inv(Ttrue).astype(np.float32)
+    I = np.eye(4, dtype=np.float32)
+    off = np.eye(4, dtype=np.float32)
+    off[:3, 3] = [0.004, -0.003, 0.02]
+    Ts = [I, I, I, Tinv, off, Tinv, off]
+    monkeypatch.setenv("MGICP_ASYNC_COV", "0" if lazy else "1")
+    monkeypatch.setenv("MGICP_LAZY_SRC_COV", str(lazy))
+    res = {}
+    for fuse in (1, 0):
+        monkeypatch.setenv("MGICP_FUSE_COMPACT", str(fuse))
+        e = engine_mod()
+        e.set_target_xyz(tgt)
+        e.set_source_xyz(src)
+        sweeps = [e.debug_correspondences(T, len(src)) for T in Ts]
+        aligns = []
+        for _ in range(3):
+            T = e.align()
+            aligns.append((T, e.last_result["iterations"], e.last_result["n_evals"], e.last_result["n_corr"]))
+        e.close()
+        res[fuse] = (sweeps, aligns)
+    for (ma, ta, Ma), (mb, tb, Mb) in zip(res[1][0], res[0][0]):
+        assert ma == mb
+        np.testing.assert_array_equal(ta, tb)
+        np.testing.assert_array_equal(Ma, Mb)
+    for (Ta, *ra), (Tb, *rb) in zip(res[1][1], res[0][1]):
+        np.testing.assert_array_equal(Ta, Tb)
+        assert ra == rb
 
 
 @pytest.mark.parametrize("case,eager", [("part", 0), ("fod", 0), ("lattice", 0), ("part", 1)])
