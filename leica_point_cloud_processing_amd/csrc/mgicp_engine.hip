@@ -424,6 +424,8 @@ struct mgicp_ctx {
   // every point, computed while the first sweep runs)
   bool tgt_cov_pending = false;     // the aux stream's covariance launches not joined yet
   bool src_cov_pending = false;
+  bool src_async_lazy = false;      // the source's launch was ring-capped (lazy mode): the rest stays lazy
+  int async_ring_cap = 4;           // env MGICP_ASYNC_RING_CAP: rings the source's head start searches
   hipStream_t aux_stream = nullptr;
   hipEvent_t aux_ev[2] = {nullptr, nullptr};  // completion of the target's [0] / source's [1] launch
   DevBuf<unsigned int> aux_cnt;     // their hand-off counts: [0] target, [1] source
@@ -664,6 +666,7 @@ int cov_join(mgicp_ctx* ctx, bool tgt) {
                            nullptr, nullptr, ctx->stream));
     }
   }
+  if (!tgt && ctx->src_async_lazy) return MGICP_OK;  // the points it gave up on: computed if a sweep accepts them
   c.have_cov = true;
   c.cov_p0 = 0;
   c.cov_p1 = c.n;
@@ -686,6 +689,19 @@ int cov_prep_async(mgicp_ctx* ctx, bool tgt) {
   if (build_grid(ctx, c) != MGICP_OK || c.n < static_cast<size_t>(ctx->prm.k)) return MGICP_OK;
   HIPCK(c.cov.reserve(3 * c.n));
   c.cov_stride = c.n;
+  // the source in the lazy mode: a ring-capped launch (a point whose 20 neighbours lie beyond the
+  // cap -- scan clutter, debris -- is left to the lazy pass, which computes it only if a sweep accepts
+  // it; r04 C4F: the uncapped head start spent ~40 ms on them); its points are marked in cov_ok
+  const bool capped = !tgt && ctx->lazy_src_cov && ctx->knn_logged && ctx->async_ring_cap >= 0;
+  ctx->src_async_lazy = capped;
+  if (capped) {
+    HIPCK(ctx->cov_ok.reserve(c.n));
+    HIPCK(ctx->cov_need.reserve(c.n));
+    HIPCK(hipMemsetAsync(ctx->cov_ok.p, 0, c.n, ctx->stream));
+    ctx->src_lazy_ready = true;
+    ctx->src_lazy_p0 = 0;
+    ctx->src_lazy_p1 = c.n;
+  }
   if (ctx->knn_logged) {
     HIPCK((tgt ? ctx->knn_fb : ctx->knn_fb2).reserve(c.n));
     HIPCK(ctx->aux_cnt.reserve(2));
@@ -694,7 +710,8 @@ int cov_prep_async(mgicp_ctx* ctx, bool tgt) {
   HIPCK(hipStreamSynchronize(ctx->stream));  // the grid (and the count) before the aux stream reads them
   HIPCK(launch_knn_cov(c.view, ctx->prm.k, ctx->prm.gicp_eps, 0, c.n, c.cov3(), nullptr,
                        ctx->knn_logged ? (tgt ? ctx->knn_fb.p : ctx->knn_fb2.p) : nullptr,
-                       ctx->knn_logged ? ctx->aux_cnt.p + (tgt ? 0 : 1) : nullptr, ctx->aux_stream));
+                       ctx->knn_logged ? ctx->aux_cnt.p + (tgt ? 0 : 1) : nullptr, ctx->aux_stream,
+                       capped ? ctx->async_ring_cap : -1, capped ? ctx->cov_ok.p : nullptr));
   HIPCK(hipEventRecord(ctx->aux_ev[tgt ? 0 : 1], ctx->aux_stream));
   (tgt ? ctx->tgt_cov_pending : ctx->src_cov_pending) = true;
   return MGICP_OK;
@@ -2216,6 +2233,7 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
   if (const char* lc = std::getenv("MGICP_LAZY_TGT_COV")) ctx->lazy_tgt_cov = std::atoi(lc) != 0;
   if (const char* at = std::getenv("MGICP_ASYNC_COV")) ctx->async_tgt = std::atoi(at) != 0;
   if (const char* fc = std::getenv("MGICP_FUSE_COMPACT")) ctx->fuse_compact = std::atoi(fc) != 0;
+  if (const char* rc = std::getenv("MGICP_ASYNC_RING_CAP")) ctx->async_ring_cap = std::atoi(rc);
   ctx->tgt.want_pairs = ctx->corr_wave;
   if (const char* cb = std::getenv("MGICP_CELL_BOXES")) ctx->tgt.want_boxes = std::atoi(cb) != 0;
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {

@@ -122,9 +122,11 @@ hipError_t launch_xform_points(const float4* in, size_t n, Xf34 T, float4* out,
 // k-NN covariances of [p0, p1).  fb / fb_count (nullable): the logged-threshold kernel, which lists
 // in fb (count in *fb_count, device, zeroed by the caller) the points it leaves to the register-list
 // kernel; run that list with perm = fb, p0 = 0, p1 = count, fb = nullptr.
+// ring_cap >= 0 (logged kernel only): a query whose search passes that ring gives up -- no
+// covariance, not listed in fb, ok[p] stays 0; every other query sets ok[p] = 1 (ok nullable)
 hipError_t launch_knn_cov(const GridView& g, int k, double eps, size_t p0, size_t p1,
                           Cov3 cov, const uint32_t* perm /*nullable: query order*/, uint32_t* fb,
-                          unsigned int* fb_count, hipStream_t s);
+                          unsigned int* fb_count, hipStream_t s, int ring_cap = -1, uint8_t* ok = nullptr);
 bool knn_logged_enabled();  // env MGICP_KNN2 (default on)
 // nn_pos: per source point (shard-relative) the matched target sorted position, UINT32_MAX when
 // rejected; with `seeded` its previous contents seed the exact 1-NN search.  flags: 1 if accepted.

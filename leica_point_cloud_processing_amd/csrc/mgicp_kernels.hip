@@ -159,6 +159,12 @@ __device__ __forceinline__ void ring_search(const GridView& g, float qx, float q
                         static_cast<size_t>(g.nx) * (static_cast<size_t>(cy) + static_cast<size_t>(g.ny) * cz)];
   }
   for (int r = rmin; r < (1 << 22); ++r) {
+    if constexpr (V::kRingCap) {
+      if (r > vis.ring_cap) {
+        vis.gave_up = true;
+        return;
+      }
+    }
     if (r > 0) {
       const float L = fminf(fminf(axis_bound(qx, g.ox, g.h, cx, r - 1, g.nx),
                                   axis_bound(qy, g.oy, g.h, cy, r - 1, g.ny)),
@@ -297,6 +303,7 @@ __device__ __forceinline__ void ring_search_boxed(const GridView& g, float qx, f
 template <int K>
 struct KnnVisitor {
   static constexpr bool kNearFirst = true;
+  static constexpr bool kRingCap = false;
   float qx, qy, qz;
   unsigned long long key[K];
   uint32_t pos[K];
@@ -390,6 +397,7 @@ __device__ unsigned long long g_corr_stats[8];
 // exact 1-NN visitor, optionally bounded by an acceptance threshold thr on d2
 struct NnVisitor {
   static constexpr bool kNearFirst = false;
+  static constexpr bool kRingCap = false;
   float qx, qy, qz;
   double thr;
   float thr_f;  // float upper bound of thr (pruning radius cap)
@@ -535,6 +543,7 @@ __device__ __forceinline__ void box_search_lds(const GridView& g, float qx, floa
 // stopping as soon as `need` are found
 struct RadiusCountVisitor {
   static constexpr bool kNearFirst = false;
+  static constexpr bool kRingCap = false;
   float qx, qy, qz;
   float r2;
   int need, count;
@@ -807,6 +816,9 @@ constexpr int kLogBatch = MGICP_KNN_LOG_BATCH;
 template <int K>
 struct KthVisitor {
   static constexpr bool kNearFirst = true;
+  static constexpr bool kRingCap = true;
+  int ring_cap = 1 << 30;  // rings past this one: give up (the point's covariance is left for later)
+  bool gave_up = false;
   float qx, qy, qz;
   float key[K];  // ascending; the first nsent slots hold the sentinel -1 (always in front)
   uint32_t* lpos;  // lane-strided LDS log of sorted positions, cap entries
@@ -1005,7 +1017,8 @@ struct SumCert {
 template <int K>
 __global__ __launch_bounds__(64) void knn_cov2_kernel(GridView g, double eps, size_t p0, size_t p1, Cov3 cov,
                                                       const uint32_t* __restrict__ perm, int nsent, int cap,
-                                                      uint32_t* __restrict__ fb, unsigned int* __restrict__ fb_count) {
+                                                      uint32_t* __restrict__ fb, unsigned int* __restrict__ fb_count,
+                                                      int ring_cap, uint8_t* __restrict__ ok_out) {
   extern __shared__ uint32_t s_pos[];
   const size_t t = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (t >= p1 - p0) return;
@@ -1019,7 +1032,11 @@ __global__ __launch_bounds__(64) void knn_cov2_kernel(GridView g, double eps, si
   v1.lpos = s_pos + threadIdx.x;
   v1.pts = g.pts;
   v1.cap = cap;
+  if (ring_cap >= 0) v1.ring_cap = ring_cap;
   ring_search(g, q.x, q.y, q.z, v1);
+  // ring_cap (the source's head start, lazy mode): a point whose k-NN lie farther out (clutter, debris)
+  // is left to the lazy pass, which computes it only if a sweep accepts it (ok_out stays 0)
+  if (v1.gave_up) return;
 #if MGICP_KNN_DIV
   {  // [18] wave iterations of test() [19] max over lanes of the lane's tests [20] lane tests [21] waves
     // [22] search cycles [23] moments + finish cycles (shader clock, summed over waves)
@@ -1089,6 +1106,7 @@ __global__ __launch_bounds__(64) void knn_cov2_kernel(GridView g, double eps, si
   // log overflow, ties at tau or an uncertified sum: KnnVisitor's sorted (d2, index) list finishes
   // this point in a follow-up launch over the list (knn_cov_kernel with perm = fb)
   if (!ok) fb[atomicAdd(fb_count, 1u)] = static_cast<uint32_t>(p);
+  if (ok_out) ok_out[p] = 1;  // computed here or by the hand-off launch
 }
 
 // ------------------------------------------------------------------------------------
@@ -3411,6 +3429,7 @@ __global__ void scatter_flagged_kernel(const float4* __restrict__ in, const uint
 // proves absence before giving up)
 struct WithinVisitor {
   static constexpr bool kNearFirst = false;
+  static constexpr bool kRingCap = false;
   float qx, qy, qz;
   double thr;
   float thr_f;  // float upper bound of thr (pruning radius)
@@ -3627,11 +3646,13 @@ static bool knn_two_phase() {  // env MGICP_KNN2 (default 1): knn_cov2_kernel, e
 
 template <int K>
 static hipError_t knn_cov_k(const GridView& g, double eps, size_t p0, size_t p1, Cov3 cov,
-                            const uint32_t* perm, int k, uint32_t* fb, unsigned int* fb_count, hipStream_t s) {
+                            const uint32_t* perm, int k, uint32_t* fb, unsigned int* fb_count, hipStream_t s,
+                            int ring_cap, uint8_t* ok) {
   if (fb) {
     const int cap = knn_log_cap(K);
     knn_cov2_kernel<K><<<nblk(p1 - p0, 64), 64, cap * 64 * sizeof(uint32_t), s>>>(g, eps, p0, p1, cov, perm,
-                                                                                 K - k, cap, fb, fb_count);
+                                                                                 K - k, cap, fb, fb_count, ring_cap,
+                                                                                 ok);
   } else {
     knn_cov_kernel<K><<<nblk(p1 - p0), 256, 0, s>>>(g, eps, p0, p1, cov, perm, K - k);
   }
@@ -3643,22 +3664,23 @@ static hipError_t knn_cov_k(const GridView& g, double eps, size_t p0, size_t p1,
 // logged-threshold kernel runs and lists the points it leaves to KnnVisitor; without, (or for that
 // list: perm = fb, p0 = 0, p1 = count) the register-list kernel runs.
 hipError_t launch_knn_cov(const GridView& g, int k, double eps, size_t p0, size_t p1, Cov3 cov,
-                          const uint32_t* perm, uint32_t* fb, unsigned int* fb_count, hipStream_t s) {
+                          const uint32_t* perm, uint32_t* fb, unsigned int* fb_count, hipStream_t s, int ring_cap,
+                          uint8_t* ok) {
   if (p1 <= p0) return hipSuccess;
   switch (k) {
-    case 5: return knn_cov_k<5>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s);
-    case 10: return knn_cov_k<10>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s);
-    case 15: return knn_cov_k<15>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s);
-    case 20: return knn_cov_k<20>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s);
-    case 25: return knn_cov_k<25>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s);
-    case 30: return knn_cov_k<30>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s);
+    case 5: return knn_cov_k<5>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok);
+    case 10: return knn_cov_k<10>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok);
+    case 15: return knn_cov_k<15>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok);
+    case 20: return knn_cov_k<20>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok);
+    case 25: return knn_cov_k<25>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok);
+    case 30: return knn_cov_k<30>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok);
     default: break;
   }
   if (k < 1 || k > kMaxK) return hipErrorInvalidValue;
-  if (k <= 8) return knn_cov_k<8>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s);
-  if (k <= 16) return knn_cov_k<16>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s);
-  if (k <= 24) return knn_cov_k<24>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s);
-  return knn_cov_k<32>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s);
+  if (k <= 8) return knn_cov_k<8>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok);
+  if (k <= 16) return knn_cov_k<16>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok);
+  if (k <= 24) return knn_cov_k<24>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok);
+  return knn_cov_k<32>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok);
 }
 
 bool knn_logged_enabled() { return knn_two_phase(); }
