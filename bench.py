@@ -570,7 +570,7 @@ def main():
         "fdf_72B_stored": stored,
         "fdf_launched_52B": launched,
         "correspondence_plus_mahalanobis": roof(
-            "correspond_wave_kernel + compact_kernel (1-NN sweep, Mahalanobis, compaction; once per outer iteration)",
+            "vl_query_compact_kernel (listed 1-NN sweep with the Mahalanobis compaction fused, r04) + chunk_compact_list_kernel (its deferred chunks); once per outer iteration",
             CORR_BYTES, n_shard, corr_ms, kt["correspond"]["count"], "correspond_plus_compact",
             "SURVEY 8d: 72 B per source point (s 12 + Cs 24 + NN 12 + Ct 24)"),
         "knn_cov": roof(

@@ -7,8 +7,8 @@ STREAMING read, and "other access widths are uncalibrated".  So the x2 correctio
 kernel only where the kernel's reads are all 16-byte-per-lane coalesced streams:
   * fdf_soa_kernel and the resident server's streamed part (fdf_server_kernel<true, W>) -- every load
     is a float4 / double2 stream at consecutive addresses: x2;
-  * correspond_kernel, knn_cov_kernel, fitness / segdiff (grid gathers), compact_kernel and
-    gn_moments_kernel (coalesced 4 B index loads mixed with 16 B gathers): raw FETCH_SIZE,
+  * correspond_kernel, the 1-NN cell-list kernels, knn_cov_kernel, fitness / segdiff (grid gathers),
+    the compaction kernels and gn_moments_kernel (coalesced 4 B index loads mixed with 16 B gathers): raw FETCH_SIZE,
     labelled uncalibrated -- the true HBM bytes lie between 1x and 2x the raw figure.
 WRITE_SIZE is taken as is.  FETCH_SIZE and WRITE_SIZE come from separate --pmc passes.
 
@@ -25,7 +25,9 @@ STREAMING = {"fdf_soa_kernel", "fdf_server_kernel<true"}
 # --pass-bench-passes): its figures are per pass (dispatch / PASSES, the one-time resident load
 # included pro rata)
 PASSES = {"fdf_server_kernel<true": int(os.environ.get("PASS_BENCH_PASSES", "50"))}
-KERNELS = ("fdf_server_kernel<true", "fdf_soa_kernel", "correspond_wave_kernel", "correspond_kernel", "compact_kernel", "chunk_base_kernel", "knn_cov2_kernel",
+KERNELS = ("fdf_server_kernel<true", "fdf_soa_kernel", "vl_query_compact_kernel", "vl_query_kernel",
+           "vl_fallback_kernel", "vl_build_kernel", "chunk_compact_list_kernel", "chunk_compact_kernel",
+           "correspond_wave_kernel", "correspond_kernel", "knn_cov2_kernel",
            "knn_cov_kernel", "fitness_kernel", "gn_moments_kernel", "segdiff_kernel", "voxel_key_kernel",
            "voxel_centroid_kernel")
 
@@ -40,9 +42,19 @@ def per_dispatch(directory, counter, kernel):
     return vals
 
 
-def entry(fk, wk, streaming, passes=1):
-    f_kib = sum(fk) / len(fk) / passes
-    w_kib = sum(wk) / len(wk) / passes
+# r04: the listed sweep's kernels run in three states in one bench run (the align that builds the
+# lists defers most chunks to the compaction launch; the timed aligns defer none): their figure is the
+# MEDIAN dispatch, i.e. the steady state the timed aligns run
+MEDIAN = {"vl_query_compact_kernel", "chunk_compact_list_kernel"}
+
+
+def entry(fk, wk, streaming, passes=1, median=False):
+    if median:
+        f_kib = sorted(fk)[len(fk) // 2] / passes
+        w_kib = sorted(wk)[len(wk) // 2] / passes
+    else:
+        f_kib = sum(fk) / len(fk) / passes
+        w_kib = sum(wk) / len(wk) / passes
     mult = 2.0 if streaming else 1.0
     return {
         "dispatches": len(fk),
@@ -62,17 +74,25 @@ def main():
     for k in KERNELS:
         fk, wk = per_dispatch(fdir, "FETCH_SIZE", k), per_dispatch(wdir, "WRITE_SIZE", k)
         if fk and wk:
-            kernels[k] = entry(fk, wk, k in STREAMING, PASSES.get(k, 1))
+            kernels[k] = entry(fk, wk, k in STREAMING, PASSES.get(k, 1), k in MEDIAN)
+            if k in MEDIAN:
+                kernels[k]["per"] = "median dispatch (steady state of the timed aligns)"
             if k in PASSES:
                 kernels[k]["per"] = f"pass (dispatch / {PASSES[k]})"
     if "fdf_server_kernel<true" in kernels:  # bench.py's key for the server's roofline traffic
         kernels["fdf_server_kernel"] = kernels.pop("fdf_server_kernel<true")
-    sweep = "correspond_wave_kernel" if "correspond_wave_kernel" in kernels else "correspond_kernel"
-    if sweep in kernels and "compact_kernel" in kernels:
-        a, b = kernels[sweep], kernels["compact_kernel"]
+    # the sweep + compaction of the timed aligns: r04 the fused listed sweep (vl_query_compact_kernel,
+    # its deferred chunks in chunk_compact_list_kernel), before the r03 sweep + its compaction
+    if "vl_query_compact_kernel" in kernels:
+        parts = [kernels["vl_query_compact_kernel"]] + [kernels[k] for k in ("chunk_compact_list_kernel",) if k in kernels]
+    else:
+        sweep = "correspond_wave_kernel" if "correspond_wave_kernel" in kernels else "correspond_kernel"
+        comp = "chunk_compact_kernel"
+        parts = [kernels[k] for k in (sweep, comp) if k in kernels] if sweep in kernels and comp in kernels else []
+    if parts:
         kernels["correspond_plus_compact"] = {
-            "hbm_bytes_per_launch": a["hbm_bytes_per_launch"] + b["hbm_bytes_per_launch"],
-            "correction": a["correction"],
+            "hbm_bytes_per_launch": sum(p["hbm_bytes_per_launch"] for p in parts),
+            "correction": parts[0]["correction"],
         }
     if "fdf_soa_kernel" not in kernels:
         raise SystemExit("no counters found for fdf_soa_kernel")
