@@ -426,8 +426,8 @@ struct mgicp_ctx {
   bool src_cov_pending = false;
   bool src_async_lazy = false;      // the source's launch was ring-capped (lazy mode): the rest stays lazy
   int async_ring_cap = 4;           // env MGICP_ASYNC_RING_CAP: rings the source's head start searches
-  hipStream_t aux_stream = nullptr;
-  hipEvent_t aux_ev[2] = {nullptr, nullptr};  // completion of the target's [0] / source's [1] launch
+  hipStream_t aux_stream[2] = {nullptr, nullptr};  // the target's [0] / source's [1] launches (concurrent)
+  hipEvent_t aux_ev[2] = {nullptr, nullptr};        // their completion
   DevBuf<unsigned int> aux_cnt;     // their hand-off counts: [0] target, [1] source
   DevBuf<uint32_t> knn_fb2;         // the source's hand-off list
   bool knn_logged = true;           // env MGICP_KNN2 at create: logged k-NN kernel, else register-list
@@ -683,7 +683,7 @@ int cov_join_all(mgicp_ctx* ctx) {
 // failure leaves the cloud for prepare, which reports it as before.
 int cov_prep_async(mgicp_ctx* ctx, bool tgt) {
   Cloud& c = tgt ? ctx->tgt : ctx->src;
-  if (!ctx->async_tgt || !ctx->aux_stream || ctx->nranks != 1 || ctx->comm || ctx->have_shm || ctx->profiling ||
+  if (!ctx->async_tgt || !ctx->aux_stream[tgt ? 0 : 1] || ctx->nranks != 1 || ctx->comm || ctx->have_shm || ctx->profiling ||
       (tgt && ctx->lazy_tgt_cov) || static_cast<size_t>(ctx->prm.k) > c.n)
     return MGICP_OK;
   if (build_grid(ctx, c) != MGICP_OK || c.n < static_cast<size_t>(ctx->prm.k)) return MGICP_OK;
@@ -710,9 +710,9 @@ int cov_prep_async(mgicp_ctx* ctx, bool tgt) {
   HIPCK(hipStreamSynchronize(ctx->stream));  // the grid (and the count) before the aux stream reads them
   HIPCK(launch_knn_cov(c.view, ctx->prm.k, ctx->prm.gicp_eps, 0, c.n, c.cov3(), nullptr,
                        ctx->knn_logged ? (tgt ? ctx->knn_fb.p : ctx->knn_fb2.p) : nullptr,
-                       ctx->knn_logged ? ctx->aux_cnt.p + (tgt ? 0 : 1) : nullptr, ctx->aux_stream,
+                       ctx->knn_logged ? ctx->aux_cnt.p + (tgt ? 0 : 1) : nullptr, ctx->aux_stream[tgt ? 0 : 1],
                        capped ? ctx->async_ring_cap : -1, capped ? ctx->cov_ok.p : nullptr));
-  HIPCK(hipEventRecord(ctx->aux_ev[tgt ? 0 : 1], ctx->aux_stream));
+  HIPCK(hipEventRecord(ctx->aux_ev[tgt ? 0 : 1], ctx->aux_stream[tgt ? 0 : 1]));
   (tgt ? ctx->tgt_cov_pending : ctx->src_cov_pending) = true;
   return MGICP_OK;
 }
@@ -2250,16 +2250,17 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
     delete ctx;
     return MGICP_E_HIP;
   }
-  // the second stream of set_target's covariance head start (created here: a stream's creation costs
-  // milliseconds of host time, which set_target would otherwise pay before the launch)
-  if (ctx->async_tgt && (hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking) != hipSuccess ||
-                         hipEventCreateWithFlags(&ctx->aux_ev[0], hipEventDisableTiming) != hipSuccess ||
-                         hipEventCreateWithFlags(&ctx->aux_ev[1], hipEventDisableTiming) != hipSuccess)) {
-    if (ctx->aux_stream) (void)hipStreamDestroy(ctx->aux_stream);
-    for (hipEvent_t& e : ctx->aux_ev)
-      if (e) (void)hipEventDestroy(e), e = nullptr;
-    ctx->aux_stream = nullptr;
-  }
+  // the streams of the covariance head start, one per cloud so both k-NN passes can run at once
+  // (created here: a stream's creation costs milliseconds of host time, which set_* would otherwise
+  // pay before the launch)
+  for (int i = 0; i < 2 && ctx->async_tgt; ++i)
+    if (hipStreamCreateWithFlags(&ctx->aux_stream[i], hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&ctx->aux_ev[i], hipEventDisableTiming) != hipSuccess) {
+      if (ctx->aux_stream[i]) (void)hipStreamDestroy(ctx->aux_stream[i]);
+      if (ctx->aux_ev[i]) (void)hipEventDestroy(ctx->aux_ev[i]);
+      ctx->aux_stream[i] = nullptr;
+      ctx->aux_ev[i] = nullptr;
+    }
   *out = ctx;
   return MGICP_OK;
 }
@@ -2288,7 +2289,8 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   cancel_gated(ctx);
-  if (ctx->aux_stream) (void)hipStreamSynchronize(ctx->aux_stream);
+  for (hipStream_t a : ctx->aux_stream)
+    if (a) (void)hipStreamSynchronize(a);
   ctx->tgt_cov_pending = ctx->src_cov_pending = false;
   (void)hipStreamSynchronize(ctx->stream);
   srv_release(ctx);
@@ -2337,7 +2339,8 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   for (hipEvent_t e : ctx->pool) (void)hipEventDestroy(e);
   if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
-  if (ctx->aux_stream) (void)hipStreamDestroy(ctx->aux_stream);
+  for (hipStream_t a : ctx->aux_stream)
+    if (a) (void)hipStreamDestroy(a);
   for (hipEvent_t e : ctx->aux_ev)
     if (e) (void)hipEventDestroy(e);
   delete ctx;

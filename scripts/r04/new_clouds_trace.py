@@ -13,14 +13,19 @@ for rep in range(3):
     e = GICPEngine()
     print(f"---- rep {rep}: new engine ----", file=sys.stderr, flush=True)
     t0 = time.perf_counter()
-    e.set_target_xyz(cad)
-    t1 = time.perf_counter()
-    e.set_source_xyz(scan)
+    if os.environ.get("SOURCE_FIRST") == "1":  # the reference's order (GICPAlignment.cpp:89-90)
+        e.set_source_xyz(scan)
+        t1 = time.perf_counter()
+        e.set_target_xyz(cad)
+    else:
+        e.set_target_xyz(cad)
+        t1 = time.perf_counter()
+        e.set_source_xyz(scan)
     t2 = time.perf_counter()
     e.align()
     t3 = time.perf_counter()
     r = e.last_result
-    print(f"rep {rep}: set_target {1e3*(t1-t0):.3f} ms, set_source {1e3*(t2-t1):.3f} ms, align {1e3*(t3-t2):.3f} ms, "
+    print(f"rep {rep} ({'source' if os.environ.get('SOURCE_FIRST') == '1' else 'target'} first): set_* {1e3*(t1-t0):.3f} ms, set_* {1e3*(t2-t1):.3f} ms, align {1e3*(t3-t2):.3f} ms, "
           f"total {1e3*(t3-t0):.3f} ms | upload {r['ms_upload']:.3f} prep {r['ms_prep']:.3f} loop {r['ms_loop']:.3f}",
           flush=True)
     e.close()
