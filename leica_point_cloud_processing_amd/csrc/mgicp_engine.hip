@@ -178,6 +178,27 @@ void r_derivative(const Vec6& x, const double R[3][3], Vec6& g) {
   }
 }
 
+// Device buffers a reserve() replaces are freed at quiet points (the end of an align, a destroy), not
+// at once: hipFree waits for the whole device, which stalled set_*'s grid build behind the other
+// cloud's covariance head start on the second stream (r04, ~2 ms, profiles/r04/prep7)
+struct Graveyard {
+  std::mutex mu;
+  std::vector<void*> v;
+};
+Graveyard& graveyard() {
+  static Graveyard g;
+  return g;
+}
+void defer_free(void* p) {
+  std::lock_guard<std::mutex> lk(graveyard().mu);
+  graveyard().v.push_back(p);
+}
+void flush_graveyard() {
+  std::lock_guard<std::mutex> lk(graveyard().mu);
+  for (void* p : graveyard().v) (void)hipFree(p);
+  graveyard().v.clear();
+}
+
 template <class T>
 struct DevBuf {
   T* p = nullptr;
@@ -187,7 +208,7 @@ struct DevBuf {
   hipError_t reserve(size_t n) {
     if (n <= cap && p) return hipSuccess;
     const size_t want = std::max<size_t>(std::max<size_t>(n, 1), cap ? cap + cap / 4 : 0);
-    if (p) (void)hipFree(p);
+    if (p) defer_free(p);
     p = nullptr;
     cap = 0;
     hipError_t e = hipMalloc(&p, want * sizeof(T));
@@ -420,14 +441,17 @@ struct mgicp_ctx {
   // r04: set_target builds the target's grid and starts its k-NN covariances on a second stream, so
   // they run while the caller uploads the source; prepare joins them (env MGICP_ASYNC_COV=0: off)
   bool async_tgt = true;
+  int aux_cu_skip = 8;              // the aux stream leaves every 8th CU to the main stream (A/B 0, 2, 4, 8: profiles/r04/ncab1)
   // (and set_source the source's: single rank, same stream; with the lazy source mode these cover
   // every point, computed while the first sweep runs)
   bool tgt_cov_pending = false;     // the aux stream's covariance launches not joined yet
   bool src_cov_pending = false;
   bool src_async_lazy = false;      // the source's launch was ring-capped (lazy mode): the rest stays lazy
   int async_ring_cap = 4;           // env MGICP_ASYNC_RING_CAP: rings the source's head start searches
-  hipStream_t aux_stream[2] = {nullptr, nullptr};  // the target's [0] / source's [1] launches (concurrent)
-  hipEvent_t aux_ev[2] = {nullptr, nullptr};        // their completion
+  // one stream for both clouds' launches: with a stream each the process exceeds its hardware queues
+  // (GPU_MAX_HW_QUEUES, 4) and the main stream ends up sharing one with them (profiles/r04/prep7)
+  hipStream_t aux_stream = nullptr;
+  hipEvent_t aux_ev[2] = {nullptr, nullptr};  // completion of the target's [0] / source's [1] launch
   DevBuf<unsigned int> aux_cnt;     // their hand-off counts: [0] target, [1] source
   DevBuf<uint32_t> knn_fb2;         // the source's hand-off list
   bool knn_logged = true;           // env MGICP_KNN2 at create: logged k-NN kernel, else register-list
@@ -441,6 +465,7 @@ struct mgicp_ctx {
   float vlist_cell = 0.6f;            // fine cell edge / the target grid's cell edge (env MGICP_VLIST_CELL)
   bool vl_stats = false;              // env MGICP_VLIST_STATS: per-sweep list diagnostics on stderr
   bool vl_valid = false;              // lists belong to the current target grid and gate
+  bool vl_alloc = false;              // their state words and pool are allocated and initialised
   bool vl_off = false;                // the gate is too large for a fine grid of this target: r03 sweeps
   VListView vl{};
   size_t vl_ncells = 0;
@@ -653,18 +678,16 @@ int cov_join(mgicp_ctx* ctx, bool tgt) {
   if (!pending) return MGICP_OK;
   pending = false;
   Cloud& c = tgt ? ctx->tgt : ctx->src;
-  HIPCK(hipEventSynchronize(ctx->aux_ev[tgt ? 0 : 1]));  // this cloud's launch only
-  if (ctx->knn_logged) {
+  // this cloud's launches only (the logged k-NN pass and its hand-off, chained on the aux stream):
+  // the main stream waits for them on the device, the host does not
+  HIPCK(hipStreamWaitEvent(ctx->stream, ctx->aux_ev[tgt ? 0 : 1], 0));
+  if (ctx->knn_logged && std::getenv("MGICP_KNN_STATS")) {  // as compute_cov reports it
     unsigned int nfb = 0;
-    HIPCK(hipMemcpy(&nfb, ctx->aux_cnt.p + (tgt ? 0 : 1), sizeof(nfb), hipMemcpyDeviceToHost));
+    HIPCK(hipMemcpyAsync(ctx->h_small, ctx->aux_cnt.p + (tgt ? 0 : 1), sizeof(nfb), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCK(hipStreamSynchronize(ctx->stream));
+    std::memcpy(&nfb, ctx->h_small, sizeof(nfb));
     ctx->knn_fallbacks = nfb;
-    if (std::getenv("MGICP_KNN_STATS"))  // as compute_cov reports it
-      std::fprintf(stderr, "[knn] %zu points, %u left to the register-list kernel\n", c.n, nfb);
-    if (nfb) {
-      ProfScope ps(ctx, kFamCov);
-      HIPCK(launch_knn_cov(c.view, ctx->prm.k, ctx->prm.gicp_eps, 0, nfb, c.cov3(), tgt ? ctx->knn_fb.p : ctx->knn_fb2.p,
-                           nullptr, nullptr, ctx->stream));
-    }
+    std::fprintf(stderr, "[knn] %zu points, %u left to the register-list kernel\n", c.n, nfb);
   }
   if (!tgt && ctx->src_async_lazy) return MGICP_OK;  // the points it gave up on: computed if a sweep accepts them
   c.have_cov = true;
@@ -683,7 +706,7 @@ int cov_join_all(mgicp_ctx* ctx) {
 // failure leaves the cloud for prepare, which reports it as before.
 int cov_prep_async(mgicp_ctx* ctx, bool tgt) {
   Cloud& c = tgt ? ctx->tgt : ctx->src;
-  if (!ctx->async_tgt || !ctx->aux_stream[tgt ? 0 : 1] || ctx->nranks != 1 || ctx->comm || ctx->have_shm || ctx->profiling ||
+  if (!ctx->async_tgt || !ctx->aux_stream || ctx->nranks != 1 || ctx->comm || ctx->have_shm || ctx->profiling ||
       (tgt && ctx->lazy_tgt_cov) || static_cast<size_t>(ctx->prm.k) > c.n)
     return MGICP_OK;
   if (build_grid(ctx, c) != MGICP_OK || c.n < static_cast<size_t>(ctx->prm.k)) return MGICP_OK;
@@ -710,9 +733,10 @@ int cov_prep_async(mgicp_ctx* ctx, bool tgt) {
   HIPCK(hipStreamSynchronize(ctx->stream));  // the grid (and the count) before the aux stream reads them
   HIPCK(launch_knn_cov(c.view, ctx->prm.k, ctx->prm.gicp_eps, 0, c.n, c.cov3(), nullptr,
                        ctx->knn_logged ? (tgt ? ctx->knn_fb.p : ctx->knn_fb2.p) : nullptr,
-                       ctx->knn_logged ? ctx->aux_cnt.p + (tgt ? 0 : 1) : nullptr, ctx->aux_stream[tgt ? 0 : 1],
-                       capped ? ctx->async_ring_cap : -1, capped ? ctx->cov_ok.p : nullptr));
-  HIPCK(hipEventRecord(ctx->aux_ev[tgt ? 0 : 1], ctx->aux_stream[tgt ? 0 : 1]));
+                       ctx->knn_logged ? ctx->aux_cnt.p + (tgt ? 0 : 1) : nullptr, ctx->aux_stream,
+                       capped ? ctx->async_ring_cap : -1, capped ? ctx->cov_ok.p : nullptr,
+                       ctx->knn_logged ? 2 * std::max(ctx->cus, 1) : 0));
+  HIPCK(hipEventRecord(ctx->aux_ev[tgt ? 0 : 1], ctx->aux_stream));
   (tgt ? ctx->tgt_cov_pending : ctx->src_cov_pending) = true;
   return MGICP_OK;
 }
@@ -1596,6 +1620,18 @@ int vl_prepare(mgicp_ctx* ctx) {
     v.nx = nd[0];
     v.ny = nd[1];
     v.nz = nd[2];
+    ctx->vl_ncells = nc;
+    ctx->vl_valid = true;
+    ctx->vl_alloc = false;
+    ctx->vl_epoch = 0;
+    ctx->vl_groups = 0;
+  }
+  // the state words and the pool (~0.4 + 2 GB at C4) only once a sweep uses the lists: the first align
+  // after a set_target runs the r03 sweep and must not pay for their allocation (r04)
+  if (!ctx->vl_off && !ctx->vl_alloc && (ctx->vl_groups > 0 || !ctx->vl_cold_r03)) {
+    const Cloud& t = ctx->tgt;
+    VListView& v = ctx->vl;
+    const size_t nc = ctx->vl_ncells;
     HIPCK(ctx->vl_cell.reserve(nc));
     HIPCK(hipMemsetAsync(ctx->vl_cell.p, 0xff, nc * sizeof(uint32_t), ctx->stream));
     // list starts are stored in units of 4 entries in 25 bits: at most 2^27 entries (16 bytes each)
@@ -1607,12 +1643,9 @@ int vl_prepare(mgicp_ctx* ctx) {
     v.pool = ctx->vl_pool.p;
     v.pool_cap = static_cast<uint32_t>(cap);
     v.ctr = ctx->vl_ctr.p;
-    ctx->vl_ncells = nc;
-    ctx->vl_valid = true;
-    ctx->vl_epoch = 0;
-    ctx->vl_groups = 0;
+    ctx->vl_alloc = true;
   }
-  if (ctx->vl_off) return MGICP_OK;
+  if (ctx->vl_off || !ctx->vl_alloc) return MGICP_OK;
   // per-sweep lists sized by the shard (one request / pending entry per query at most)
   const size_t q = std::max<size_t>(ns, 1);
   HIPCK(ctx->vl_build.reserve(q));
@@ -1635,7 +1668,7 @@ int vl_prepare(mgicp_ctx* ctx) {
 // wave-uniform scan when the target has its pair copy, else the per-lane search (env MGICP_VLIST=0,
 // MGICP_CORR_WAVE=0); all exact, same results.
 bool sweep_listed(const mgicp_ctx* ctx) {
-  return ctx->vlist && ctx->vl_valid && !ctx->vl_off && (ctx->vl_groups > 0 || !ctx->vl_cold_r03);
+  return ctx->vlist && ctx->vl_valid && ctx->vl_alloc && !ctx->vl_off && (ctx->vl_groups > 0 || !ctx->vl_cold_r03);
 }
 
 // fc (nullable, listed sweeps only): the compaction fused into the sweep
@@ -1700,7 +1733,7 @@ int correspond(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
     HIPCK(launch_sweep(ctx, T, thr, seeded, qp, fused ? &fc : nullptr));
   }
   ctx->seed_valid = true;
-  if (ctx->vl_stats && ctx->vlist && !ctx->vl_off && (ctx->vl_groups > 0 || !ctx->vl_cold_r03)) {
+  if (ctx->vl_stats && sweep_listed(ctx)) {
     unsigned int c3[3];
     HIPCK(hipMemcpyAsync(c3, ctx->vl_ctr.p, 3 * sizeof(unsigned int), hipMemcpyDeviceToHost, s));
     HIPCK(ctx->u64.reserve(64));
@@ -2234,6 +2267,7 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
   if (const char* at = std::getenv("MGICP_ASYNC_COV")) ctx->async_tgt = std::atoi(at) != 0;
   if (const char* fc = std::getenv("MGICP_FUSE_COMPACT")) ctx->fuse_compact = std::atoi(fc) != 0;
   if (const char* rc = std::getenv("MGICP_ASYNC_RING_CAP")) ctx->async_ring_cap = std::atoi(rc);
+  if (const char* cs = std::getenv("MGICP_AUX_CU_SKIP")) ctx->aux_cu_skip = std::atoi(cs);
   ctx->tgt.want_pairs = ctx->corr_wave;
   if (const char* cb = std::getenv("MGICP_CELL_BOXES")) ctx->tgt.want_boxes = std::atoi(cb) != 0;
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -2250,17 +2284,33 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
     delete ctx;
     return MGICP_E_HIP;
   }
-  // the streams of the covariance head start, one per cloud so both k-NN passes can run at once
-  // (created here: a stream's creation costs milliseconds of host time, which set_* would otherwise
-  // pay before the launch)
-  for (int i = 0; i < 2 && ctx->async_tgt; ++i)
-    if (hipStreamCreateWithFlags(&ctx->aux_stream[i], hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&ctx->aux_ev[i], hipEventDisableTiming) != hipSuccess) {
-      if (ctx->aux_stream[i]) (void)hipStreamDestroy(ctx->aux_stream[i]);
-      if (ctx->aux_ev[i]) (void)hipEventDestroy(ctx->aux_ev[i]);
-      ctx->aux_stream[i] = nullptr;
-      ctx->aux_ev[i] = nullptr;
+  // the pass path's pinned command / result words and the BAR command block (its memset is
+  // synchronous): here, not in the first align, where they waited for the covariance head start
+  (void)ensure_host_red(ctx);  // (retried by the first align if it failed)
+  // the stream of the covariance head start (created here: a stream's creation costs milliseconds
+  // of host time, which set_* would otherwise pay before the launch)
+  // on a CU mask that leaves every ctx->aux_cu_skip-th CU free (env MGICP_AUX_CU_SKIP, 8; 0: all CUs):
+  // its k-NN grids (78k blocks at 5M) otherwise take every CU and the main stream's grid build and
+  // first sweep wait behind them (stream priorities did not change that, profiles/r04/prep12)
+  hipError_t se = hipSuccess;
+  if (ctx->async_tgt) {
+    if (ctx->aux_cu_skip > 1 && ctx->cus > 0) {
+      std::vector<uint32_t> mask(static_cast<size_t>((ctx->cus + 31) / 32), 0u);
+      for (int c = 0; c < ctx->cus; ++c)
+        if (c % ctx->aux_cu_skip != ctx->aux_cu_skip - 1) mask[c / 32] |= 1u << (c % 32);
+      se = hipExtStreamCreateWithCUMask(&ctx->aux_stream, static_cast<uint32_t>(mask.size()), mask.data());
+    } else {
+      se = hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking);
     }
+  }
+  if (ctx->async_tgt && (se != hipSuccess ||
+                         hipEventCreateWithFlags(&ctx->aux_ev[0], hipEventDisableTiming) != hipSuccess ||
+                         hipEventCreateWithFlags(&ctx->aux_ev[1], hipEventDisableTiming) != hipSuccess)) {
+    if (ctx->aux_stream) (void)hipStreamDestroy(ctx->aux_stream);
+    for (hipEvent_t& ev : ctx->aux_ev)
+      if (ev) (void)hipEventDestroy(ev), ev = nullptr;
+    ctx->aux_stream = nullptr;
+  }
   *out = ctx;
   return MGICP_OK;
 }
@@ -2289,8 +2339,7 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   cancel_gated(ctx);
-  for (hipStream_t a : ctx->aux_stream)
-    if (a) (void)hipStreamSynchronize(a);
+  if (ctx->aux_stream) (void)hipStreamSynchronize(ctx->aux_stream);
   ctx->tgt_cov_pending = ctx->src_cov_pending = false;
   (void)hipStreamSynchronize(ctx->stream);
   srv_release(ctx);
@@ -2339,8 +2388,8 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   for (hipEvent_t e : ctx->pool) (void)hipEventDestroy(e);
   if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
-  for (hipStream_t a : ctx->aux_stream)
-    if (a) (void)hipStreamDestroy(a);
+  if (ctx->aux_stream) (void)hipStreamDestroy(ctx->aux_stream);
+  flush_graveyard();
   for (hipEvent_t e : ctx->aux_ev)
     if (e) (void)hipEventDestroy(e);
   delete ctx;
@@ -2434,6 +2483,7 @@ int mgicp_align(mgicp_ctx* ctx, const float guess_cm[16], float out_T_cm[16], mg
   }
   // polled passes leave their kernels' completion unobserved: drain the stream once
   if ((rc = sync(ctx))) return rc;
+  if (!ctx->tgt_cov_pending && !ctx->src_cov_pending) flush_graveyard();  // a quiet point
   if (ctx->vl_valid) ctx->vl_groups++;
   if (ctx->tgt_lazy) ctx->tgt_lazy_aligns++;
   if (ctx->h_gtrace) {
@@ -2931,7 +2981,7 @@ int mgicp_debug_target_cov_slice(mgicp_ctx* ctx, int nranks, int rank, double* o
 int mgicp_debug_vlist_stats(mgicp_ctx* ctx, long long out[8]) {
   if (!ctx || !out) return MGICP_E_INVALID;
   for (int i = 0; i < 8; ++i) out[i] = 0;
-  if (!ctx->vlist || !ctx->vl_valid || ctx->vl_off) return MGICP_OK;
+  if (!ctx->vlist || !ctx->vl_valid || ctx->vl_off || !ctx->vl_alloc) return MGICP_OK;
   HIPCK(hipSetDevice(ctx->device));
   hipStream_t s = ctx->stream;
   unsigned int c3[3];

@@ -126,7 +126,8 @@ hipError_t launch_xform_points(const float4* in, size_t n, Xf34 T, float4* out,
 // covariance, not listed in fb, ok[p] stays 0; every other query sets ok[p] = 1 (ok nullable)
 hipError_t launch_knn_cov(const GridView& g, int k, double eps, size_t p0, size_t p1,
                           Cov3 cov, const uint32_t* perm /*nullable: query order*/, uint32_t* fb,
-                          unsigned int* fb_count, hipStream_t s, int ring_cap = -1, uint8_t* ok = nullptr);
+                          unsigned int* fb_count, hipStream_t s, int ring_cap = -1, uint8_t* ok = nullptr,
+                          int chain = 0 /*> 0: the hand-off launch follows on s, that many blocks, device count*/);
 bool knn_logged_enabled();  // env MGICP_KNN2 (default on)
 // nn_pos: per source point (shard-relative) the matched target sorted position, UINT32_MAX when
 // rejected; with `seeded` its previous contents seed the exact 1-NN search.  flags: 1 if accepted.

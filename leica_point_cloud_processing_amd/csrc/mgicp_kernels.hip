@@ -904,18 +904,23 @@ __device__ __forceinline__ void cov_from_sorted(const GridView& g, double eps, c
 
 // `perm` (optional): query order over [p0, p1) (Morton order: compact 3-D patch per wave)
 // k = K - nsent neighbours (nsent > 0 only on the generic rounded-up instantiations)
+// dcount (nullable): the number of queries is *dcount (the logged kernel's hand-off count, read on
+// the device so the hand-off can follow it in stream order); the grid strides over them
 template <int K>
 __global__ __launch_bounds__(256, MGICP_COV_WAVES) void knn_cov_kernel(GridView g, double eps, size_t p0,
                                                       size_t p1, Cov3 cov,
-                                                      const uint32_t* __restrict__ perm, int nsent) {
-  const size_t t = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (t >= p1 - p0) return;
-  const size_t p = p0 + (perm ? perm[t] : t);
-  const float4 q = g.pts[p];
-  KnnVisitor<K> vis;
-  vis.init(q.x, q.y, q.z, nsent);
-  ring_search(g, q.x, q.y, q.z, vis);
-  cov_from_sorted<K>(g, eps, vis.pos, nsent, cov, p);
+                                                      const uint32_t* __restrict__ perm, int nsent,
+                                                      const unsigned int* __restrict__ dcount) {
+  const size_t n = dcount ? static_cast<size_t>(*dcount) : p1 - p0;
+  for (size_t t = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; t < n;
+       t += static_cast<size_t>(gridDim.x) * blockDim.x) {
+    const size_t p = p0 + (perm ? perm[t] : t);
+    const float4 q = g.pts[p];
+    KnnVisitor<K> vis;
+    vis.init(q.x, q.y, q.z, nsent);
+    ring_search(g, q.x, q.y, q.z, vis);
+    cov_from_sorted<K>(g, eps, vis.pos, nsent, cov, p);
+  }
 }
 
 // PCL's covariance from the raw moments of the k neighbours (sums in the oracle's order or proven
@@ -3647,14 +3652,17 @@ static bool knn_two_phase() {  // env MGICP_KNN2 (default 1): knn_cov2_kernel, e
 template <int K>
 static hipError_t knn_cov_k(const GridView& g, double eps, size_t p0, size_t p1, Cov3 cov,
                             const uint32_t* perm, int k, uint32_t* fb, unsigned int* fb_count, hipStream_t s,
-                            int ring_cap, uint8_t* ok) {
+                            int ring_cap, uint8_t* ok, int chain) {
   if (fb) {
     const int cap = knn_log_cap(K);
     knn_cov2_kernel<K><<<nblk(p1 - p0, 64), 64, cap * 64 * sizeof(uint32_t), s>>>(g, eps, p0, p1, cov, perm,
                                                                                  K - k, cap, fb, fb_count, ring_cap,
                                                                                  ok);
+    // chain: the hand-off follows at once in stream order, its count read on the device (a grid of
+    // `chain` blocks striding over the list)
+    if (chain > 0) knn_cov_kernel<K><<<chain, 256, 0, s>>>(g, eps, 0, 0, cov, fb, K - k, fb_count);
   } else {
-    knn_cov_kernel<K><<<nblk(p1 - p0), 256, 0, s>>>(g, eps, p0, p1, cov, perm, K - k);
+    knn_cov_kernel<K><<<nblk(p1 - p0), 256, 0, s>>>(g, eps, p0, p1, cov, perm, K - k, nullptr);
   }
   return hipGetLastError();
 }
@@ -3665,22 +3673,22 @@ static hipError_t knn_cov_k(const GridView& g, double eps, size_t p0, size_t p1,
 // list: perm = fb, p0 = 0, p1 = count) the register-list kernel runs.
 hipError_t launch_knn_cov(const GridView& g, int k, double eps, size_t p0, size_t p1, Cov3 cov,
                           const uint32_t* perm, uint32_t* fb, unsigned int* fb_count, hipStream_t s, int ring_cap,
-                          uint8_t* ok) {
+                          uint8_t* ok, int chain) {
   if (p1 <= p0) return hipSuccess;
   switch (k) {
-    case 5: return knn_cov_k<5>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok);
-    case 10: return knn_cov_k<10>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok);
-    case 15: return knn_cov_k<15>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok);
-    case 20: return knn_cov_k<20>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok);
-    case 25: return knn_cov_k<25>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok);
-    case 30: return knn_cov_k<30>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok);
+    case 5: return knn_cov_k<5>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain);
+    case 10: return knn_cov_k<10>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain);
+    case 15: return knn_cov_k<15>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain);
+    case 20: return knn_cov_k<20>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain);
+    case 25: return knn_cov_k<25>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain);
+    case 30: return knn_cov_k<30>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain);
     default: break;
   }
   if (k < 1 || k > kMaxK) return hipErrorInvalidValue;
-  if (k <= 8) return knn_cov_k<8>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok);
-  if (k <= 16) return knn_cov_k<16>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok);
-  if (k <= 24) return knn_cov_k<24>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok);
-  return knn_cov_k<32>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok);
+  if (k <= 8) return knn_cov_k<8>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain);
+  if (k <= 16) return knn_cov_k<16>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain);
+  if (k <= 24) return knn_cov_k<24>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain);
+  return knn_cov_k<32>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain);
 }
 
 bool knn_logged_enabled() { return knn_two_phase(); }
