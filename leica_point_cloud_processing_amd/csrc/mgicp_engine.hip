@@ -441,7 +441,11 @@ struct mgicp_ctx {
   // r04: set_target builds the target's grid and starts its k-NN covariances on a second stream, so
   // they run while the caller uploads the source; prepare joins them (env MGICP_ASYNC_COV=0: off)
   bool async_tgt = true;
-  int aux_cu_skip = 8;              // the aux stream leaves every 8th CU to the main stream (A/B 0, 2, 4, 8: profiles/r04/ncab1)
+  // MGICP_AUX_CU_SKIP=k > 1: the aux stream on a CU mask leaving every k-th CU to the main stream (A/B
+  // 0, 2, 4, 8: profiles/r04/ncab1, up to -1.4 ms new clouds).  Off: a CU mask belongs to the hardware
+  // queue, and past GPU_MAX_HW_QUEUES streams share queues, so another context's main stream could
+  // inherit the mask -- and a resident server needs every CU (it stalled test_inlaunch_finish_*)
+  int aux_cu_skip = 0;
   // (and set_source the source's: single rank, same stream; with the lazy source mode these cover
   // every point, computed while the first sweep runs)
   bool tgt_cov_pending = false;     // the aux stream's covariance launches not joined yet
@@ -2289,7 +2293,7 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
   (void)ensure_host_red(ctx);  // (retried by the first align if it failed)
   // the stream of the covariance head start (created here: a stream's creation costs milliseconds
   // of host time, which set_* would otherwise pay before the launch)
-  // on a CU mask that leaves every ctx->aux_cu_skip-th CU free (env MGICP_AUX_CU_SKIP, 8; 0: all CUs):
+  // optionally on a CU mask that leaves every ctx->aux_cu_skip-th CU free (env MGICP_AUX_CU_SKIP, off):
   // its k-NN grids (78k blocks at 5M) otherwise take every CU and the main stream's grid build and
   // first sweep wait behind them (stream priorities did not change that, profiles/r04/prep12)
   hipError_t se = hipSuccess;
