@@ -1019,8 +1019,11 @@ struct SumCert {
 // order without sorting.  Any other lane (log overflow, ties at tau, uncertified sums) is listed in
 // fb for the register-list kernel.  64-thread blocks, cap x 4 bytes of dynamic LDS per lane.
 
+#ifndef MGICP_KNN_MINW
+#define MGICP_KNN_MINW 1  // A/B: resident waves per SIMD requested for the logged k-NN kernel (VGPR cap)
+#endif
 template <int K>
-__global__ __launch_bounds__(64) void knn_cov2_kernel(GridView g, double eps, size_t p0, size_t p1, Cov3 cov,
+__global__ __launch_bounds__(64, MGICP_KNN_MINW) void knn_cov2_kernel(GridView g, double eps, size_t p0, size_t p1, Cov3 cov,
                                                       const uint32_t* __restrict__ perm, int nsent, int cap,
                                                       uint32_t* __restrict__ fb, unsigned int* __restrict__ fb_count,
                                                       int ring_cap, uint8_t* __restrict__ ok_out) {
