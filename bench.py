@@ -64,7 +64,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=5)  # the 1-NN cell lists are built by aligns 3-4
     ap.add_argument("--config", default="C4", choices=sorted(CONFIGS),
                     help="BASELINE.json workload (default C4: the metric's 5M<->5M)")
     ap.add_argument("--n-source", type=int, default=None, help="override the config's scan size")

@@ -482,8 +482,14 @@ struct mgicp_ctx {
   // the ms-to-converge of a one-off align is unchanged), the second builds the lists of every cell it
   // queries, later aligns (GICPAlignment::iterate, the next scans of the same CAD target) read them.
   int vl_groups = 0;                  // aligns / debug sweep groups finished over the current lists
-  bool vl_eager = true;               // env MGICP_VLIST_EAGER=0: build a cell only at its query in a later sweep
-  bool vl_cold_r03 = true;            // env MGICP_VLIST_COLD=0: the first align uses the lists too (builds them)
+  bool vl_eager = false;              // env MGICP_VLIST_EAGER=1: build every queried cell at once (default: a cell
+                                      // is built when a later sweep queries it again)
+  // aligns (or debug sweep groups) after a set_target / gate change that run the r03 sweep before the
+  // lists are used (env MGICP_VLIST_COLD=N).  The lists pay off only over many aligns on one target
+  // (a later scan against the same CAD cloud, bench.py's steady state): building them costs ~57 ms
+  // eagerly or ~15 ms spread over two aligns lazily at C4, so the reference's align + iterate pair on
+  // one cloud pair (GICPAlignment.cpp:96, :116) runs both aligns without them (r04, profiles/r04/policy)
+  int vl_cold_groups = 2;
   // multi-GPU
   int nranks = 1, rank = 0;
   ncclComm_t comm = nullptr;
@@ -1194,6 +1200,8 @@ int cov_lazy(mgicp_ctx* ctx, bool tgt_rest = false) {
   if (rc) return rc;
   unsigned int need[2] = {0, 0};
   std::memcpy(need, ctx->h_small, sizeof(need));
+  if (std::getenv("MGICP_KNN_STATS"))
+    std::fprintf(stderr, "[knn-lazy] covariances to compute for this sweep: source %u, target %u\n", need[0], need[1]);
   const bool logged = ctx->knn_logged;
   if (need[0] || need[1]) {
     if (logged) HIPCK(ctx->knn_fb.reserve(static_cast<size_t>(need[0]) + need[1]));
@@ -1632,7 +1640,7 @@ int vl_prepare(mgicp_ctx* ctx) {
   }
   // the state words and the pool (~0.4 + 2 GB at C4) only once a sweep uses the lists: the first align
   // after a set_target runs the r03 sweep and must not pay for their allocation (r04)
-  if (!ctx->vl_off && !ctx->vl_alloc && (ctx->vl_groups > 0 || !ctx->vl_cold_r03)) {
+  if (!ctx->vl_off && !ctx->vl_alloc && ctx->vl_groups >= ctx->vl_cold_groups) {
     const Cloud& t = ctx->tgt;
     VListView& v = ctx->vl;
     const size_t nc = ctx->vl_ncells;
@@ -1672,7 +1680,7 @@ int vl_prepare(mgicp_ctx* ctx) {
 // wave-uniform scan when the target has its pair copy, else the per-lane search (env MGICP_VLIST=0,
 // MGICP_CORR_WAVE=0); all exact, same results.
 bool sweep_listed(const mgicp_ctx* ctx) {
-  return ctx->vlist && ctx->vl_valid && ctx->vl_alloc && !ctx->vl_off && (ctx->vl_groups > 0 || !ctx->vl_cold_r03);
+  return ctx->vlist && ctx->vl_valid && ctx->vl_alloc && !ctx->vl_off && ctx->vl_groups >= ctx->vl_cold_groups;
 }
 
 // fc (nullable, listed sweeps only): the compaction fused into the sweep
@@ -1712,10 +1720,12 @@ int correspond(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
   const bool seeded = seed && ctx->seed_valid;
   HIPCK(hipMemsetAsync(ctx->flags.p + ns, 0, sizeof(uint32_t), s));
   const uint32_t* qp = query_perm(ctx);
+  MGICP_TRACE_AT("corr: query order ready");
   if (ctx->vlist) {
     int rc = vl_prepare(ctx);
     if (rc) return rc;
   }
+  MGICP_TRACE_AT("corr: lists prepared");
   // the compaction fused into a listed sweep: both clouds' covariances must be complete (or, lazy
   // source mode, marked per point) -- not on the first align after set_*, which runs the r03 sweep
   const bool fused = ctx->fuse_compact && sweep_listed(ctx) && ctx->tgt.have_cov && !ctx->tgt_lazy &&
@@ -1737,6 +1747,7 @@ int correspond(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
     HIPCK(launch_sweep(ctx, T, thr, seeded, qp, fused ? &fc : nullptr));
   }
   ctx->seed_valid = true;
+  MGICP_TRACE_AT("corr: sweep queued");
   if (ctx->vl_stats && sweep_listed(ctx)) {
     unsigned int c3[3];
     HIPCK(hipMemcpyAsync(c3, ctx->vl_ctr.p, 3 * sizeof(unsigned int), hipMemcpyDeviceToHost, s));
@@ -1790,6 +1801,7 @@ int correspond(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
     int rc = cov_join(ctx, false);  // set_source's covariances (they ran beside this sweep)
     if (rc) return rc;
     rc = cov_lazy(ctx);  // covariances of newly accepted source points / matched target points (lazy modes)
+    MGICP_TRACE_AT("corr: lazy covariances queued (sweep drained)");
     if (rc) return rc;
   }
   {
@@ -2265,7 +2277,7 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
   }
   if (const char* vs = std::getenv("MGICP_VLIST_STATS")) ctx->vl_stats = std::atoi(vs) != 0;
   if (const char* ve = std::getenv("MGICP_VLIST_EAGER")) ctx->vl_eager = std::atoi(ve) != 0;
-  if (const char* vc = std::getenv("MGICP_VLIST_COLD")) ctx->vl_cold_r03 = std::atoi(vc) != 0;
+  if (const char* vc = std::getenv("MGICP_VLIST_COLD")) ctx->vl_cold_groups = std::max(0, std::atoi(vc));
   if (const char* lc = std::getenv("MGICP_LAZY_SRC_COV")) ctx->lazy_src_cov = std::atoi(lc) != 0;
   if (const char* lc = std::getenv("MGICP_LAZY_TGT_COV")) ctx->lazy_tgt_cov = std::atoi(lc) != 0;
   if (const char* at = std::getenv("MGICP_ASYNC_COV")) ctx->async_tgt = std::atoi(at) != 0;
@@ -2458,7 +2470,9 @@ int mgicp_align(mgicp_ctx* ctx, const float guess_cm[16], float out_T_cm[16], mg
     if (rc) return rc;
     prev = T;
     int ncorr = 0;
+    MGICP_TRACE_AT("align: sweep done");
     rc = gn_mode ? estimate_gn(ctx, T, &ncorr) : estimate_bfgs(ctx, T, &ncorr);
+    MGICP_TRACE_AT("align: solve done");
     r.n_corr = ncorr;
     if (rc == MGICP_E_SOLVER) {  // PCLException caught: converged_ stays false
       T = prev;
