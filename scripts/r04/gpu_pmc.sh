@@ -1,17 +1,7 @@
-# r04 final evidence: GPU suite, smoke, default C4 and C4F bench lines, rocprofv3 kernel-trace stats of the C4 / C4F
-# bench commands, PMC passes (each counter group in its own run, no trace domains) -> profiles/r04/final
+# r04: the profile half of gpu_final.sh alone (rocprofv3 kernel stats of the C4 / C4F bench, PMC passes)
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-O=gpurun_out/r04/${1:-final}; mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests -x -v --timeout 300 --timeout-method thread -m gpu -rP > $O/pytest_gpu.log 2>&1 || { echo "pytest failed"; grep -E "FAILED|Error" $O/pytest_gpu.log | head; exit 1; }
-tail -1 $O/pytest_gpu.log
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke failed"; tail -20 $O/smoke.log; exit 1; }
-cat $O/smoke.log
-timeout -k 10 400 python3 -u bench.py > $O/bench_C4.json 2> $O/bench_C4.err || { tail -30 $O/bench_C4.err; exit 1; }
-timeout -k 10 400 python3 -u bench.py --config C4F --gn-steps 0 > $O/bench_C4F.json 2> $O/bench_C4F.err || { tail -30 $O/bench_C4F.err; exit 1; }
-python3 -c "
-import json; d=json.load(open('$O/bench_C4.json')); r=d['roofline']
-print('bench', d['value'], d['ms_per_step'], 'frac', r['frac'], 'us/pass', r['avg_launch_ms']*1e3, 'parity', d['parity_full_size'], 'cpu', d['cpu_baseline']['value'])"
+O=gpurun_out/r04/${1:-pmc}; mkdir -p $O
 B="bench.py --steps 3 --warmup 5 --cpu-sample 0 --oracle-full 0 --fod-cpu-sample 0 --gn-steps 2"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_c4 -o run -- python3 $B > $O/b_c4_under_rocprof.json 2> $O/kt_c4.log || { tail -20 $O/kt_c4.log; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_c4f -o run -- python3 $B --config C4F > $O/b_c4f_under_rocprof.json 2> $O/kt_c4f.log || { tail -20 $O/kt_c4f.log; exit 1; }
