@@ -4,7 +4,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/r04/${1:-ab}; mkdir -p $O
 shift
-B="bench.py --steps 20 --warmup 3 --cpu-sample 0 --oracle-full 0 --fod-cpu-sample 0 --gn-steps 0 ${AB_ARGS}"
+B="bench.py --steps 20 --warmup 5 --cpu-sample 0 --oracle-full 0 --fod-cpu-sample 0 --gn-steps 0 ${AB_ARGS}"
 for rep in 1 2; do
   i=0
   for cfg in "$@"; do
