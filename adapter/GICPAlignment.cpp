@@ -129,11 +129,15 @@ bool GICPAlignment::alignOnce(PointCloudRGB::Ptr output, Eigen::Matrix4f& T)
     mgicp_result res;
     Eigen::Matrix4f out = Eigen::Matrix4f::Identity();
     int rc = mgicp_align(engine_, nullptr, out.data(), &res);  // Eigen storage is column-major
-    if (rc == MGICP_E_SOLVER)
-        return false;  // PCL swallowed the solver exception: hasConverged() == false
-    if (rc != MGICP_OK)
+    // MGICP_E_SOLVER: PCL's computeTransformation caught the solver exception, broke out of its loop
+    // and still ended with final = previous * guess and transformPointCloud(*input_, output, final):
+    // the output cloud is written (iterate() overwrites aligned_cloud_, src/GICPAlignment.cpp:116),
+    // hasConverged() == false.  The engine returns that final transform on this path.
+    const bool solver_failed = rc == MGICP_E_SOLVER;
+    if (rc != MGICP_OK && !solver_failed)
     {
-        // no cloud, too few points, device / transport failure: the align did not run, T untouched
+        // no cloud, too few points, device / transport failure: the align did not run (PCL's
+        // initCompute rejects these before computeTransformation), output and T untouched
         reportEngineError(engine_, rc, "align");
         return false;
     }
@@ -148,7 +152,7 @@ bool GICPAlignment::alignOnce(PointCloudRGB::Ptr output, Eigen::Matrix4f& T)
         }
     }
     T = out;
-    return res.converged != 0;
+    return !solver_failed && res.converged != 0;
 }
 
 // getFitnessScore for the log line; an engine failure is logged as such, never as a score

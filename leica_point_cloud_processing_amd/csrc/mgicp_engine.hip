@@ -178,37 +178,35 @@ void r_derivative(const Vec6& x, const double R[3][3], Vec6& g) {
   }
 }
 
-// Device buffers a reserve() replaces are freed at quiet points (the end of an align, a destroy), not
-// at once: hipFree waits for the whole device, which stalled set_*'s grid build behind the other
-// cloud's covariance head start on the second stream (r04, ~2 ms, profiles/r04/prep7)
+// Device buffers a reserve() replaces are freed at quiet points of their OWN context (the end of an
+// align, a destroy), not at once: hipFree waits for the whole device, which stalled set_*'s grid build
+// behind the other cloud's covariance head start on the second stream (r04, ~2 ms, profiles/r04/prep7).
+// One graveyard per context: a context's quiet point never frees -- and so never waits
+// on -- buffers of another context or device.
 struct Graveyard {
-  std::mutex mu;
   std::vector<void*> v;
+  void flush() {
+    for (void* p : v) (void)hipFree(p);
+    v.clear();
+  }
 };
-Graveyard& graveyard() {
-  static Graveyard g;
-  return g;
-}
-void defer_free(void* p) {
-  std::lock_guard<std::mutex> lk(graveyard().mu);
-  graveyard().v.push_back(p);
-}
-void flush_graveyard() {
-  std::lock_guard<std::mutex> lk(graveyard().mu);
-  for (void* p : graveyard().v) (void)hipFree(p);
-  graveyard().v.clear();
-}
+// the graveyard of the context being constructed: every DevBuf member of a mgicp_ctx picks it up
+thread_local Graveyard* t_new_ctx_grave = nullptr;
 
 template <class T>
 struct DevBuf {
   T* p = nullptr;
   size_t cap = 0;
+  Graveyard* grave = t_new_ctx_grave;
   // grows by >= 1/4 so that a sequence of slightly larger requests (grid sizing iterations,
   // the second cloud) does not pay a hipFree/hipMalloc pair each time
   hipError_t reserve(size_t n) {
     if (n <= cap && p) return hipSuccess;
     const size_t want = std::max<size_t>(std::max<size_t>(n, 1), cap ? cap + cap / 4 : 0);
-    if (p) defer_free(p);
+    if (p) {
+      if (grave) grave->v.push_back(p);
+      else (void)hipFree(p);
+    }
     p = nullptr;
     cap = 0;
     hipError_t e = hipMalloc(&p, want * sizeof(T));
@@ -274,6 +272,7 @@ std::atomic<int> g_srv_busy[64];
 }  // namespace
 
 struct mgicp_ctx {
+  std::unique_ptr<Graveyard> grave;  // replaced device buffers of THIS context, freed at its quiet points
   mgicp_params prm{};
   std::string err;
   int device = 0;
@@ -2021,6 +2020,23 @@ struct GateGuard {  // a BFGS run leaves no gated pass queued behind it
   ~GateGuard() { cancel_gated(ctx); }
 };
 
+// every error return of an align (a HIP error mid-loop, MGICP_E_COMM from a quitting rank, ...) drains
+// the stream and gives the device's server slot back, so other contexts on the device keep their
+// resident server; the error message of the failure is kept
+struct AlignDrain {
+  mgicp_ctx* ctx;
+  bool armed = true;
+  ~AlignDrain() {
+    if (!armed) return;
+    const std::string err = ctx->err;
+    cancel_gated(ctx);
+    (void)hipStreamSynchronize(ctx->stream);
+    srv_release(ctx);
+    if (!ctx->srv_ev.empty()) srv_resolve(ctx);
+    ctx->err = err;
+  }
+};
+
 int estimate_bfgs(mgicp_ctx* ctx, Mat4& T, int* n_corr) {
   GateGuard guard{ctx};
   Vec6 x;
@@ -2183,7 +2199,11 @@ int mgicp_device_count(int* n) {
 int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
   if (!out) return MGICP_E_INVALID;
   *out = nullptr;
+  std::unique_ptr<Graveyard> grave(new Graveyard());
+  t_new_ctx_grave = grave.get();
   mgicp_ctx* ctx = new mgicp_ctx();
+  t_new_ctx_grave = nullptr;
+  ctx->grave = std::move(grave);
   if (const char* occ = std::getenv("MGICP_GRID_OCC")) {
     const double v = std::atof(occ);
     if (v >= 1.0 && v <= 256.0) ctx->occupancy = v;
@@ -2405,7 +2425,7 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->aux_stream) (void)hipStreamDestroy(ctx->aux_stream);
-  flush_graveyard();
+  ctx->grave->flush();
   for (hipEvent_t e : ctx->aux_ev)
     if (e) (void)hipEventDestroy(e);
   delete ctx;
@@ -2445,6 +2465,7 @@ int mgicp_align(mgicp_ctx* ctx, const float guess_cm[16], float out_T_cm[16], mg
   std::memset(&r, 0, sizeof(r));
   const double t0 = now_ms();
   MGICP_TRACE_AT("align: begin");
+  AlignDrain drain{ctx};
   int rc = prepare(ctx, true);
   if (rc) return rc;
   if (ctx->tgt_lazy && ctx->tgt_lazy_aligns > 0 && (rc = cov_lazy(ctx, true))) return rc;  // the rest, once
@@ -2501,7 +2522,8 @@ int mgicp_align(mgicp_ctx* ctx, const float guess_cm[16], float out_T_cm[16], mg
   }
   // polled passes leave their kernels' completion unobserved: drain the stream once
   if ((rc = sync(ctx))) return rc;
-  if (!ctx->tgt_cov_pending && !ctx->src_cov_pending) flush_graveyard();  // a quiet point
+  drain.armed = false;
+  if (!ctx->tgt_cov_pending && !ctx->src_cov_pending) ctx->grave->flush();  // a quiet point
   if (ctx->vl_valid) ctx->vl_groups++;
   if (ctx->tgt_lazy) ctx->tgt_lazy_aligns++;
   if (ctx->h_gtrace) {

@@ -2113,10 +2113,13 @@ __global__ __launch_bounds__(64 * kVlWaves) void vl_build_kernel(GridView tg, VL
     cntl = __builtin_amdgcn_readfirstlane(cntl);
     const bool lng = cntl >= static_cast<unsigned int>(kVlLong);
     const unsigned int cnt4 = ((cntl + 3u) & ~3u) + (lng ? 4u : 0u);
-    unsigned int off = 0;
-    if (lane == 0) off = atomicAdd(&v.ctr[0], cnt4);
+    // pool head: no reservation once the head has passed the cap, so the head exceeds the cap by at
+    // most the reservations of the waves in flight (never wraps); the fit test cannot overflow
+    unsigned int off = 0xffffffffu;
+    if (lane == 0 && __hip_atomic_load(&v.ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < v.pool_cap)
+      off = atomicAdd(&v.ctr[0], cnt4);
     off = __builtin_amdgcn_readfirstlane(off);
-    if (off + cnt4 > v.pool_cap) {
+    if (off >= v.pool_cap || cnt4 > v.pool_cap - off) {
       if (lane == 0) v.cell[ci] = kVlOverflow;
       continue;
     }

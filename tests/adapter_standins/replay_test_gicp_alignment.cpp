@@ -197,6 +197,37 @@ int main(int argc, char** argv)
         check(g.transform_exists_ && g.getFineTransform() == T_good, "errors_empty_target_untouched");
         std::printf("errors_logged %d\n", ros::error_count());
     }
+    {  // the solver-failure path: a source 10 m off the target leaves fewer than 4
+       // correspondences inside the gate -> PCL's estimateRigidTransformationBFGS throws, the
+       // exception is caught in computeTransformation, and align() still writes
+       // output = (previous * guess) * source.  So run() logs "no converge" and leaves fine_tf_, and
+       // iterate() (src/GICPAlignment.cpp:116) overwrites aligned_cloud_ with the far source under T = I
+        PointCloudRGB::Ptr sourceRGB(new PointCloudRGB(*sourceRGB0)), targetRGB(new PointCloudRGB(*targetRGB0));
+        GICPAlignment g(targetRGB, sourceRGB, false);
+        ros::Time::init();
+        g.run();
+        const Eigen::Matrix4f T_good = g.getFineTransform();
+        check(g.transform_exists_, "solver_good_run_exists");
+        PointCloudRGB::Ptr far(new PointCloudRGB);
+        for (int i = 0; i < 30; ++i)
+        {
+            pcl::PointXYZRGB p = sourceRGB0->points[static_cast<size_t>(i) * 97];
+            p.x += 10.f;
+            far->push_back(p);
+        }
+        g.setSourceCloud(far);
+        const int e0 = ros::error_count();
+        g.run();
+        check(ros::error_count() > e0, "solver_run_logged");
+        check(g.transform_exists_ && g.getFineTransform() == T_good, "solver_run_untouched");
+        const int e1 = ros::error_count();
+        g.iterate();
+        check(ros::error_count() > e1, "solver_iterate_logged");
+        check(g.getFineTransform() == T_good, "solver_iterate_untouched");
+        PointCloudRGB::Ptr aligned(new PointCloudRGB);
+        g.getAlignedCloud(aligned);
+        check(same_xyz(*aligned, *far), "solver_iterate_output_written");
+    }
     {  // the Filter members either side of the path (adapter/Filter_mi355x.cpp)
         PointCloudRGB::Ptr src(new PointCloudRGB(*sourceRGB0));
         Filter f(0.25);

@@ -88,3 +88,8 @@ def test_adapter_replays_reference_gicp_tests(cube_clouds, tmp_path):
     # error paths: logged, transform_exists_ / fine_tf_ untouched
     for name in ("errors_empty_source", "errors_too_few_points", "errors_empty_target"):
         assert checks[name + "_logged"] and checks[name + "_untouched"], name
+    # solver failure: PCL still writes output = final * source, so iterate()
+    # overwrites aligned_cloud_ while fine_tf_ stays
+    for name in ("solver_run_logged", "solver_run_untouched", "solver_iterate_logged", "solver_iterate_untouched",
+                 "solver_iterate_output_written"):
+        assert checks[name], name
