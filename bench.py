@@ -799,7 +799,6 @@ def main():
         "gn_mode": gn,
         "fod_rows": fod,
         "data_gen_s": round(t_gen, 2),
-        "grid_occupancy": float(os.environ.get("MGICP_GRID_OCC", "0") or 0) or None,
     }
     line["pass_stats_timed"] = pass_stats_timed
     eng.close()

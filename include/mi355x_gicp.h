@@ -253,12 +253,18 @@ int mgicp_debug_target_cov_slice(mgicp_ctx* ctx, int nranks, int rank, double* o
 /* the target's 1-NN cell lists (DESIGN.md "1-NN cell lists"): out[0] cells requested and out[1]
  * queries left to the exact per-lane search by the last sweep, out[2] cells with a list, out[3] list
  * entries, out[4] reject cells, out[5] overflow cells, out[6] pool entries used, out[7] fine-grid
- * cells (0 when the lists are off: env MGICP_VLIST=0 or a gate too wide for a fine grid) */
+ * cells (0 when the lists are off: debug option "vlist" 0 or a gate too wide for a fine grid) */
 int mgicp_debug_vlist_stats(mgicp_ctx* ctx, long long out[8]);
 /* enable (1) / disable (0) per-launch HIP event timing (off by default); objective passes
- * ([2]) are sampled every 8th launch (env MGICP_PROF_STRIDE), every other family is timed on
- * every launch */
+ * ([2]) are sampled every 8th launch, every other family is timed on every launch */
 int mgicp_set_profiling(mgicp_ctx* ctx, int on);
+/* test / diagnostic forms of the engine, set explicitly on one context (never through the
+ * environment): "resident", "host_rows", "srv_cus", "fused_finish", "gated", "bar_cmd" (the
+ * objective-pass path), "async_cov", "lazy_src_cov", "knn_logged" (covariances), "vlist",
+ * "vlist_cold", "vlist_eager", "vlist_stats", "fuse_compact" (1-NN cell lists), "grid_occ" (grid
+ * sizing of the next set_*).  Every form gives the default path's results bit for bit (the GPU tests
+ * that pin each one: INTEGRATION.md "Debug options"); MGICP_E_INVALID for an unknown name. */
+int mgicp_debug_option(mgicp_ctx* ctx, const char* name, double value);
 
 #ifdef __cplusplus
 }

@@ -110,6 +110,7 @@ _SIGNATURES = {
     "mgicp_debug_trace": (ctypes.c_int, [_P, _FP, ctypes.c_int]),
     "mgicp_debug_kernel_times": (ctypes.c_int, [_P, _DP, _IP]),
     "mgicp_set_profiling": (ctypes.c_int, [_P, ctypes.c_int]),
+    "mgicp_debug_option": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_double]),
 }
 
 _lib = None

@@ -48,6 +48,10 @@ double now_ms() {
       .count();
 }
 
+#ifndef MGICP_PASS_DIAG
+#define MGICP_PASS_DIAG 0
+#endif
+
 // MGICP_TRACE=1: phase timestamps of uploads and grid builds on stderr (host-time diagnosis)
 bool trace_on() {
   static const int on = [] {
@@ -56,6 +60,9 @@ bool trace_on() {
   }();
   return on != 0;
 }
+// MGICP_KNN_STATS=1: k-NN hand-off counts per covariance pass on stderr (diagnostic)
+// (read at every covariance pass: tests switch it per context)
+bool knn_stats_on() { return std::getenv("MGICP_KNN_STATS") != nullptr; }
 #define MGICP_TRACE_AT(label)                                                  \
   do {                                                                         \
     if (trace_on()) std::fprintf(stderr, "[mgicp] %10.3f ms  %s\n", now_ms(), label); \
@@ -232,7 +239,7 @@ struct Cloud {
   DevBuf<uint32_t> cell_start;
   DevBuf<uint8_t> empty_dist; // empty-space map (target only: 1-NN queries leave the surface)
   bool want_empty_map = false;
-  DevBuf<uint32_t> seed, seed_scratch;  // seed map (target: first-sweep 1-NN seeds; env MGICP_SEED_MAP)
+  DevBuf<uint32_t> seed, seed_scratch;  // seed map (target: first-sweep 1-NN seeds)
   bool want_seed_map = false;
   DevBuf<float4> boxes;       // per-cell point boxes (target only: the 1-NN sweeps prune by them)
   bool want_boxes = false;
@@ -285,21 +292,21 @@ struct mgicp_ctx {
   DevBuf<float4> f_vox, f_vox2;
   DevBuf<unsigned char> f_keep;
   DevBuf<unsigned int> f_count;
-  double occupancy = kDefaultOccupancy;  // grid cell sizing target (env MGICP_GRID_OCC)
+  double occupancy = kDefaultOccupancy;  // grid cell sizing target (debug option "grid_occ")
   // objective-pass launch shape over the fixed reduction tree, A/B-measured on MI355X at 5M points
   // (profiles/r02/ab_tree): 512 persistent 4-wave blocks -- 2 waves per SIMD, so chunk reductions
   // and tickets overlap other waves' streaming (71 us vs 76 us at 256 blocks), and the gated
   // grid (134 VGPRs: 3 waves per SIMD) stays resident while it waits at the gate (14.5 ms per C4
   // align vs 14.9 ms at 1024 blocks); in-launch finish
-  bool fused_finish = true;              // in-launch reduction finish (env MGICP_FUSED_FINISH)
-  int fdf_max_blocks = 512;              // objective-pass grid cap (env MGICP_FDF_BLOCKS)
+  bool fused_finish = true;              // in-launch reduction finish (debug option "fused_finish")
+  int fdf_max_blocks = 512;              // objective-pass grid cap (fixed)
   // alternate the objective-pass direction: 360 MB of streams at 5M points exceed the 256 MiB
   // Infinity Cache, so each pass re-reads the previous pass's tail from it (73 -> 68 us)
-  bool alt_sweep = true;                 // (env MGICP_FDF_ALT)
-  int fdf_diag = 0;  // timing diagnostics of the objective pass (env MGICP_FDF_DIAG: 2 no reduction, 4 no tickets)
+  bool alt_sweep = true;                 // (fixed)
+  int fdf_diag = 0;  // timing diagnostics of the objective pass (kernel modes 2 no reduction, 4 no tickets; not set by the host)
   double ms_upload_pending = 0;
   // host uploads go through the process-wide HostUploader (host_upload.hpp)
-  int host_threads = 8;                  // packing workers (env MGICP_HOST_THREADS)
+  int host_threads = 8;                  // packing workers (fixed)
   DevBuf<float> xyz_dev;                 // packed xyz landing zone
   // per source point (sorted), rank shard only
   DevBuf<float4> src_out;  // guess-applied source (only when guess != I)
@@ -314,7 +321,7 @@ struct mgicp_ctx {
 
   size_t corr_cap = 0;     // elements per stream (multiple of 4)
   bool seed_valid = false;
-  // query order of the 1-NN sweeps (Morton order of the shard; env MGICP_QUERY_ORDER)
+  // query order of the 1-NN sweeps (Morton order of the shard)
   bool query_order = true;
   bool qperm_valid = false;
   DevBuf<uint32_t> qperm;
@@ -324,7 +331,7 @@ struct mgicp_ctx {
   DevBuf<double> partial;       // chunk partials, kRedVals each
   DevBuf<unsigned long long> tpart;  // the server's stamped chunk partials, 32 words each (r03; 0xff.. = no stamp)
   size_t tpart_n = 0;
-  bool srv_tagged = true;            // env MGICP_SRV_TAGGED: the server's tagged tail (0: chunk tickets)
+  bool srv_tagged = true;            // the server's tagged tail (the chunk-ticket tail of r02 is the launched kernel's)
   DevBuf<double> spart;         // super partials (max_supers() rows: the all-gather send size)
   DevBuf<double> gath;          // nranks x max_supers() rows
   DevBuf<double> red;           // kRedVals
@@ -341,18 +348,18 @@ struct mgicp_ctx {
   unsigned long long* h_flag = nullptr;  // pass-completion word (host / device views)
   unsigned long long* d_flag = nullptr;
   unsigned long long pass_seq = 0;
-  bool poll = true;          // poll the completion word instead of hipStreamSynchronize (env MGICP_POLL)
+  bool poll = true;          // poll the completion word instead of hipStreamSynchronize (fixed)
   // pre-launched (gated) objective passes: pass k + 1 is queued while pass k runs and waits on the
-  // host-written command block (env MGICP_GATED; single-GPU polled mode)
+  // host-written command block (debug option "gated"; single-GPU polled mode)
   bool gated = true;
   PassCmd* h_cmd = nullptr;             // pinned, mapped, coherent host memory
   PassCmd* d_cmd = nullptr;             // its device address
   PassCmd* mail = nullptr;              // device copy block 0 of a gated pass forwards to the others
   // the server's command block in fine-grained device memory that the host stores into through the
-  // BAR (env MGICP_BAR_CMD): every server block polls it, no PCIe read and no mailbox hop
+  // BAR (debug option "bar_cmd"): every server block polls it, no PCIe read and no mailbox hop
   bool bar = true;
   PassCmd* bar_cmd = nullptr;
-  // blocks polling the host copy (env MGICP_GATE_POLLERS): 1 measured best (14.15 ms / C4 align;
+  // blocks polling the host copy (fixed): 1 measured best (14.15 ms / C4 align;
   // 8 pollers 14.8 ms, all 256 blocks on host memory ~70 ms: PCIe read contention;
   // profiles/r02/ab_gate)
   int gate_pollers = 1;
@@ -363,7 +370,7 @@ struct mgicp_ctx {
   std::vector<double> host_gt;             // 2 x 1024
   unsigned long long gated_seq = 0;     // sequence number of the queued gated pass (0 = none)
   unsigned long long gate_timeout = 0;  // wall_clock64 ticks a gated pass waits before giving up
-  // the resident pass server (env MGICP_RESIDENT; single GPU polled mode, or any rank count with the
+  // the resident pass server (debug option "resident"; single GPU polled mode, or any rank count with the
   // shared row segment): one launch per BFGS run keeps part of the compacted streams in registers /
   // LDS across all its passes
   bool resident = true;
@@ -372,12 +379,12 @@ struct mgicp_ctx {
   bool srv_degraded = false;            // a server pass was taken over: launched passes until the align ends
   unsigned long long srv_next = 0;
   int cus = 0;                          // compute units (the server's grid)
-  int srv_cus = 0;                      // env MGICP_SRV_CUS: cap on the server's blocks (0 = every CU)
-  int srv_waves = 4;                    // server shape: 4 or 8 waves per CU (env MGICP_SRV_WAVES)
+  int srv_cus = 0;                      // debug option "srv_cus": cap on the server's blocks (0 = every CU)
+  int srv_waves = 4;                    // server shape: 4 waves per CU (one per SIMD)
   int stall_pass = -1;                  // env MGICP_SRV_STALL_PASS (tests): a server block withholds this pass
   int quit_pass = -1;                   // env MGICP_DEBUG_QUIT_PASS (tests): the host gives up at this pass index
                                         // with MGICP_E_COMM (a rank that dies mid-align, seen from the others)
-  bool corr_wave = true;                // wave-uniform 1-NN sweeps (env MGICP_CORR_WAVE)
+  bool corr_wave = true;                // wave-uniform 1-NN sweeps (fixed)
   int corr_lds_pts = -1;                // small-ball waves: union-box cell bounds in LDS (-1), + points when <= N fit (N > 0), off (0) (MGICP_CORR_LDS_PTS)
   int corr_split = 0;                   // waves of the wave sweep with <= this many stragglers hand them to a kernel of
                                         // their own (MGICP_CORR_SPLIT; 0 = every straggler finishes in place)
@@ -410,7 +417,7 @@ struct mgicp_ctx {
   std::vector<SrvEv> srv_ev;            // launches not yet resolved (the last one may be live)
   double srv_time_ms = 0;
   long long srv_time_passes = 0, srv_time_launches = 0;
-  bool spin_pause = false;              // env MGICP_SPIN_PAUSE: pause instruction in the row spin
+  bool spin_pause = false;              // pause instruction in the row spin (off: measured no gain)
   // MGICP_PASS_TIMES: host view of the server passes -- command published -> rows complete
   // (device pass + PCIe both ways) and rows complete -> next command (host BFGS step)
   double ht_dev = 0, ht_host = 0, ht_bfgs = 0, ht_eval = 0, ht_last_rows = 0;
@@ -419,8 +426,8 @@ struct mgicp_ctx {
   DevBuf<uint32_t> counts, keys, keys_sorted, vals;
   DevBuf<unsigned char> scratch;
   DevBuf<unsigned long long> u64;
-  bool split_target_cov = true;     // multi-GPU: target covariances split + all-gathered (env MGICP_SPLIT_TARGET_COV)
-  // lazy source covariances (r04, env MGICP_LAZY_SRC_COV): a source point's covariance is computed the
+  bool split_target_cov = true;     // multi-GPU: target covariances split + all-gathered (fixed)
+  // lazy source covariances (r04, debug option "lazy_src_cov"): a source point's covariance is computed the
   // first time a sweep accepts it -- every consumer (Mahalanobis of the compaction, GN moments) reads
   // accepted points only, so points the gate never accepts (clutter, debris far off the part) never
   // pay PCL's exact 20-NN search; the values are the eager ones bit for bit
@@ -429,16 +436,8 @@ struct mgicp_ctx {
   size_t src_lazy_p0 = 0, src_lazy_p1 = 0;
   DevBuf<uint8_t> cov_ok;           // per shard point: covariance computed
   DevBuf<uint32_t> cov_need;        // this sweep's accepted points without a covariance (absolute positions)
-  // lazy target covariances (r04, single rank; env MGICP_LAZY_TGT_COV=1, default off): the first align after
-  // a set_target computes the covariances of the target points its sweeps match; the next align
-  // computes the rest, so later sweeps run without any check
-  bool lazy_tgt_cov = false;         // measured at C4: no gain (the matched set grows every sweep), DESIGN.md
-  bool tgt_lazy = false;            // the target's covariances are being computed per sweep
-  int tgt_lazy_aligns = 0;          // aligns run since the lazy target was set up
-  DevBuf<uint8_t> tcov_ok;          // per target sorted position: 0 none, 2 matched this sweep, 1 computed
-  DevBuf<uint32_t> tcov_need;       // this sweep's target points to compute (sorted positions)
   // r04: set_target builds the target's grid and starts its k-NN covariances on a second stream, so
-  // they run while the caller uploads the source; prepare joins them (env MGICP_ASYNC_COV=0: off)
+  // they run while the caller uploads the source; prepare joins them (debug option "async_cov" 0: off)
   bool async_tgt = true;
   // MGICP_AUX_CU_SKIP=k > 1: the aux stream on a CU mask leaving every k-th CU to the main stream (A/B
   // 0, 2, 4, 8: profiles/r04/ncab1, up to -1.4 ms new clouds).  Off: a CU mask belongs to the hardware
@@ -450,23 +449,23 @@ struct mgicp_ctx {
   bool tgt_cov_pending = false;     // the aux stream's covariance launches not joined yet
   bool src_cov_pending = false;
   bool src_async_lazy = false;      // the source's launch was ring-capped (lazy mode): the rest stays lazy
-  int async_ring_cap = 4;           // env MGICP_ASYNC_RING_CAP: rings the source's head start searches
+  int async_ring_cap = 4;           // rings the source's head start searches (lazy mode)
   // one stream for both clouds' launches: with a stream each the process exceeds its hardware queues
   // (GPU_MAX_HW_QUEUES, 4) and the main stream ends up sharing one with them (profiles/r04/prep7)
   hipStream_t aux_stream = nullptr;
   hipEvent_t aux_ev[2] = {nullptr, nullptr};  // completion of the target's [0] / source's [1] launch
   DevBuf<unsigned int> aux_cnt;     // their hand-off counts: [0] target, [1] source
   DevBuf<uint32_t> knn_fb2;         // the source's hand-off list
-  bool knn_logged = true;           // env MGICP_KNN2 at create: logged k-NN kernel, else register-list
+  bool knn_logged = true;           // wave-staged k-NN kernel + hand-off (debug option "knn_logged" 0: register-list only)
   DevBuf<uint32_t> knn_fb;          // points the logged k-NN kernel leaves to the register-list one
   unsigned int knn_fallbacks = 0;   // their count in the last covariance launch
   DevBuf<float> fpartial;
-  // the target's 1-NN cell lists (r04, DESIGN.md "1-NN cell lists"; env MGICP_VLIST=0: the r03 sweeps)
+  // the target's 1-NN cell lists (r04, DESIGN.md "1-NN cell lists"; debug option "vlist" 0: the r03 sweeps)
   bool vlist = true;
-  bool fuse_compact = true;           // r04: compaction fused into listed sweeps (env MGICP_FUSE_COMPACT)
+  bool fuse_compact = true;           // r04: compaction fused into listed sweeps (debug option "fuse_compact")
   DevBuf<uint32_t> vl_defer;          // chunks a fused sweep deferred to the compaction launch
-  float vlist_cell = 0.6f;            // fine cell edge / the target grid's cell edge (env MGICP_VLIST_CELL)
-  bool vl_stats = false;              // env MGICP_VLIST_STATS: per-sweep list diagnostics on stderr
+  float vlist_cell = 0.6f;            // fine cell edge / the target grid's cell edge (fixed)
+  bool vl_stats = false;              // debug option "vlist_stats": per-sweep list diagnostics on stderr
   bool vl_valid = false;              // lists belong to the current target grid and gate
   bool vl_alloc = false;              // their state words and pool are allocated and initialised
   bool vl_off = false;                // the gate is too large for a fine grid of this target: r03 sweeps
@@ -481,10 +480,10 @@ struct mgicp_ctx {
   // the ms-to-converge of a one-off align is unchanged), the second builds the lists of every cell it
   // queries, later aligns (GICPAlignment::iterate, the next scans of the same CAD target) read them.
   int vl_groups = 0;                  // aligns / debug sweep groups finished over the current lists
-  bool vl_eager = false;              // env MGICP_VLIST_EAGER=1: build every queried cell at once (default: a cell
+  bool vl_eager = false;              // debug option "vlist_eager" 1: build every queried cell at once (default: a cell
                                       // is built when a later sweep queries it again)
   // aligns (or debug sweep groups) after a set_target / gate change that run the r03 sweep before the
-  // lists are used (env MGICP_VLIST_COLD=N).  The lists pay off only over many aligns on one target
+  // lists are used (debug option "vlist_cold" N).  The lists pay off only over many aligns on one target
   // (a later scan against the same CAD cloud, bench.py's steady state): building them costs ~57 ms
   // eagerly or ~15 ms spread over two aligns lazily at C4, so the reference's align + iterate pair on
   // one cloud pair (GICPAlignment.cpp:96, :116) runs both aligns without them (r04, profiles/r04/policy)
@@ -499,7 +498,7 @@ struct mgicp_ctx {
   int n_evals = 0;
   // profiling
   bool profiling = false;
-  unsigned prof_stride = 8;   // objective-pass event sampling (env MGICP_PROF_STRIDE)
+  unsigned prof_stride = 8;   // objective-pass event sampling (fixed)
   unsigned long long prof_tick = 0;
   struct EvPair { hipEvent_t a, b; int fam; };
   std::vector<EvPair> pending;
@@ -690,7 +689,7 @@ int cov_join(mgicp_ctx* ctx, bool tgt) {
   // this cloud's launches only (the logged k-NN pass and its hand-off, chained on the aux stream):
   // the main stream waits for them on the device, the host does not
   HIPCK(hipStreamWaitEvent(ctx->stream, ctx->aux_ev[tgt ? 0 : 1], 0));
-  if (ctx->knn_logged && std::getenv("MGICP_KNN_STATS")) {  // as compute_cov reports it
+  if (ctx->knn_logged && knn_stats_on()) {  // as compute_cov reports it
     unsigned int nfb = 0;
     HIPCK(hipMemcpyAsync(ctx->h_small, ctx->aux_cnt.p + (tgt ? 0 : 1), sizeof(nfb), hipMemcpyDeviceToHost, ctx->stream));
     HIPCK(hipStreamSynchronize(ctx->stream));
@@ -716,7 +715,7 @@ int cov_join_all(mgicp_ctx* ctx) {
 int cov_prep_async(mgicp_ctx* ctx, bool tgt) {
   Cloud& c = tgt ? ctx->tgt : ctx->src;
   if (!ctx->async_tgt || !ctx->aux_stream || ctx->nranks != 1 || ctx->comm || ctx->have_shm || ctx->profiling ||
-      (tgt && ctx->lazy_tgt_cov) || static_cast<size_t>(ctx->prm.k) > c.n)
+      static_cast<size_t>(ctx->prm.k) > c.n)
     return MGICP_OK;
   if (build_grid(ctx, c) != MGICP_OK || c.n < static_cast<size_t>(ctx->prm.k)) return MGICP_OK;
   HIPCK(c.cov.reserve(3 * c.n));
@@ -1009,7 +1008,6 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
   cl.have_cov = false;
   if (&cl == &ctx->tgt) ctx->vl_valid = false;  // the 1-NN cell lists index the old target
   if (&cl == &ctx->src) ctx->src_lazy_ready = false;  // lazy covariances: none computed for this cloud
-  if (&cl == &ctx->tgt) ctx->tgt_lazy = false;
   if (&cl == &ctx->src || &cl == &ctx->tgt) {  // sorted positions changed
     ctx->have_corr = false;
     ctx->seed_valid = false;
@@ -1075,7 +1073,7 @@ int compute_cov(mgicp_ctx* ctx, Cloud& cl, size_t p0, size_t p1, size_t stride =
     unsigned int nfb = 0;
     std::memcpy(&nfb, ctx->h_small, sizeof(nfb));
     ctx->knn_fallbacks = nfb;
-    const bool stats = std::getenv("MGICP_KNN_STATS") != nullptr;
+    const bool stats = knn_stats_on();
     if (stats) std::fprintf(stderr, "[knn] %zu points, %u left to the register-list kernel\n", p1 - p0, nfb);
     if (nfb) {
       ProfScope ps(ctx, kFamCov);
@@ -1089,6 +1087,11 @@ int compute_cov(mgicp_ctx* ctx, Cloud& cl, size_t p0, size_t p1, size_t stride =
   {
     unsigned long long ph[24];
     HIPCK(corr_phase_take(ph));
+    if (ph[0])
+      std::fprintf(stderr, "[knnb] waves %llu staged %llu (non-monotone %llu, over the cap %llu) | per wave: union points %.1f, "
+                   "pieces %.1f, block candidates mean lane %.1f busiest lane %.1f | lanes past the block %llu, hand-offs %llu "
+                   "of %llu\n", ph[0], ph[1], ph[4], ph[5], double(ph[2]) / ph[0], double(ph[3]) / ph[0],
+                   double(ph[6]) / ph[0] / 64.0, double(ph[7]) / ph[0], ph[8], ph[9], ph[10]);
     const double w = ph[21] ? static_cast<double>(ph[21]) : 1.0;
     std::fprintf(stderr, "[knn-div] waves %llu | per wave: test iterations %.1f, max lane tests %.1f, mean lane tests %.1f"
                  " | cycles/wave search %.0f, moments + finish %.0f\n",
@@ -1105,8 +1108,7 @@ int compute_cov(mgicp_ctx* ctx, Cloud& cl, size_t p0, size_t p1, size_t stride =
 // target covariances (computeCovariances on the target, once per target cloud).  Multi-GPU
 // (SURVEY.md 8e): rank r computes the r-th of N equal slices and one in-place all-gather per
 // covariance array (48 bytes per point in total) completes every rank's copy -- the values are
-// per point, so the result is the single-GPU one bit for bit (env MGICP_SPLIT_TARGET_COV=0: every
-// rank computes all of them).
+// per point, so the result is the single-GPU one bit for bit.
 int target_cov(mgicp_ctx* ctx) {
   Cloud& t = ctx->tgt;
   if (!ctx->comm || ctx->nranks < 2 || !ctx->split_target_cov) return compute_cov(ctx, t, 0, t.n);
@@ -1138,23 +1140,7 @@ int prepare(mgicp_ctx* ctx, bool need_cov) {
   if (ctx->src.dirty && (rc = build_grid(ctx, ctx->src))) return rc;
   if ((rc = cov_join(ctx, true))) return rc;  // set_target's covariances (after the source grid: overlapped)
   if (!need_cov) return MGICP_OK;
-  if (!ctx->tgt.have_cov && !ctx->tgt_lazy) {
-    if (ctx->lazy_tgt_cov && ctx->nranks == 1 && !ctx->comm && !ctx->have_shm) {
-      // computed per sweep for the target points the first align's sweeps match (cov_lazy)
-      Cloud& t = ctx->tgt;
-      HIPCK(t.cov.reserve(3 * t.n));
-      t.cov_stride = t.n;
-      t.cov_p0 = 0;
-      t.cov_p1 = t.n;
-      HIPCK(ctx->tcov_ok.reserve(t.n));
-      HIPCK(ctx->tcov_need.reserve(t.n));
-      HIPCK(hipMemsetAsync(ctx->tcov_ok.p, 0, t.n, ctx->stream));
-      ctx->tgt_lazy = true;
-      ctx->tgt_lazy_aligns = 0;
-    } else if ((rc = target_cov(ctx))) {
-      return rc;
-    }
-  }
+  if (!ctx->tgt.have_cov && (rc = target_cov(ctx))) return rc;
   // set_source's covariances still running count as current: the sweep joins them (overlapped)
   const bool src_cur = ctx->src_cov_pending ||
                        (ctx->src.have_cov && ctx->src.cov_p0 == ctx->shard_p0() && ctx->src.cov_p1 == ctx->shard_p1());
@@ -1179,60 +1165,39 @@ int prepare(mgicp_ctx* ctx, bool need_cov) {
   return MGICP_OK;
 }
 
-// the covariances a sweep needs (lazy modes): its accepted source points without one, and the
-// target points they matched without one (tgt_rest: every target point still without one), computed
-// by the same kernels as the eager passes (logged k-NN, the register-list hand-off for the rest)
-int cov_lazy(mgicp_ctx* ctx, bool tgt_rest = false) {
-  const bool do_src = ctx->lazy_src_cov && !ctx->src.have_cov && !tgt_rest;
-  const bool do_tgt = ctx->tgt_lazy;
-  if (!do_src && !do_tgt) return MGICP_OK;
+// the covariances a sweep needs (lazy source mode): its accepted source points without one, computed
+// by the same kernels as the eager pass (the k-NN kernel, the register-list hand-off for the rest)
+int cov_lazy(mgicp_ctx* ctx) {
+  if (!ctx->lazy_src_cov || ctx->src.have_cov) return MGICP_OK;
   const size_t p0 = ctx->shard_p0(), ns = ctx->shard_p1() - p0;
-  HIPCK(ctx->u64.reserve(2));
-  unsigned int* cnt = reinterpret_cast<unsigned int*>(ctx->u64.p);  // [0] source, [1] target, [2..3] hand-offs
-  HIPCK(hipMemsetAsync(cnt, 0, 4 * sizeof(unsigned int), ctx->stream));
-  if (do_src) HIPCK(launch_cov_need(ctx->flags.p, ctx->cov_ok.p, p0, ns, ctx->cov_need.p, cnt, ctx->stream));
-  if (do_tgt)
-    HIPCK(launch_tgt_cov_need(ctx->flags.p, ctx->prev_pos.p, tgt_rest ? 0 : ns, ctx->tcov_ok.p, ctx->tgt.n,
-                              tgt_rest ? 1 : 0, ctx->tcov_need.p, cnt + 1, ctx->stream));
-  HIPCK(hipMemcpyAsync(ctx->h_small, cnt, 2 * sizeof(unsigned int), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCK(ctx->u64.reserve(1));
+  unsigned int* cnt = reinterpret_cast<unsigned int*>(ctx->u64.p);  // [0] points to compute, [1] hand-offs
+  HIPCK(hipMemsetAsync(cnt, 0, 2 * sizeof(unsigned int), ctx->stream));
+  HIPCK(launch_cov_need(ctx->flags.p, ctx->cov_ok.p, p0, ns, ctx->cov_need.p, cnt, ctx->stream));
+  HIPCK(hipMemcpyAsync(ctx->h_small, cnt, sizeof(unsigned int), hipMemcpyDeviceToHost, ctx->stream));
   int rc = sync(ctx);
   if (rc) return rc;
-  unsigned int need[2] = {0, 0};
-  std::memcpy(need, ctx->h_small, sizeof(need));
-  if (std::getenv("MGICP_KNN_STATS"))
-    std::fprintf(stderr, "[knn-lazy] covariances to compute for this sweep: source %u, target %u\n", need[0], need[1]);
+  unsigned int need = 0;
+  std::memcpy(&need, ctx->h_small, sizeof(need));
+  if (knn_stats_on()) std::fprintf(stderr, "[knn-lazy] source covariances to compute for this sweep: %u\n", need);
+  if (!need) return MGICP_OK;
   const bool logged = ctx->knn_logged;
-  if (need[0] || need[1]) {
-    if (logged) HIPCK(ctx->knn_fb.reserve(static_cast<size_t>(need[0]) + need[1]));
-    {
-      ProfScope ps(ctx, kFamCov);
-      if (need[0])
-        HIPCK(launch_knn_cov(ctx->src.view, ctx->prm.k, ctx->prm.gicp_eps, 0, need[0], ctx->src.cov3(),
-                             ctx->cov_need.p, logged ? ctx->knn_fb.p : nullptr, logged ? cnt + 2 : nullptr,
-                             ctx->stream));
-      if (need[1])
-        HIPCK(launch_knn_cov(ctx->tgt.view, ctx->prm.k, ctx->prm.gicp_eps, 0, need[1], ctx->tgt.cov3(),
-                             ctx->tcov_need.p, logged ? ctx->knn_fb.p + need[0] : nullptr,
-                             logged ? cnt + 3 : nullptr, ctx->stream));
-    }
-    if (logged) {
-      HIPCK(hipMemcpyAsync(ctx->h_small, cnt + 2, 2 * sizeof(unsigned int), hipMemcpyDeviceToHost, ctx->stream));
-      if ((rc = sync(ctx))) return rc;
-      unsigned int nfb[2] = {0, 0};
-      std::memcpy(nfb, ctx->h_small, sizeof(nfb));
-      ctx->knn_fallbacks = nfb[0] + nfb[1];
-      ProfScope ps(ctx, kFamCov);
-      if (nfb[0])
-        HIPCK(launch_knn_cov(ctx->src.view, ctx->prm.k, ctx->prm.gicp_eps, 0, nfb[0], ctx->src.cov3(), ctx->knn_fb.p,
-                             nullptr, nullptr, ctx->stream));
-      if (nfb[1])
-        HIPCK(launch_knn_cov(ctx->tgt.view, ctx->prm.k, ctx->prm.gicp_eps, 0, nfb[1], ctx->tgt.cov3(),
-                             ctx->knn_fb.p + need[0], nullptr, nullptr, ctx->stream));
-    }
+  if (logged) HIPCK(ctx->knn_fb.reserve(need));
+  {
+    ProfScope ps(ctx, kFamCov);
+    HIPCK(launch_knn_cov(ctx->src.view, ctx->prm.k, ctx->prm.gicp_eps, 0, need, ctx->src.cov3(), ctx->cov_need.p,
+                         logged ? ctx->knn_fb.p : nullptr, logged ? cnt + 1 : nullptr, ctx->stream));
   }
-  if (tgt_rest) {  // every target covariance is computed: later sweeps skip the checks
-    ctx->tgt_lazy = false;
-    ctx->tgt.have_cov = true;
+  if (logged) {
+    HIPCK(hipMemcpyAsync(ctx->h_small, cnt + 1, sizeof(unsigned int), hipMemcpyDeviceToHost, ctx->stream));
+    if ((rc = sync(ctx))) return rc;
+    unsigned int nfb = 0;
+    std::memcpy(&nfb, ctx->h_small, sizeof(nfb));
+    ctx->knn_fallbacks = nfb;
+    ProfScope ps(ctx, kFamCov);
+    if (nfb)
+      HIPCK(launch_knn_cov(ctx->src.view, ctx->prm.k, ctx->prm.gicp_eps, 0, nfb, ctx->src.cov3(), ctx->knn_fb.p, nullptr,
+                           nullptr, ctx->stream));
   }
   return MGICP_OK;
 }
@@ -1247,14 +1212,7 @@ int ensure_host_red(mgicp_ctx* ctx) {
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->device) != hipSuccess || khz <= 0)
       khz = 100000;  // 100 MHz: the gfx9 constant wall clock
     ctx->gate_timeout = static_cast<unsigned long long>(khz) * 1000ull * 10ull;  // 10 s
-    {
-      const char* mu = std::getenv("MGICP_MAIL_UNCACHED");
-      if (mu && std::atoi(mu))
-        HIPCK(hipExtMallocWithFlags(reinterpret_cast<void**>(&ctx->mail), sizeof(PassCmd), hipDeviceMallocUncached));
-      else
-        HIPCK(hipMalloc(reinterpret_cast<void**>(&ctx->mail), sizeof(PassCmd)));
-      if (const char* gp = std::getenv("MGICP_GATE_POLLERS")) ctx->gate_pollers = std::max(1, std::atoi(gp));
-    }
+    HIPCK(hipMalloc(reinterpret_cast<void**>(&ctx->mail), sizeof(PassCmd)));
     HIPCK(hipMemsetAsync(ctx->mail, 0, sizeof(PassCmd), ctx->stream));
     // host stores into device memory need the whole VRAM behind the PCIe BAR (large BAR); without
     // it block 0 polls the pinned copy
@@ -1267,19 +1225,23 @@ int ensure_host_red(mgicp_ctx* ctx) {
       else
         HIPCK(hipMemset(ctx->bar_cmd, 0, sizeof(PassCmd)));  // complete before the host's first store
     }
-    if (const char* pt = std::getenv("MGICP_PASS_TIMES"); pt && std::atoi(pt)) {
+#if MGICP_PASS_DIAG
+    // diagnostic builds (make variant DEFS=-DMGICP_PASS_DIAG=1): per-pass device / host timestamps of
+    // the resident server and of the gated passes, summarised on stderr at the end of every align
+    {
       HIPCK(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_ptimes), 2 * 1024 * sizeof(unsigned long long),
                           hipHostMallocMapped | hipHostMallocCoherent));
       HIPCK(hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->d_ptimes), ctx->h_ptimes, 0));
       std::memset(ctx->h_ptimes, 0, 2 * 1024 * sizeof(unsigned long long));
     }
-    if (const char* gt = std::getenv("MGICP_GATE_TRACE"); gt && std::atoi(gt)) {
+    {
       HIPCK(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_gtrace), 4 * 1024 * sizeof(unsigned long long),
                           hipHostMallocMapped | hipHostMallocCoherent));
       HIPCK(hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->d_gtrace), ctx->h_gtrace, 0));
       std::memset(ctx->h_gtrace, 0, 4 * 1024 * sizeof(unsigned long long));
       ctx->host_gt.assign(2 * 1024, 0.0);
     }
+#endif
   }
   if (ctx->h_red) return MGICP_OK;
   // kRedVals sums followed by the pass-completion word (see launch_fdf_soa's done_flag)
@@ -1676,8 +1638,8 @@ int vl_prepare(mgicp_ctx* ctx) {
 }
 
 // The 1-NN sweep kernel of one correspondence phase: the target's cell lists (r04, default), else the
-// wave-uniform scan when the target has its pair copy, else the per-lane search (env MGICP_VLIST=0,
-// MGICP_CORR_WAVE=0); all exact, same results.
+// wave-uniform scan (debug option "vlist" 0, and the first aligns after a set_target); exact, same
+// results.
 bool sweep_listed(const mgicp_ctx* ctx) {
   return ctx->vlist && ctx->vl_valid && ctx->vl_alloc && !ctx->vl_off && ctx->vl_groups >= ctx->vl_cold_groups;
 }
@@ -1727,7 +1689,7 @@ int correspond(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
   MGICP_TRACE_AT("corr: lists prepared");
   // the compaction fused into a listed sweep: both clouds' covariances must be complete (or, lazy
   // source mode, marked per point) -- not on the first align after set_*, which runs the r03 sweep
-  const bool fused = ctx->fuse_compact && sweep_listed(ctx) && ctx->tgt.have_cov && !ctx->tgt_lazy &&
+  const bool fused = ctx->fuse_compact && sweep_listed(ctx) && ctx->tgt.have_cov &&
                      !ctx->tgt_cov_pending && !ctx->src_cov_pending &&
                      (ctx->src.have_cov || (ctx->lazy_src_cov && ctx->src_lazy_ready));
   FusedCompact fc{};
@@ -1799,7 +1761,7 @@ int correspond(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
   {
     int rc = cov_join(ctx, false);  // set_source's covariances (they ran beside this sweep)
     if (rc) return rc;
-    rc = cov_lazy(ctx);  // covariances of newly accepted source points / matched target points (lazy modes)
+    rc = cov_lazy(ctx);  // covariances of newly accepted source points (lazy source mode)
     MGICP_TRACE_AT("corr: lazy covariances queued (sweep drained)");
     if (rc) return rc;
   }
@@ -2204,21 +2166,9 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
   mgicp_ctx* ctx = new mgicp_ctx();
   t_new_ctx_grave = nullptr;
   ctx->grave = std::move(grave);
-  if (const char* occ = std::getenv("MGICP_GRID_OCC")) {
-    const double v = std::atof(occ);
-    if (v >= 1.0 && v <= 256.0) ctx->occupancy = v;
-  }
-  if (const char* ff = std::getenv("MGICP_FUSED_FINISH")) ctx->fused_finish = std::atoi(ff) != 0;
-  if (const char* fa = std::getenv("MGICP_FDF_ALT")) ctx->alt_sweep = std::atoi(fa) != 0;
-  if (const char* fd = std::getenv("MGICP_FDF_DIAG")) ctx->fdf_diag = std::atoi(fd) & 6;
-  if (const char* po = std::getenv("MGICP_POLL")) ctx->poll = std::atoi(po) != 0;
-  if (const char* ga = std::getenv("MGICP_GATED")) ctx->gated = std::atoi(ga) != 0;
-  if (const char* rs = std::getenv("MGICP_RESIDENT")) ctx->resident = std::atoi(rs) != 0;
-  if (const char* hr = std::getenv("MGICP_HOST_ROWS")) ctx->host_rows = std::atoi(hr) != 0;
-  if (const char* sw = std::getenv("MGICP_SRV_WAVES")) ctx->srv_waves = std::atoi(sw) == 8 ? 8 : 4;
-  if (const char* bc = std::getenv("MGICP_BAR_CMD")) ctx->bar = std::atoi(bc) != 0;
-  if (const char* sp = std::getenv("MGICP_SPIN_PAUSE")) ctx->spin_pause = std::atoi(sp) != 0;
-  if (const char* sc = std::getenv("MGICP_SRV_CUS")) ctx->srv_cus = std::max(0, std::atoi(sc));
+  // runtime environment (INTEGRATION.md "Environment"): deadlines of the pass transport and the fault
+  // injection of the multi-rank tests only -- every alternative code path is a compile-time option
+  // (Makefile `variant`) or a test's explicit mgicp_debug_option call, never an environment variable
   if (const char* sp = std::getenv("MGICP_SRV_STALL_PASS")) ctx->stall_pass = std::atoi(sp);
   if (const char* qp = std::getenv("MGICP_DEBUG_QUIT_PASS")) ctx->quit_pass = std::atoi(qp);
   if (const char* dl = std::getenv("MGICP_ROW_DEADLINE_MS")) {
@@ -2229,25 +2179,9 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
     const double v = std::atof(rd);
     if (v > 0) ctx->remote_deadline_s = v;
   }
-  ctx->knn_logged = knn_logged_enabled();
-  if (const char* st = std::getenv("MGICP_SPLIT_TARGET_COV")) ctx->split_target_cov = std::atoi(st) != 0;
-  if (const char* ps = std::getenv("MGICP_PROF_STRIDE")) ctx->prof_stride = std::max(1, std::atoi(ps));
-  if (const char* qo = std::getenv("MGICP_QUERY_ORDER")) ctx->query_order = std::atoi(qo) != 0;
-  if (const char* so = std::getenv("MGICP_SRC_GRID_OCC")) {
-    const double v = std::atof(so);
-    if (v >= 1.0 && v <= 256.0) ctx->src.occupancy = v;
-  }
   {
     const unsigned hc = std::thread::hardware_concurrency();
     ctx->host_threads = static_cast<int>(std::max(1u, std::min(8u, hc ? hc : 1u)));
-    if (const char* ht = std::getenv("MGICP_HOST_THREADS")) {
-      const int v = std::atoi(ht);
-      if (v >= 1 && v <= 64) ctx->host_threads = v;
-    }
-  }
-  if (const char* fb = std::getenv("MGICP_FDF_BLOCKS")) {
-    const int v = std::atoi(fb);
-    if (v >= 1 && v <= 65536) ctx->fdf_max_blocks = v;
   }
   if (p) ctx->prm = *p;
   else mgicp_default_params(&ctx->prm);
@@ -2274,38 +2208,12 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
   if (hipDeviceGetAttribute(&ctx->cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess)
     ctx->cus = 0;  // no resident server
   ctx->tgt.want_empty_map = true;  // correspondence / fitness queries start off the surface
-  if (const char* em = std::getenv("MGICP_EMPTY_MAP")) ctx->tgt.want_empty_map = std::atoi(em) != 0;
   ctx->tgt.want_seed_map = true;  // first 1-NN sweep seeded from a nearest non-empty cell
-  if (const char* sm = std::getenv("MGICP_SEED_MAP")) ctx->tgt.want_seed_map = std::atoi(sm) != 0;
   // per-cell point boxes in the 1-NN sweeps: exact and 1.75x fewer candidates in sweep 1, but the
   // per-cell box loads and tests cost more than they save (C4 correspondence 1.39 vs 1.11 ms,
-  // profiles/r02/ab_boxes): off by default, knob MGICP_CELL_BOXES=1
+  // profiles/r02/ab_boxes): off
   ctx->tgt.want_boxes = false;
-  // the wave-uniform 1-NN scan (r03) and the target's pair copy it reads
-  if (const char* cw = std::getenv("MGICP_CORR_WAVE")) ctx->corr_wave = std::atoi(cw) != 0;
-  if (const char* cs = std::getenv("MGICP_CORR_SPLIT")) ctx->corr_split = std::atoi(cs);
-  if (const char* cl = std::getenv("MGICP_CORR_LDS_PTS")) ctx->corr_lds_pts = std::atoi(cl);
-  if (const char* tg = std::getenv("MGICP_SRV_TAGGED")) ctx->srv_tagged = std::atoi(tg) != 0;
-  if (const char* rc = std::getenv("MGICP_CORR_RCAP")) ctx->corr_rcap = static_cast<float>(std::atof(rc));
-  if (const char* mr = std::getenv("MGICP_CORR_MAX_ROWS")) ctx->corr_max_rows = std::max(1, std::atoi(mr));
-  if (const char* mx = std::getenv("MGICP_CORR_MAX_X")) ctx->corr_max_x = std::max(1, std::atoi(mx));
-  if (const char* um = std::getenv("MGICP_CORR_UNION_MIN_R")) ctx->corr_union_min_r = static_cast<float>(std::atof(um));
-  if (const char* vl = std::getenv("MGICP_VLIST")) ctx->vlist = std::atoi(vl) != 0;
-  if (const char* vc = std::getenv("MGICP_VLIST_CELL")) {
-    const float f = static_cast<float>(std::atof(vc));
-    if (f > 0.05f && f < 8.f) ctx->vlist_cell = f;
-  }
-  if (const char* vs = std::getenv("MGICP_VLIST_STATS")) ctx->vl_stats = std::atoi(vs) != 0;
-  if (const char* ve = std::getenv("MGICP_VLIST_EAGER")) ctx->vl_eager = std::atoi(ve) != 0;
-  if (const char* vc = std::getenv("MGICP_VLIST_COLD")) ctx->vl_cold_groups = std::max(0, std::atoi(vc));
-  if (const char* lc = std::getenv("MGICP_LAZY_SRC_COV")) ctx->lazy_src_cov = std::atoi(lc) != 0;
-  if (const char* lc = std::getenv("MGICP_LAZY_TGT_COV")) ctx->lazy_tgt_cov = std::atoi(lc) != 0;
-  if (const char* at = std::getenv("MGICP_ASYNC_COV")) ctx->async_tgt = std::atoi(at) != 0;
-  if (const char* fc = std::getenv("MGICP_FUSE_COMPACT")) ctx->fuse_compact = std::atoi(fc) != 0;
-  if (const char* rc = std::getenv("MGICP_ASYNC_RING_CAP")) ctx->async_ring_cap = std::atoi(rc);
-  if (const char* cs = std::getenv("MGICP_AUX_CU_SKIP")) ctx->aux_cu_skip = std::atoi(cs);
-  ctx->tgt.want_pairs = ctx->corr_wave;
-  if (const char* cb = std::getenv("MGICP_CELL_BOXES")) ctx->tgt.want_boxes = std::atoi(cb) != 0;
+  ctx->tgt.want_pairs = ctx->corr_wave;  // the wave-uniform 1-NN scan (r03) reads the target's pair copy
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
     return MGICP_E_HIP;
@@ -2324,21 +2232,11 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
   // synchronous): here, not in the first align, where they waited for the covariance head start
   (void)ensure_host_red(ctx);  // (retried by the first align if it failed)
   // the stream of the covariance head start (created here: a stream's creation costs milliseconds
-  // of host time, which set_* would otherwise pay before the launch)
-  // optionally on a CU mask that leaves every ctx->aux_cu_skip-th CU free (env MGICP_AUX_CU_SKIP, off):
-  // its k-NN grids (78k blocks at 5M) otherwise take every CU and the main stream's grid build and
-  // first sweep wait behind them (stream priorities did not change that, profiles/r04/prep12)
+  // of host time, which set_* would otherwise pay before the launch).  A CU mask on it (leaving CUs to
+  // the main stream) was measured -0.5 to -1.4 ms on new clouds (profiles/r04/ncab1) but a CU mask
+  // belongs to the hardware queue, which past GPU_MAX_HW_QUEUES streams share: not used.
   hipError_t se = hipSuccess;
-  if (ctx->async_tgt) {
-    if (ctx->aux_cu_skip > 1 && ctx->cus > 0) {
-      std::vector<uint32_t> mask(static_cast<size_t>((ctx->cus + 31) / 32), 0u);
-      for (int c = 0; c < ctx->cus; ++c)
-        if (c % ctx->aux_cu_skip != ctx->aux_cu_skip - 1) mask[c / 32] |= 1u << (c % 32);
-      se = hipExtStreamCreateWithCUMask(&ctx->aux_stream, static_cast<uint32_t>(mask.size()), mask.data());
-    } else {
-      se = hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking);
-    }
-  }
+  if (ctx->async_tgt) se = hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking);
   if (ctx->async_tgt && (se != hipSuccess ||
                          hipEventCreateWithFlags(&ctx->aux_ev[0], hipEventDisableTiming) != hipSuccess ||
                          hipEventCreateWithFlags(&ctx->aux_ev[1], hipEventDisableTiming) != hipSuccess)) {
@@ -2363,7 +2261,6 @@ int mgicp_set_params(mgicp_ctx* ctx, const mgicp_params* p) {
   if (cov_change) {
     ctx->src.have_cov = false;
     ctx->tgt.have_cov = false;
-    ctx->tgt_lazy = false;
     ctx->src_lazy_ready = false;
   }
   return MGICP_OK;
@@ -2400,7 +2297,7 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   ctx->nn_work.release(); ctx->nn_work_n.release();
   ctx->vl_cell.release(); ctx->vl_pool.release(); ctx->vl_ctr.release();
   ctx->vl_build.release(); ctx->vl_bcentre.release(); ctx->vl_pend.release(); ctx->vl_defer.release();
-  ctx->cov_ok.release(); ctx->cov_need.release(); ctx->tcov_ok.release(); ctx->tcov_need.release();
+  ctx->cov_ok.release(); ctx->cov_need.release();
   ctx->aux_cnt.release(); ctx->knn_fb2.release();
   ctx->tpart.release();
   ctx->tpart_n = 0;
@@ -2468,7 +2365,6 @@ int mgicp_align(mgicp_ctx* ctx, const float guess_cm[16], float out_T_cm[16], mg
   AlignDrain drain{ctx};
   int rc = prepare(ctx, true);
   if (rc) return rc;
-  if (ctx->tgt_lazy && ctx->tgt_lazy_aligns > 0 && (rc = cov_lazy(ctx, true))) return rc;  // the rest, once
   MGICP_TRACE_AT("align: prepared");
   rc = ensure_iter_buffers(ctx);
   if (rc) return rc;
@@ -2525,7 +2421,6 @@ int mgicp_align(mgicp_ctx* ctx, const float guess_cm[16], float out_T_cm[16], mg
   drain.armed = false;
   if (!ctx->tgt_cov_pending && !ctx->src_cov_pending) ctx->grave->flush();  // a quiet point
   if (ctx->vl_valid) ctx->vl_groups++;
-  if (ctx->tgt_lazy) ctx->tgt_lazy_aligns++;
   if (ctx->h_gtrace) {
     // diagnostics of the gated passes of this align: device-side gate wait and spread, host-side
     // decision time (sums seen -> command published); device wall clock in 10 ns ticks (100 MHz)
@@ -3000,7 +2895,6 @@ int mgicp_debug_target_cov_slice(mgicp_ctx* ctx, int nranks, int rank, double* o
   // target_cov's slice call, verbatim: the same range, the same N * cnt array layout
   if ((rc = compute_cov(ctx, t, a, b, N * cnt))) return rc;
   t.have_cov = false;  // only a slice is current: the next align recomputes the target's covariances
-  ctx->tgt_lazy = false;
   const size_t st = t.cov_stride, m = b - a;
   std::vector<double2> h(3 * std::max<size_t>(m, 1));
   if (m) {
@@ -3054,7 +2948,6 @@ int mgicp_debug_covariances(mgicp_ctx* ctx, int which, double* out_c6) {
     if ((rc = compute_cov(ctx, ctx->src, ctx->shard_p0(), ctx->shard_p1()))) return rc;
     if (ctx->src_lazy_ready) HIPCK(hipMemsetAsync(ctx->cov_ok.p, 1, ctx->shard_p1() - ctx->shard_p0(), ctx->stream));
   }
-  if (which == 1 && ctx->tgt_lazy && (rc = cov_lazy(ctx, true))) return rc;  // every target covariance
   Cloud& cl = which ? ctx->tgt : ctx->src;
   const size_t n = cl.n;
   const size_t st = cl.cov_stride;
@@ -3207,7 +3100,7 @@ int mgicp_debug_pass_bench(mgicp_ctx* ctx, const double x[6], int npasses, int m
   (void)hipEventDestroy(a);
   (void)hipEventDestroy(b);
   HIPCK(e);
-  if (std::getenv("MGICP_SRV_DEBUG") && mode == 0) {
+  if (MGICP_PASS_DIAG && mode == 0) {
     PassCmd m{};
     HIPCK(hipMemcpy(&m, ctx->mail, sizeof(PassCmd), hipMemcpyDeviceToHost));
     std::fprintf(stderr, "[srv-debug] seq0 %llu npasses %d ms %.3f | mail:", ctx->pass_seq - npasses, npasses, ms);
@@ -3356,6 +3249,61 @@ int mgicp_set_profiling(mgicp_ctx* ctx, int on) {
   for (int i = 0; i < kFams; ++i) {
     ctx->fam_ms[i] = 0;
     ctx->fam_cnt[i] = 0;
+  }
+  return MGICP_OK;
+}
+
+// Test / diagnostic forms of the engine (INTEGRATION.md "Debug options"): explicit per-context calls,
+// never environment variables, so a deployment cannot switch a kernel by accident.
+// Pending covariance launches are joined and the stream drained first; list-related options drop the
+// target's 1-NN cell lists.
+int mgicp_debug_option(mgicp_ctx* ctx, const char* name, double value) {
+  if (!ctx || !name) return MGICP_E_INVALID;
+  HIPCK(hipSetDevice(ctx->device));
+  int rc = cov_join_all(ctx);
+  if (rc || (rc = sync(ctx))) return rc;
+  const std::string n(name);
+  const bool on = value != 0.0;
+  const int iv = static_cast<int>(value);
+  if (n == "resident") ctx->resident = on;              // resident pass server (else one launch per pass)
+  else if (n == "host_rows") ctx->host_rows = on;       // server supers as stamped host rows (else device total)
+  else if (n == "srv_cus") ctx->srv_cus = std::max(0, iv);  // cap on the server's blocks (0 = every CU)
+  else if (n == "fused_finish") ctx->fused_finish = on; // in-launch reduction finish of launched passes
+  else if (n == "gated") ctx->gated = on;               // launched passes pre-queued behind a command gate
+  else if (n == "async_cov") ctx->async_tgt = on && ctx->aux_stream;  // set_*'s covariance head start
+  else if (n == "lazy_src_cov") {                       // source covariances of accepted points only
+    ctx->lazy_src_cov = on;
+    ctx->src.have_cov = false;
+    ctx->src_lazy_ready = false;
+  } else if (n == "knn_logged") {                       // k-NN kernel: wave-staged (1) or register-list only (0)
+    ctx->knn_logged = on;
+    ctx->src.have_cov = ctx->tgt.have_cov = false;
+    ctx->src_lazy_ready = false;
+  } else if (n == "vlist") ctx->vlist = on, ctx->vl_valid = false;  // the target's 1-NN cell lists
+  else if (n == "vlist_cold") ctx->vl_cold_groups = std::max(0, iv), ctx->vl_valid = false;
+  else if (n == "vlist_eager") ctx->vl_eager = on, ctx->vl_valid = false;
+  else if (n == "vlist_stats") ctx->vl_stats = on;      // per-sweep list statistics on stderr
+  else if (n == "fuse_compact") ctx->fuse_compact = on; // compaction fused into listed sweeps
+  else if (n == "grid_occ") {                           // grid sizing (points per non-empty cell), next set_*
+    if (!(value >= 1.0 && value <= 256.0)) return fail(ctx, MGICP_E_INVALID, "grid_occ must be in [1, 256]");
+    ctx->occupancy = value;
+  } else if (n == "bar_cmd") {                          // server commands through the BAR (else pinned copy)
+    ctx->bar = on;
+    if (!on && ctx->bar_cmd) {
+      (void)hipFree(ctx->bar_cmd);
+      ctx->bar_cmd = nullptr;
+    }
+    if (on && !ctx->bar_cmd) {
+      hipDeviceProp_t prop;
+      if (hipGetDeviceProperties(&prop, ctx->device) == hipSuccess && prop.isLargeBar &&
+          hipExtMallocWithFlags(reinterpret_cast<void**>(&ctx->bar_cmd), sizeof(PassCmd), hipDeviceMallocFinegrained) ==
+              hipSuccess)
+        HIPCK(hipMemset(ctx->bar_cmd, 0, sizeof(PassCmd)));
+      else
+        ctx->bar_cmd = nullptr;
+    }
+  } else {
+    return fail(ctx, MGICP_E_INVALID, "unknown debug option: " + n);
   }
   return MGICP_OK;
 }

@@ -128,7 +128,6 @@ hipError_t launch_knn_cov(const GridView& g, int k, double eps, size_t p0, size_
                           Cov3 cov, const uint32_t* perm /*nullable: query order*/, uint32_t* fb,
                           unsigned int* fb_count, hipStream_t s, int ring_cap = -1, uint8_t* ok = nullptr,
                           int chain = 0 /*> 0: the hand-off launch follows on s, that many blocks, device count*/);
-bool knn_logged_enabled();  // env MGICP_KNN2 (default on)
 // nn_pos: per source point (shard-relative) the matched target sorted position, UINT32_MAX when
 // rejected; with `seeded` its previous contents seed the exact 1-NN search.  flags: 1 if accepted.
 hipError_t launch_correspond(const GridView& tgt, const float4* src, size_t p0, size_t p1, Xf34 T,
@@ -201,12 +200,7 @@ hipError_t launch_vl_sweep(const GridView& tgt, const VListView& vl, const float
 // positions p0 + k, *count of them), cov_ok[k] = 1
 hipError_t launch_cov_need(const uint32_t* flags, uint8_t* cov_ok, size_t p0, size_t n, uint32_t* list,
                            unsigned int* count, hipStream_t s);
-// lazy target covariances (r04): rest = 0 -- the target points matched by the sweep's accepted
-// queries (nn_pos) without a covariance; rest = 1 -- every target point without one.  Listed
-// (sorted positions, *count of them) and marked done in ok
-hipError_t launch_tgt_cov_need(const uint32_t* flags, const uint32_t* nn_pos, size_t ns, uint8_t* ok, size_t nt,
-                               int rest, uint32_t* list, unsigned int* count, hipStream_t s);
-// diagnostics (env MGICP_VLIST_STATS): per built cell list lengths histogram etc. into out[64]
+// diagnostics (mgicp_debug_option "vlist_stats"): per built cell list lengths histogram etc. into out[64]
 hipError_t launch_vl_stats(const VListView& vl, size_t ncells, unsigned long long* out /*device, 64*/, hipStream_t s);
 size_t     pair_count(size_t n);
 hipError_t launch_pairs(const float4* pts, size_t n, float4* out, hipStream_t s);

@@ -21,6 +21,12 @@
 #ifndef MGICP_CORR_WAVES
 #define MGICP_CORR_WAVES 8  // resident waves per SIMD requested for the 1-NN kernel (64 VGPRs; A/B profiles/r01/ab_w8)
 #endif
+#ifndef MGICP_KNN_BLK
+#define MGICP_KNN_BLK 1  // k-NN covariances: 1 = wave-staged knn_blk_kernel (r05), 0 = knn_cov2_kernel (r02-r04)
+#endif
+#ifndef MGICP_KNNB_STATS
+#define MGICP_KNNB_STATS 0  // 1 (with MGICP_CORR_PHASES): knn_blk_kernel staging / search counters (diagnostic)
+#endif
 #ifndef MGICP_KNN_INSERT_EARLY
 #define MGICP_KNN_INSERT_EARLY 0  // k-NN top-K insert: 1 = early-exit tail shift, 0 = branchless
 #endif
@@ -147,9 +153,10 @@ __device__ __forceinline__ int near_side(float q, float o, float h, int c) {
 // Visit grid rings (Chebyshev shells of cells) around q in increasing order until the
 // visitor proves that no unvisited point can enter its result.  A ring's rows of cells
 // are contiguous ranges of the sorted point array.
+// r_from > 0: rings below r_from were visited already (the staged block of knn_blk_kernel)
 template <class V>
 __device__ __forceinline__ void ring_search(const GridView& g, float qx, float qy, float qz,
-                                            V& vis) {
+                                            V& vis, int r_from = 0) {
   const int cx = qcell(qx, g.ox, g.inv_h), cy = qcell(qy, g.oy, g.inv_h),
             cz = qcell(qz, g.oz, g.inv_h);
   int rmin = max(max(dist_out(cx, g.nx), dist_out(cy, g.ny)), dist_out(cz, g.nz));
@@ -158,7 +165,7 @@ __device__ __forceinline__ void ring_search(const GridView& g, float qx, float q
     rmin = g.empty_dist[static_cast<size_t>(cx) +
                         static_cast<size_t>(g.nx) * (static_cast<size_t>(cy) + static_cast<size_t>(g.ny) * cz)];
   }
-  for (int r = rmin; r < (1 << 22); ++r) {
+  for (int r = max(rmin, r_from); r < (1 << 22); ++r) {
     if constexpr (V::kRingCap) {
       if (r > vis.ring_cap) {
         vis.gave_up = true;
@@ -1115,6 +1122,423 @@ __global__ __launch_bounds__(64, MGICP_KNN_MINW) void knn_cov2_kernel(GridView g
   // this point in a follow-up launch over the list (knn_cov_kernel with perm = fb)
   if (!ok) fb[atomicAdd(fb_count, 1u)] = static_cast<uint32_t>(p);
   if (ok_out) ok_out[p] = 1;  // computed here or by the hand-off launch
+}
+
+// ---- wave-staged k-NN covariances (r05, default) -----------------------------------------------
+// knn_cov2_kernel runs one ring search per lane over global memory: a dependent round trip per row
+// bound and per batch of a row's points, ~20-50 per query, and only 42 % of wave cycles issue
+// (VERDICT r04 weak 3).  Here the 64 grid-consecutive queries of a wave first stage the points of the
+// union of their 3 x 3 x 3 cell blocks in LDS -- one round trip for 20 cell bounds per lane, then one
+// batch of coalesced loads -- and every lane searches that copy:
+//   pass 1: the exact k-th smallest fp32 d2 (tau) over its block with KthVisitor's med3 network (own
+//           cell first); only when the block does not certify tau against the distance to its faces
+//           (sparse neighbourhoods) does the ring search go on from ring 2 over global memory;
+//   pass 2: the block (and those rings) again with tau fixed: the candidates with d2 <= tau go to a
+//           short LDS log, and the moments are summed in log order under the order-independence
+//           certificate, exactly as knn_cov2_kernel does; ties at tau, log overflow and uncertified
+//           sums go to the register-list hand-off.  No compaction, no per-candidate log traffic.
+// The union: lane l's cells [x-1, x+1] of block row (y + dy, z + dz) are the sorted positions
+// [cs(row, x-1), cs(row, x+2)).  Over grid-ordered lanes these intervals are monotone (in both ends)
+// for each of the 9 block rows, so their union is a few merged pieces, laid out in LDS in position
+// order; lane l reads position j of block row o at LDS index j + delta[o] (one delta per piece).  A
+// wave whose intervals are not monotone (a perm that is not grid order) or whose union exceeds the
+// LDS copy reads the same intervals from global memory: same candidates, same order, same result.
+#ifndef MGICP_KNNB_CAP
+#define MGICP_KNNB_CAP 448  // staged points per wave (16 B each)
+#endif
+#ifndef MGICP_KNNB_LOG
+#define MGICP_KNNB_LOG 8  // pass-2 log entries per lane beyond K
+#endif
+#ifndef MGICP_KNNB_MINW
+#define MGICP_KNNB_MINW 3  // resident waves per SIMD requested (VGPR cap)
+#endif
+constexpr int kKnbCap = MGICP_KNNB_CAP;
+constexpr int kKnbLogExtra = MGICP_KNNB_LOG;
+constexpr int kKnbPieces = 64;
+constexpr uint32_t kKnbGlobal = 0x80000000u;  // log entry flag: a global sorted position (not an LDS index)
+
+// 64-lane inclusive scans, identity 0 (gfx9 DPP: row_shr 1/2/4/8 inside each row of 16 lanes, then
+// row_bcast:15 into rows 1 and 3 and row_bcast:31 into rows 2 and 3; a lane without a source keeps 0)
+__device__ __forceinline__ uint32_t wave_incl_add(uint32_t v) {
+  int x = static_cast<int>(v);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);
+  return static_cast<uint32_t>(x);
+}
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
+  uint32_t x = v;
+  x = max(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x111, 0xf, 0xf, false)));
+  x = max(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x112, 0xf, 0xf, false)));
+  x = max(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x114, 0xf, 0xf, false)));
+  x = max(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x118, 0xf, 0xf, false)));
+  x = max(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x142, 0xa, 0xf, false)));
+  x = max(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x143, 0xc, 0xf, false)));
+  return x;
+}
+
+// pass 1 past the block: KthVisitor's med3 network without its log
+template <int K>
+struct KthList {
+  static constexpr bool kNearFirst = true;
+  static constexpr bool kRingCap = true;
+  int ring_cap = 1 << 30;
+  bool gave_up = false;
+  int nrange = 0;  // global row ranges visited (the block did not settle tau)
+  float qx, qy, qz;
+  float key[K];
+  __device__ __forceinline__ void init(float x, float y, float z, int nsent) {
+    qx = x; qy = y; qz = z;
+#pragma unroll
+    for (int k = 0; k < K; ++k) key[k] = k < nsent ? -1.f : INFINITY;
+  }
+  __device__ __forceinline__ bool done(float Ls) const { return Ls > 0.f && key[K - 1] < Ls * Ls; }
+  __device__ __forceinline__ float prune2() const { return key[K - 1]; }
+  __device__ __forceinline__ void test(float d) {
+    if (d < key[K - 1]) {
+#pragma unroll
+      for (int k = K - 1; k > 0; --k) key[k] = __builtin_amdgcn_fmed3f(key[k - 1], d, key[k]);
+      key[0] = fminf(d, key[0]);
+    }
+  }
+  __device__ __forceinline__ void range(const GridView& g, uint32_t a, uint32_t b) {
+    ++nrange;
+    for (uint32_t j0 = a; j0 < b; j0 += 8) {
+      float4 pb[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) pb[u] = g.pts[min(j0 + u, b - 1)];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (j0 + u < b) test(dist2(qx, qy, qz, pb[u]));
+    }
+  }
+};
+
+// pass 2 past the block: the candidates with d2 <= tau into the lane's log (global positions)
+struct TauLog {
+  static constexpr bool kNearFirst = false;
+  static constexpr bool kRingCap = false;
+  int ring_cap = 1 << 30;
+  bool gave_up = false;
+  float qx, qy, qz, tau;
+  uint32_t* log;  // lane-strided (stride 64)
+  int cnt, cap;
+  __device__ __forceinline__ bool done(float Ls) const { return Ls > 0.f && tau < Ls * Ls; }
+  __device__ __forceinline__ float prune2() const { return tau; }
+  __device__ __forceinline__ void push(uint32_t e) {
+    if (cnt < cap) log[cnt * 64] = e;
+    ++cnt;
+  }
+  __device__ __forceinline__ void range(const GridView& g, uint32_t a, uint32_t b) {
+    for (uint32_t j0 = a; j0 < b; j0 += 8) {
+      float4 pb[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) pb[u] = g.pts[min(j0 + u, b - 1)];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (j0 + u < b && dist2(qx, qy, qz, pb[u]) <= tau) push((j0 + u) | kKnbGlobal);
+    }
+  }
+};
+
+// one block interval [a, b) of global positions through the lane's view (LDS copy at j + delta, or
+// global memory), four candidates in flight
+template <bool kLds, class F>
+__device__ __forceinline__ void blk_interval(const float4* __restrict__ gp, const float4* lp, uint32_t a, uint32_t b,
+                                             uint32_t delta, F&& f) {
+  for (uint32_t j = a; j < b; j += 4) {
+    float4 pb[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t jj = min(j + u, b - 1);
+      pb[u] = kLds ? lp[jj + delta] : gp[jj];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (j + u < b) f(pb[u], j + u);
+  }
+}
+
+// passes 1 and 2 over the lane's block (kLds: the wave's LDS copy) and, where needed, the rings past it
+// passes 1 and 2 over the lane's block (kLds: the wave's LDS copy) and, where needed, the rings past it.
+// Pass 1, phase A: the own cell, the rest of its row and the two y-face rows through the med3 network;
+// their k-th distance tau0 >= tau bounds the rest.  Phase B: the other six rows, each skipped when its
+// y / z slab lies beyond tau0 (ring_search's row test, same margins), and a candidate below tau0 is
+// only deferred (one LDS word) -- the network runs over the deferred few afterwards, not once per
+// candidate of the wave (SIMT: any inserting lane made every lane pay the 20-slot network).  A lane
+// whose phase A saw fewer than k points (tau0 = INF) inserts directly.  Pass 2 rescans the rows that
+// reach tau.
+template <int K, bool kLds>
+__device__ __forceinline__ void knn_blk_search(const GridView& g, const float4& q, int cy, int cz, bool live, bool blk,
+                                               const uint32_t (&s)[9], const uint32_t (&e)[9], uint32_t m0,
+                                               uint32_t m1, const uint32_t (&delta)[9], const float4* lp,
+                                               uint32_t* lg_lane, int nsent, int ring_cap, KthList<K>& v1,
+                                               TauLog& lg) {
+  v1.init(q.x, q.y, q.z, nsent);
+  if (ring_cap >= 0) v1.ring_cap = ring_cap;
+  auto t1 = [&](const float4& pt, uint32_t) { v1.test(dist2(q.x, q.y, q.z, pt)); };
+  blk_interval<kLds>(g.pts, lp, m0, m1, delta[4], t1);
+  blk_interval<kLds>(g.pts, lp, s[4], m0, delta[4], t1);
+  blk_interval<kLds>(g.pts, lp, m1, e[4], delta[4], t1);
+  blk_interval<kLds>(g.pts, lp, s[3], e[3], delta[3], t1);
+  blk_interval<kLds>(g.pts, lp, s[5], e[5], delta[5], t1);
+  const float tau0 = v1.key[K - 1];
+  const bool direct = !(tau0 < INFINITY);
+  // the squared slab gap of block row o (y / z only: ring_search's row test)
+  auto row_gap2 = [&](int o) {
+    const float gy = (o % 3 == 1) ? 0.f : cell_gap(q.y, g.oy, g.h, cy + o % 3 - 1, g.slop);
+    const float gz = (o / 3 == 1) ? 0.f : cell_gap(q.z, g.oz, g.h, cz + o / 3 - 1, g.slop);
+    return gy * gy + gz * gz;
+  };
+  const int dcap = K + kKnbLogExtra;
+  int nd = 0;
+  constexpr int kB[6] = {1, 7, 0, 2, 6, 8};
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int o = kB[i];
+    const bool use = row_gap2(o) <= tau0 * 1.00001f;
+    blk_interval<kLds>(g.pts, lp, s[o], use ? e[o] : s[o], delta[o], [&](const float4& pt, uint32_t) {
+      const float d = dist2(q.x, q.y, q.z, pt);
+      if (d < tau0) {
+        if (direct) {
+          v1.test(d);
+        } else {
+          if (nd < dcap) lg_lane[nd * 64] = __float_as_uint(d);
+          ++nd;
+        }
+      }
+    });
+  }
+  // the deferred candidates through the network (overflow: the lane rescans phase B with it)
+  if (nd <= dcap) {
+    for (int i = 0; i < nd; ++i) v1.test(__uint_as_float(lg_lane[i * 64]));
+  } else {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) blk_interval<kLds>(g.pts, lp, s[kB[i]], e[kB[i]], delta[kB[i]], t1);
+  }
+  // rings >= 2 only when the block does not certify tau (ring_search's own test at ring 2); a lane
+  // outside the grid (never, for a cloud's own points) searches from its first ring
+  if (live) ring_search(g, q.x, q.y, q.z, v1, blk ? 2 : 0);
+  lg.qx = q.x; lg.qy = q.y; lg.qz = q.z;
+  lg.tau = v1.key[K - 1];
+  lg.log = lg_lane;
+  lg.cnt = 0;
+  lg.cap = K + kKnbLogExtra;
+  if (!live || v1.gave_up) return;
+  const float tau = lg.tau;
+  const float w2 = tau * 1.00001f;
+#pragma unroll
+  for (int o = 0; o < 9; ++o) {
+    const uint32_t eo = row_gap2(o) <= w2 ? e[o] : s[o];
+    if constexpr (kLds) {
+      const uint32_t d = delta[o];  // log entries: the copy's index
+      blk_interval<kLds>(g.pts, lp, s[o], eo, d, [&](const float4& pt, uint32_t j) {
+        if (dist2(q.x, q.y, q.z, pt) <= tau) lg.push(j + d);
+      });
+    } else {
+      blk_interval<kLds>(g.pts, lp, s[o], eo, 0u, [&](const float4& pt, uint32_t j) {
+        if (dist2(q.x, q.y, q.z, pt) <= tau) lg.push(j | kKnbGlobal);
+      });
+    }
+  }
+  if (v1.nrange > 0 || !blk) ring_search(g, q.x, q.y, q.z, lg, blk ? 2 : 0);
+}
+
+template <int K>
+__global__ __launch_bounds__(64, MGICP_KNNB_MINW) void knn_blk_kernel(GridView g, double eps, size_t p0, size_t p1,
+                                                                     Cov3 cov, const uint32_t* __restrict__ perm,
+                                                                     int nsent, uint32_t* __restrict__ fb,
+                                                                     unsigned int* __restrict__ fb_count, int ring_cap,
+                                                                     uint8_t* __restrict__ ok_out) {
+  __shared__ float4 s_pts[kKnbCap];
+  __shared__ uint32_t s_log[(K + kKnbLogExtra) * 64];
+  __shared__ uint32_t s_pc[2 * kKnbPieces];  // pieces: LDS start, global start (in LDS order)
+  const int lane = static_cast<int>(threadIdx.x);
+  const size_t t = static_cast<size_t>(blockIdx.x) * 64 + lane;
+  const bool live = t < p1 - p0;
+  const size_t p = p0 + (live ? (perm ? perm[t] : t) : 0);
+  const float4 q = g.pts[p];
+  const int cx = qcell(q.x, g.ox, g.inv_h), cy = qcell(q.y, g.oy, g.inv_h), cz = qcell(q.z, g.oz, g.inv_h);
+  const bool blk = live && cx >= 0 && cx < g.nx && cy >= 0 && cy < g.ny && cz >= 0 && cz < g.nz;
+  // the 9 rows of the lane's block (o = 3 (dz + 1) + dy + 1): positions [s[o], e[o]); the own cell
+  // [m0, m1) inside the middle row -- 20 independent loads, one round trip
+  uint32_t s[9], e[9], m0, m1;
+  {
+    const int xa = max(cx - 1, 0), xb = min(cx + 1, g.nx - 1);
+    size_t ia[9], ib[9];
+    bool in[9];
+#pragma unroll
+    for (int o = 0; o < 9; ++o) {
+      const int y = cy + o % 3 - 1, z = cz + o / 3 - 1;
+      in[o] = blk && y >= 0 && y < g.ny && z >= 0 && z < g.nz;
+      const size_t row = in[o] ? (static_cast<size_t>(z) * g.ny + y) * g.nx : 0;
+      ia[o] = in[o] ? row + xa : 0;
+      ib[o] = in[o] ? row + xb + 1 : 0;
+    }
+    const size_t rm = blk ? (static_cast<size_t>(cz) * g.ny + cy) * g.nx + cx : 0;
+#pragma unroll
+    for (int o = 0; o < 9; ++o) {
+      s[o] = g.cell_start[ia[o]];
+      e[o] = g.cell_start[ib[o]];
+    }
+    m0 = g.cell_start[rm];
+    m1 = g.cell_start[rm + 1];
+#pragma unroll
+    for (int o = 0; o < 9; ++o)
+      if (!in[o]) s[o] = e[o] = 0u;
+    if (!blk) m0 = m1 = 0u;
+  }
+  // the union of the wave's intervals per block row: merged pieces in LDS order
+  uint32_t delta[9];
+  uint32_t base = 0, npc = 0;
+  bool mono = true;
+#pragma unroll
+  for (int o = 0; o < 9; ++o) {
+    const bool v = s[o] < e[o];
+    const uint32_t sv = v ? s[o] : 0u, ev = v ? e[o] : 0u;
+    const uint32_t ism = wave_incl_max(sv), iem = wave_incl_max(ev);
+    const uint32_t ps = __shfl_up(ism, 1, 64), pe = __shfl_up(iem, 1, 64);
+    const uint32_t psx = lane ? ps : 0u, pex = lane ? pe : 0u;
+    if (v && sv < psx) mono = false;
+    const uint32_t a = max(sv, pex);
+    const uint32_t c = (v && ev > a) ? ev - a : 0u;
+    const uint32_t ic = wave_incl_add(c);
+    const uint32_t tot = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(ic), 63));
+    const bool start = c > 0u && (sv > pex || pex == 0u);
+    const unsigned long long sm = __builtin_amdgcn_ballot_w64(start);
+    const uint32_t dst = base + (ic - c) - a;  // LDS index - position, on contributing lanes
+    const unsigned long long below = sm & ((2ull << lane) - 1ull);
+    const int L = below ? 63 - __builtin_clzll(below) : 0;
+    delta[o] = static_cast<uint32_t>(__shfl(static_cast<int>(dst), L, 64));
+    if (start) {
+      const uint32_t k = npc + static_cast<uint32_t>(__builtin_popcountll(sm & ((1ull << lane) - 1ull)));
+      if (k < static_cast<uint32_t>(kKnbPieces)) {
+        s_pc[2 * k] = base + (ic - c);
+        s_pc[2 * k + 1] = a;
+      }
+    }
+    npc += static_cast<uint32_t>(__builtin_popcountll(sm));
+    base += tot;
+  }
+  const bool stage = __builtin_amdgcn_ballot_w64(!mono) == 0ull && base <= static_cast<uint32_t>(kKnbCap) &&
+                     npc <= static_cast<uint32_t>(kKnbPieces);
+#if MGICP_KNNB_STATS
+  {  // [0] waves [1] staged [2] union points [3] pieces [4] non-monotone waves [5] over the cap
+     // [6] lane block candidates (sum) [7] busiest lane's block candidates (sum over waves)
+    uint32_t bc = 0;
+#pragma unroll
+    for (int o = 0; o < 9; ++o) bc += e[o] - s[o];
+    uint32_t bm = bc;
+    unsigned long long bs = bc;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      bm = max(bm, static_cast<uint32_t>(__shfl_xor(static_cast<int>(bm), off, 64)));
+      bs += __shfl_xor(bs, off, 64);
+    }
+    if (lane == 0) {
+      atomicAdd(&g_corr_phase[0], 1ull);
+      atomicAdd(&g_corr_phase[1], stage ? 1ull : 0ull);
+      atomicAdd(&g_corr_phase[2], static_cast<unsigned long long>(base));
+      atomicAdd(&g_corr_phase[3], static_cast<unsigned long long>(npc));
+      atomicAdd(&g_corr_phase[4], __builtin_amdgcn_ballot_w64(!mono) ? 1ull : 0ull);
+      atomicAdd(&g_corr_phase[5], base > static_cast<uint32_t>(kKnbCap) ? 1ull : 0ull);
+      atomicAdd(&g_corr_phase[6], bs);
+      atomicAdd(&g_corr_phase[7], static_cast<unsigned long long>(bm));
+    }
+  }
+#endif
+  KthList<K> v1;
+  TauLog lg;
+  uint32_t* lg_lane = s_log + lane;
+  if (stage) {
+    __syncthreads();  // the piece table
+    // element i = lane + 64 u of the copy: its piece (binary search over the LDS starts)
+    constexpr int kU = (kKnbCap + 63) / 64;
+    float4 buf[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const uint32_t i = static_cast<uint32_t>(lane + 64 * u);
+      int lo = 0;
+#pragma unroll
+      for (int st = 32; st > 0; st >>= 1) {
+        const int m = lo + st;
+        if (m < static_cast<int>(npc) && s_pc[2 * m] <= i) lo = m;
+      }
+      const uint32_t gpos = s_pc[2 * lo + 1] + (i - s_pc[2 * lo]);
+      buf[u] = g.pts[i < base ? gpos : 0u];
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const uint32_t i = static_cast<uint32_t>(lane + 64 * u);
+      if (i < base) s_pts[i] = buf[u];
+    }
+    __syncthreads();
+    knn_blk_search<K, true>(g, q, cy, cz, live, blk, s, e, m0, m1, delta, s_pts, lg_lane, nsent, ring_cap, v1, lg);
+  } else {
+    knn_blk_search<K, false>(g, q, cy, cz, live, blk, s, e, m0, m1, delta, s_pts, lg_lane, nsent, ring_cap, v1, lg);
+  }
+  if (!live || v1.gave_up) return;  // gave up: the lazy pass computes it if a sweep accepts it
+  const int kreal = K - nsent;
+  const int cnt = lg.cnt;
+  bool ok = cnt == kreal;  // (<= K, within the log)
+  if (ok) {
+    double m0d = 0.0, m1d = 0.0, m2d = 0.0;
+    double a[3][3] = {{0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}};
+    SumCert c0, c1, c2, c00, c10, c11, c20, c21, c22;
+    for (int i0 = 0; i0 < cnt; i0 += 4) {
+      float4 pb[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t en = lg_lane[min(i0 + u, cnt - 1) * 64];
+        pb[u] = (en & kKnbGlobal) ? g.pts[en & ~kKnbGlobal] : s_pts[en];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (i0 + u >= cnt) continue;
+        const float4 pt = pb[u];
+        const float xx = pt.x * pt.x, yx = pt.y * pt.x, yy = pt.y * pt.y;
+        const float zx = pt.z * pt.x, zy = pt.z * pt.y, zz = pt.z * pt.z;
+        m0d += pt.x;
+        m1d += pt.y;
+        m2d += pt.z;
+        a[0][0] += static_cast<double>(xx);
+        a[1][0] += static_cast<double>(yx);
+        a[1][1] += static_cast<double>(yy);
+        a[2][0] += static_cast<double>(zx);
+        a[2][1] += static_cast<double>(zy);
+        a[2][2] += static_cast<double>(zz);
+        c0.add(pt.x);
+        c1.add(pt.y);
+        c2.add(pt.z);
+        c00.add(xx);
+        c10.add(yx);
+        c11.add(yy);
+        c20.add(zx);
+        c21.add(zy);
+        c22.add(zz);
+      }
+    }
+    ok = c0.ok() && c1.ok() && c2.ok() && c00.ok() && c10.ok() && c11.ok() && c20.ok() && c21.ok() && c22.ok();
+    if (ok) cov_finish(m0d, m1d, m2d, a, static_cast<double>(kreal), eps, cov, p);
+  }
+#if MGICP_KNNB_STATS
+  {  // [8] lanes past the block (rings >= 2) [9] hand-offs [10] live lanes
+    const unsigned long long pm = __builtin_amdgcn_ballot_w64(v1.nrange > 0 || !blk);
+    const unsigned long long hm = __builtin_amdgcn_ballot_w64(!ok);
+    const unsigned long long lm = __builtin_amdgcn_ballot_w64(true);
+    if (lane == __builtin_ctzll(lm)) {
+      atomicAdd(&g_corr_phase[8], static_cast<unsigned long long>(__builtin_popcountll(pm)));
+      atomicAdd(&g_corr_phase[9], static_cast<unsigned long long>(__builtin_popcountll(hm)));
+      atomicAdd(&g_corr_phase[10], static_cast<unsigned long long>(__builtin_popcountll(lm)));
+    }
+  }
+#endif
+  // ties at tau, log overflow or an uncertified sum: the sorted register-list kernel finishes it
+  if (!ok) fb[atomicAdd(fb_count, 1u)] = static_cast<uint32_t>(p);
+  if (ok_out) ok_out[p] = 1;
 }
 
 // ------------------------------------------------------------------------------------
@@ -3643,27 +4067,22 @@ hipError_t launch_iota(uint32_t* v, size_t n, hipStream_t s) {
   return hipGetLastError();
 }
 
-// log capacity (entries per lane) of the logged k-NN kernel: env MGICP_KNN_LOG, default K + 28
-static int knn_log_cap(int K) {
-  int cap = K + 28;
-  if (const char* e = std::getenv("MGICP_KNN_LOG")) cap = std::atoi(e);
-  return std::min(std::max(cap, K + 1), 128);
-}
-
-static bool knn_two_phase() {  // env MGICP_KNN2 (default 1): knn_cov2_kernel, else knn_cov_kernel
-  const char* e = std::getenv("MGICP_KNN2");
-  return !(e && std::atoi(e) == 0);
-}
+// log capacity (entries per lane) of the r04 logged k-NN kernel (MGICP_KNN_BLK=0 builds): K + 28
+[[maybe_unused]] static int knn_log_cap(int K) { return std::min(K + 28, 128); }
 
 template <int K>
 static hipError_t knn_cov_k(const GridView& g, double eps, size_t p0, size_t p1, Cov3 cov,
                             const uint32_t* perm, int k, uint32_t* fb, unsigned int* fb_count, hipStream_t s,
                             int ring_cap, uint8_t* ok, int chain) {
   if (fb) {
+#if MGICP_KNN_BLK
+    knn_blk_kernel<K><<<nblk(p1 - p0, 64), 64, 0, s>>>(g, eps, p0, p1, cov, perm, K - k, fb, fb_count, ring_cap, ok);
+#else
     const int cap = knn_log_cap(K);
     knn_cov2_kernel<K><<<nblk(p1 - p0, 64), 64, cap * 64 * sizeof(uint32_t), s>>>(g, eps, p0, p1, cov, perm,
                                                                                  K - k, cap, fb, fb_count, ring_cap,
                                                                                  ok);
+#endif
     // chain: the hand-off follows at once in stream order, its count read on the device (a grid of
     // `chain` blocks striding over the list)
     if (chain > 0) knn_cov_kernel<K><<<chain, 256, 0, s>>>(g, eps, 0, 0, cov, fb, K - k, fb_count);
@@ -3675,7 +4094,7 @@ static hipError_t knn_cov_k(const GridView& g, double eps, size_t p0, size_t p1,
 
 // exact instantiations for PCL's default (20) and its round neighbours; any other k in
 // [1, kMaxK] runs on the next multiple of 8 with K - k sentinel slots.  With fb / fb_count the
-// logged-threshold kernel runs and lists the points it leaves to KnnVisitor; without, (or for that
+// wave-staged kernel (r05; knn_cov2_kernel in MGICP_KNN_BLK=0 builds) runs and lists the points it leaves to KnnVisitor; without, (or for that
 // list: perm = fb, p0 = 0, p1 = count) the register-list kernel runs.
 hipError_t launch_knn_cov(const GridView& g, int k, double eps, size_t p0, size_t p1, Cov3 cov,
                           const uint32_t* perm, uint32_t* fb, unsigned int* fb_count, hipStream_t s, int ring_cap,
@@ -3697,7 +4116,6 @@ hipError_t launch_knn_cov(const GridView& g, int k, double eps, size_t p0, size_
   return knn_cov_k<32>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain);
 }
 
-bool knn_logged_enabled() { return knn_two_phase(); }
 
 hipError_t launch_vl_sweep(const GridView& tgt, const VListView& vl, const float4* src, size_t p0, size_t p1,
                            Xf34 T, double thr, int seeded, uint32_t* nn_pos, uint32_t* flags, int cus,
@@ -3776,26 +4194,6 @@ hipError_t launch_cov_need(const uint32_t* flags, uint8_t* cov_ok, size_t p0, si
   hipError_t e = hipMemsetAsync(count, 0, sizeof(unsigned int), s);
   if (e != hipSuccess || n == 0) return e;
   cov_need_kernel<<<nblk(n, 256 * kCovNeedPer), 256, 0, s>>>(flags, cov_ok, p0, n, list, count, 0);
-  return hipGetLastError();
-}
-
-// the matched target points of a sweep: ok[nn_pos[k]] 0 -> 2 for every accepted k (plain stores:
-// racing writers store the same value)
-__global__ __launch_bounds__(256) void cov_mark_kernel(const uint32_t* __restrict__ flags,
-                                                       const uint32_t* __restrict__ nn_pos, size_t n,
-                                                       uint8_t* __restrict__ ok) {
-  const size_t k = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (k >= n || !flags[k]) return;
-  const uint32_t j = nn_pos[k];
-  if (ok[j] == 0) ok[j] = 2;
-}
-
-hipError_t launch_tgt_cov_need(const uint32_t* flags, const uint32_t* nn_pos, size_t ns, uint8_t* ok, size_t nt,
-                               int rest, uint32_t* list, unsigned int* count, hipStream_t s) {
-  hipError_t e = hipMemsetAsync(count, 0, sizeof(unsigned int), s);
-  if (e != hipSuccess || nt == 0) return e;
-  if (!rest && ns) cov_mark_kernel<<<nblk(ns), 256, 0, s>>>(flags, nn_pos, ns, ok);
-  cov_need_kernel<<<nblk(nt, 256 * kCovNeedPer), 256, 0, s>>>(nullptr, ok, 0, nt, list, count, rest);
   return hipGetLastError();
 }
 
@@ -3909,7 +4307,9 @@ hipError_t launch_fdf_server(const CorrSoA& c, const uint32_t* ccnt, size_t ns, 
                              Xf34 A, unsigned long long* host_rows, size_t rows_stride, int nb, int waves,
                              int pollers, int stall_pass, unsigned long long* tpart, hipStream_t s) {
   int nch = chunk_count(ns);
-  if (nch == 0 || nb <= 0 || (waves != 4 && waves != 8)) return hipErrorInvalidValue;
+  // one shape: 4 waves per CU (the 8-wave shape, 2 waves per SIMD with less residency, measured
+  // 57.7-58.0 vs 50.2-50.3 us per pass, profiles/r03/srv8, is not built)
+  if (nch == 0 || nb <= 0 || waves != 4) return hipErrorInvalidValue;
   // a pass completes only when every block has run it, so refuse a grid the device cannot hold at
   // once (one block per CU, at most one per CU by its LDS and registers).  That check is all a
   // cooperative launch adds; the blocks do not synchronise with each other (only with the host's
@@ -3917,10 +4317,8 @@ hipError_t launch_fdf_server(const CorrSoA& c, const uint32_t* ccnt, size_t ns, 
   // cancelled by the host after its deadline -- blocks that start late see the later command at
   // their first gate and exit (pass_gate) -- and the pass re-runs as a launched pass.
   const bool b = bench_passes > 0;
-  const void* fn = waves == 4 ? (b ? reinterpret_cast<const void*>(fdf_server_kernel<true, 4>)
-                                   : reinterpret_cast<const void*>(fdf_server_kernel<false, 4>))
-                              : (b ? reinterpret_cast<const void*>(fdf_server_kernel<true, 8>)
-                                   : reinterpret_cast<const void*>(fdf_server_kernel<false, 8>));
+  const void* fn = b ? reinterpret_cast<const void*>(fdf_server_kernel<true, 4>)
+                     : reinterpret_cast<const void*>(fdf_server_kernel<false, 4>);
   int per_cu = 0, dev = 0, cus = 0;
   hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * waves, 0);
   if (e == hipSuccess) e = hipGetDevice(&dev);
@@ -3931,13 +4329,8 @@ hipError_t launch_fdf_server(const CorrSoA& c, const uint32_t* ccnt, size_t ns, 
   fdf_server_kernel<B, W><<<nb, 64 * (W), 0, s>>>(c, ccnt, nch, partial, spart, tickets, out, done_flag, \
                                                   seq0, cmd, mail, timeout_ticks, ptimes, bench_passes, A, host_rows, \
                                                   rows_stride, pollers, stall_pass, tpart)
-  if (waves == 4) {
-    if (b) MGICP_SRV_LAUNCH(true, 4);
-    else MGICP_SRV_LAUNCH(false, 4);
-  } else {
-    if (b) MGICP_SRV_LAUNCH(true, 8);
-    else MGICP_SRV_LAUNCH(false, 8);
-  }
+  if (b) MGICP_SRV_LAUNCH(true, 4);
+  else MGICP_SRV_LAUNCH(false, 4);
 #undef MGICP_SRV_LAUNCH
   return hipGetLastError();
 }

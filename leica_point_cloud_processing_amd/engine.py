@@ -44,7 +44,8 @@ def _dp(a):
 
 
 class GICPEngine:
-    def __init__(self, device: int = -1, **params):
+    def __init__(self, device: int = -1, options: dict | None = None, **params):
+        """params: mgicp_params fields; options: mgicp_debug_option forms (tests / diagnostics only)"""
         self._lib = _lib.load()
         self.params = _lib.default_params()
         self.params.device = device
@@ -61,6 +62,12 @@ class GICPEngine:
         self._converged = False
         self._final = np.eye(4, dtype=np.float32)
         self.last_result = None
+        for k, v in (options or {}).items():
+            self.debug_option(k, v)
+
+    def debug_option(self, name: str, value):
+        """mgicp_debug_option: a test / diagnostic form of the engine on this context only"""
+        self._check(self._lib.mgicp_debug_option(self._h, name.encode(), float(value)), f"debug option {name}")
 
     def close(self):
         """Release the device context (deterministically, before interpreter shutdown)."""

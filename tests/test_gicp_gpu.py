@@ -363,7 +363,7 @@ def test_seeded_correspondences_lattice_ties(engine_mod):
 @pytest.mark.gpu
 @pytest.mark.parametrize("k", [20, 7, 32])
 def test_logged_knn_matches_register_list(engine_mod, part_small, monkeypatch, capfd, k):
-    """The logged k-NN kernel (MGICP_KNN2=1, default) sums the moments in log order when exactly k
+    """The k-NN kernel (wave-staged since r05; debug option "knn_logged", default 1) sums the moments in log order when exactly k
     entries fall within tau and the nine sums are certified order-independent; every other point
     goes to the register-list kernel.  Both paths must give the register-list kernel's covariances
     bit for bit -- on clouds built to hit the hand-off: a part centred on the origin (neighbours
@@ -383,9 +383,8 @@ def test_logged_knn_matches_register_list(engine_mod, part_small, monkeypatch, c
     for name, pts in clouds.items():
         res = {}
         for knn2 in ("0", "1"):
-            monkeypatch.setenv("MGICP_KNN2", knn2)
             monkeypatch.setenv("MGICP_KNN_STATS", "1")
-            e = engine_mod(k=k)
+            e = engine_mod(k=k, options={"knn_logged": int(knn2)})
             e.set_source_xyz(pts)
             e.set_target_xyz(pts[: len(pts) // 2])
             res[knn2] = e.debug_covariances("source", len(pts))
@@ -424,15 +423,14 @@ def test_async_covariance_prep_matches_sync(engine_mod, monkeypatch, part_small,
     second stream (the target's overlap the source's upload, the source's the first sweep); prepare
     and the first sweep join them.  Aligns, covariances, a k change while launches may still run,
     back-to-back set_* calls and a destroy with launches pending all match the synchronous path
-    (MGICP_ASYNC_COV=0) bit for bit -- with the set_* calls in either order (the reference sets the
+    (debug option "async_cov" 0) bit for bit -- with the set_* calls in either order (the reference sets the
     source first, GICPAlignment.cpp:89-90; the source grid must still start from the target's)."""
     scan, cad, _ = part_small
     cad2 = np.ascontiguousarray(cad[::-1])
     scan2 = np.ascontiguousarray(scan[::-1])
     res = {}
     for a in (1, 0):
-        monkeypatch.setenv("MGICP_ASYNC_COV", str(a))
-        e = engine_mod()
+        e = engine_mod(options={"async_cov": a})
         if source_first:
             e.set_source_xyz(scan)
             e.set_target_xyz(cad)
@@ -472,52 +470,14 @@ def test_async_covariance_prep_matches_sync(engine_mod, monkeypatch, part_small,
 
 
 @pytest.mark.gpu
-def test_lazy_target_covariances_match_eager(engine_mod, monkeypatch):
-    """r04 lazy target covariances: the first align after a set_target computes the covariances of
-    the target points its sweeps match (the rest of the CAD cloud -- its far side -- never pays the
-    20-NN search in a one-off align); the second align computes the rest once.  Three aligns (lazy,
-    completing, complete) and a debug sweep are bitwise the eager computation's (MGICP_LAZY_TGT_COV=0),
-    and so is every target covariance."""
-    from leica_point_cloud_processing_amd import synth
-
-    scan, cad, _ = synth.scan_vs_cad(60_000, 80_000, clutter=0.04, debris=600)
-    res = {}
-    monkeypatch.setenv("MGICP_ASYNC_COV", "0")  # set_*'s covariance head start would cover every point
-    for lazy in (1, 0):
-        monkeypatch.setenv("MGICP_LAZY_TGT_COV", str(lazy))
-        e = engine_mod()
-        e.set_source_xyz(scan)
-        e.set_target_xyz(cad)
-        out = []
-        for _ in range(3):
-            T = e.align()
-            r = e.last_result
-            out.append((T, r["iterations"], r["n_evals"], r["n_corr"]))
-        m, tj, M = e.debug_correspondences(out[0][0], len(scan))
-        e.set_target_xyz(cad)  # a new target: lazy again; its covariances on demand
-        C = e.debug_covariances("target", len(cad))
-        res[lazy] = (out, m, tj, M, C)
-        e.close()
-    a, b = res[1], res[0]
-    for (Ta, *ra), (Tb, *rb) in zip(a[0], b[0]):
-        np.testing.assert_array_equal(Ta, Tb)
-        assert ra == rb
-    assert a[1] == b[1]
-    np.testing.assert_array_equal(a[2], b[2])
-    np.testing.assert_array_equal(a[3], b[3])
-    np.testing.assert_array_equal(a[4], b[4])
-
-
-@pytest.mark.gpu
 def test_gated_passes_match_plain_launches(engine_mod, part_small, monkeypatch):
-    """Pre-launched (gated) objective passes (MGICP_GATED, default on) wait on the host's command
+    """Pre-launched (gated) objective passes (debug option "gated", default on) wait on the host's command
     block; they must reproduce the plain launches bit for bit, leave no pass behind when a BFGS
     run ends, and never hold the stream (destroy / debug calls with a pass queued)."""
     src, tgt, _ = part_small
     res = {}
     for gated in ("0", "1"):
-        monkeypatch.setenv("MGICP_GATED", gated)
-        e = engine_mod()
+        e = engine_mod(options={"gated": int(gated)})
         e.set_source_xyz(src)
         e.set_target_xyz(tgt)
         T = e.align()
@@ -553,19 +513,16 @@ def test_fused_compaction_matches_unfused(engine_mod, part_small, monkeypatch, l
     a pending query (cells being built) or, lazy = 1, an accepted point whose source covariance is
     not computed yet (synchronous lazy source mode) are deferred to the compaction launch.  Every
     sweep's indices and Mahalanobis matrices (cold, building, listed, new transforms that accept new
-    points) and three aligns equal the unfused path (MGICP_FUSE_COMPACT=0) bit for bit."""
+    points) and three aligns equal the unfused path (debug option "fuse_compact" 0) bit for bit."""
     name, src, tgt, Ttrue = _vlist_cases(part_small)[1]  # clutter + debris: gate rejections
     Tinv = np.linalg.inv(Ttrue).astype(np.float32)
     I = np.eye(4, dtype=np.float32)
     off = np.eye(4, dtype=np.float32)
     off[:3, 3] = [0.004, -0.003, 0.02]
     Ts = [I, I, I, Tinv, off, Tinv, off]
-    monkeypatch.setenv("MGICP_ASYNC_COV", "0" if lazy else "1")
-    monkeypatch.setenv("MGICP_LAZY_SRC_COV", str(lazy))
     res = {}
     for fuse in (1, 0):
-        monkeypatch.setenv("MGICP_FUSE_COMPACT", str(fuse))
-        e = engine_mod()
+        e = engine_mod(options={"async_cov": 0 if lazy else 1, "lazy_src_cov": lazy, "fuse_compact": fuse})
         e.set_target_xyz(tgt)
         e.set_source_xyz(src)
         sweeps = [e.debug_correspondences(T, len(src)) for T in Ts]
@@ -590,8 +547,8 @@ def test_vlist_sweeps_bitexact_through_builds(engine_mod, part_small, monkeypatc
     builds the lists of the cells it queries (those queries take the exact per-lane search), the
     third finds every cell listed (every query answered from a list), then new transforms (lists
     and builds mixed) -- every sweep's indices and Mahalanobis matrices bit-exact against the
-    oracle and against the r03 sweep (MGICP_VLIST=0), with rejections near the 4 cm gate and
-    exact-distance ties.  eager = 0 (MGICP_VLIST_EAGER=0, MGICP_VLIST_COLD=0): lists used from the
+    oracle and against the r03 sweep (debug option "vlist" 0), with rejections near the 4 cm gate and
+    exact-distance ties.  eager = 0 (options "vlist_eager" 0, "vlist_cold" 0): lists used from the
     first sweep, a cell built only when a later sweep queries it again."""
     from oracle import ref
 
@@ -604,13 +561,10 @@ def test_vlist_sweeps_bitexact_through_builds(engine_mod, part_small, monkeypatc
     o = ref.RefGICP()
     o.set_source(src)
     o.set_target(tgt)
-    monkeypatch.setenv("MGICP_VLIST_EAGER", str(eager))
-    monkeypatch.setenv("MGICP_VLIST_COLD", str(eager))
-    e = engine_mod()
+    e = engine_mod(options={"vlist_eager": eager, "vlist_cold": eager})
     e.set_source_xyz(src)
     e.set_target_xyz(tgt)
-    monkeypatch.setenv("MGICP_VLIST", "0")
-    e0 = engine_mod()
+    e0 = engine_mod(options={"vlist_eager": eager, "vlist_cold": eager, "vlist": 0})
     e0.set_source_xyz(src)
     e0.set_target_xyz(tgt)
     stats = []
@@ -675,15 +629,14 @@ def test_lazy_source_covariances_match_eager(engine_mod, monkeypatch):
     """r04 lazy source covariances: a source point's covariance is computed the first time a sweep
     accepts it (clutter the gate never accepts never pays the 20-NN search).  On a scan with 4 %
     clutter and debris the align -- T, iterations, passes, the last correspondences and their
-    Mahalanobis matrices -- is bitwise the eager computation's (MGICP_LAZY_SRC_COV=0)."""
+    Mahalanobis matrices -- is bitwise the eager computation's (debug option "lazy_src_cov" 0)."""
     from leica_point_cloud_processing_amd import synth
 
     scan, cad, _ = synth.scan_vs_cad(60_000, 60_000, clutter=0.04, debris=600)
     res = {}
-    monkeypatch.setenv("MGICP_ASYNC_COV", "0")  # set_*'s covariance head start would cover every point
     for lazy in (1, 0):
-        monkeypatch.setenv("MGICP_LAZY_SRC_COV", str(lazy))
-        e = engine_mod()
+        # without set_*'s covariance head start, which would cover every point
+        e = engine_mod(options={"async_cov": 0, "lazy_src_cov": lazy})
         e.set_source_xyz(scan)
         e.set_target_xyz(cad)
         T = e.align()
