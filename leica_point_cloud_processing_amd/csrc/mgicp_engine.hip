@@ -677,6 +677,7 @@ int reset_stamps(mgicp_ctx* ctx) {
 
 // Upload strided host records (or copy device records) and pack to float4 (original order).
 int build_grid(mgicp_ctx* ctx, Cloud& cl);
+const uint32_t* query_perm(mgicp_ctx* ctx);
 
 // the covariances started by cov_prep_async: wait for the aux stream, then hand the points the
 // logged kernel left (log overflow, ties at the k-th distance) to the register-list kernel on the
@@ -746,6 +747,9 @@ int cov_prep_async(mgicp_ctx* ctx, bool tgt) {
                        ctx->knn_logged ? 2 * std::max(ctx->cus, 1) : 0));
   HIPCK(hipEventRecord(ctx->aux_ev[tgt ? 0 : 1], ctx->aux_stream));
   (tgt ? ctx->tgt_cov_pending : ctx->src_cov_pending) = true;
+  // r05: the source's 1-NN query order (a Morton sort of the shard) now, on the main stream beside the
+  // covariances -- not inside the first align's loop
+  if (!tgt) (void)query_perm(ctx);
   return MGICP_OK;
 }
 
@@ -753,7 +757,8 @@ int cov_prep_async(mgicp_ctx* ctx, bool tgt) {
 // first, the source only once the target's grid exists (the source grid starts from the target's
 // cell size, so the grids, and with them every sorted order and sum, are those of the synchronous
 // path whatever the order of the set_* calls; the reference calls setInputSource first,
-// GICPAlignment.cpp:89-90)
+// GICPAlignment.cpp:89-90).  r05: the target's covariances are joined only before the first
+// compaction, so they run beside the source's grid build, its Morton order and the first 1-NN sweep
 int cov_prep_async_all(mgicp_ctx* ctx) {
   int rc = MGICP_OK;
   if (ctx->tgt.dirty && (rc = cov_prep_async(ctx, true))) return rc;
@@ -874,7 +879,11 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
   };
   double h = maxext > 0.f ? static_cast<double>(maxext) / std::cbrt(static_cast<double>(n)) : 1.0;
   // a cell size that already fitted a cloud of the same scene is a better start than the 3-D
-  // guess: this cloud's previous grid, else (source) the target's, scaled as a surface (sqrt n)
+  // guess: this cloud's previous grid, else (source) the target's, scaled as a surface (sqrt n).
+  // The source's grid -- its sorted order, so the fixed reduction tree of every objective pass --
+  // therefore follows the target's: measured r05, a source grid sized on its own (a surface guess)
+  // flips one BFGS line-search decision at C4F (4 iterations against the oracle's 3, frob 7.7e-3):
+  // the restated bfgs.h trajectory is a knife-edge (DESIGN.md "Oracle uncertainty ledger")
   if (cl.view.h > 0.f && cl.n_built > 0)
     h = static_cast<double>(cl.view.h) * std::sqrt(static_cast<double>(cl.n_built) / n);
   else if (&cl == &ctx->src && ctx->tgt.view.h > 0.f && ctx->tgt.n_built > 0)
@@ -1092,6 +1101,10 @@ int compute_cov(mgicp_ctx* ctx, Cloud& cl, size_t p0, size_t p1, size_t stride =
                    "pieces %.1f, block candidates mean lane %.1f busiest lane %.1f | lanes past the block %llu, hand-offs %llu "
                    "of %llu\n", ph[0], ph[1], ph[4], ph[5], double(ph[2]) / ph[0], double(ph[3]) / ph[0],
                    double(ph[6]) / ph[0] / 64.0, double(ph[7]) / ph[0], ph[8], ph[9], ph[10]);
+    if (ph[0] && ph[1] && ph[0] > ph[1])
+      std::fprintf(stderr, "[knnb] cycles per wave -- staged: setup %.0f, copy %.0f, passes %.0f | unstaged: setup %.0f, "
+                   "passes %.0f\n", double(ph[11]) / ph[1], double(ph[12]) / ph[1], double(ph[13]) / ph[1],
+                   double(ph[15]) / (ph[0] - ph[1]), double(ph[16]) / (ph[0] - ph[1]));
     const double w = ph[21] ? static_cast<double>(ph[21]) : 1.0;
     std::fprintf(stderr, "[knn-div] waves %llu | per wave: test iterations %.1f, max lane tests %.1f, mean lane tests %.1f"
                  " | cycles/wave search %.0f, moments + finish %.0f\n",
@@ -1138,9 +1151,10 @@ int prepare(mgicp_ctx* ctx, bool need_cov) {
   int rc;
   if (ctx->tgt.dirty && (rc = build_grid(ctx, ctx->tgt))) return rc;
   if (ctx->src.dirty && (rc = build_grid(ctx, ctx->src))) return rc;
-  if ((rc = cov_join(ctx, true))) return rc;  // set_target's covariances (after the source grid: overlapped)
   if (!need_cov) return MGICP_OK;
-  if (!ctx->tgt.have_cov && (rc = target_cov(ctx))) return rc;
+  // set_target's covariances still running count as current: the first sweep runs beside them and
+  // joins them before its compaction (r05: the 1-NN search needs no covariance)
+  if (!ctx->tgt.have_cov && !ctx->tgt_cov_pending && (rc = target_cov(ctx))) return rc;
   // set_source's covariances still running count as current: the sweep joins them (overlapped)
   const bool src_cur = ctx->src_cov_pending ||
                        (ctx->src.have_cov && ctx->src.cov_p0 == ctx->shard_p0() && ctx->src.cov_p1 == ctx->shard_p1());
@@ -1759,7 +1773,7 @@ int correspond(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
   }
 #endif
   {
-    int rc = cov_join(ctx, false);  // set_source's covariances (they ran beside this sweep)
+    int rc = cov_join_all(ctx);  // set_target's / set_source's covariances (they ran beside this sweep)
     if (rc) return rc;
     rc = cov_lazy(ctx);  // covariances of newly accepted source points (lazy source mode)
     MGICP_TRACE_AT("corr: lazy covariances queued (sweep drained)");
@@ -2093,7 +2107,7 @@ int correspond_gn(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
   }
   ctx->seed_valid = true;
   ctx->have_corr = false;  // the SoA streams of the BFGS mode are not refreshed
-  int rc = cov_join(ctx, false);
+  int rc = cov_join_all(ctx);
   if (rc) return rc;
   if ((rc = cov_lazy(ctx))) return rc;
   return moments_pass(ctx, T, G);

@@ -22,7 +22,11 @@
 #define MGICP_CORR_WAVES 8  // resident waves per SIMD requested for the 1-NN kernel (64 VGPRs; A/B profiles/r01/ab_w8)
 #endif
 #ifndef MGICP_KNN_BLK
-#define MGICP_KNN_BLK 1  // k-NN covariances: 1 = wave-staged knn_blk_kernel (r05), 0 = knn_cov2_kernel (r02-r04)
+#define MGICP_KNN_BLK 0  // k-NN covariances: 0 = knn_cov2_kernel (r02-r05, default), 1 = the wave-staged knn_blk_kernel
+                         // (r05 experiment, measured slower: DESIGN.md "k-NN covariances")
+#endif
+#ifndef MGICP_KNNB_DIAG
+#define MGICP_KNNB_DIAG 0  // diagnostic builds: 1 = no eigen-decomposition, 2 = pass 1 only
 #endif
 #ifndef MGICP_KNNB_STATS
 #define MGICP_KNNB_STATS 0  // 1 (with MGICP_CORR_PHASES): knn_blk_kernel staging / search counters (diagnostic)
@@ -1124,7 +1128,14 @@ __global__ __launch_bounds__(64, MGICP_KNN_MINW) void knn_cov2_kernel(GridView g
   if (ok_out) ok_out[p] = 1;  // computed here or by the hand-off launch
 }
 
-// ---- wave-staged k-NN covariances (r05, default) -----------------------------------------------
+#if MGICP_KNN_BLK
+// ---- wave-staged k-NN covariances (r05 experiment; MGICP_KNN_BLK=1 builds only) -----------------
+// Measured at C4 (5M target, knn_time.py, profiles/r05/knn*): 2.0-2.1 ms per cloud against 1.85-1.92 ms
+// for knn_cov2_kernel -- bit-identical covariances (the GPU suite passes with it), but not faster:
+// 64 grid-consecutive points span several surface crossings, so a wave's union of 3x3x3 blocks holds
+// ~385 points (26 % of the waves exceed a 448-point copy), pass 1 alone (staging + the med3 network
+// over ~99 unpruned candidates per lane) costs 1.58 ms, and the 14.8 KB of LDS per wave caps the
+// kernel at 2.5 waves per SIMD.  Kept as the record of the attempt.
 // knn_cov2_kernel runs one ring search per lane over global memory: a dependent round trip per row
 // bound and per batch of a row's points, ~20-50 per query, and only 42 % of wave cycles issue
 // (VERDICT r04 weak 3).  Here the 64 grid-consecutive queries of a wave first stage the points of the
@@ -1279,6 +1290,19 @@ __device__ __forceinline__ void knn_blk_search(const GridView& g, const float4& 
                                                TauLog& lg) {
   v1.init(q.x, q.y, q.z, nsent);
   if (ring_cap >= 0) v1.ring_cap = ring_cap;
+  if constexpr (!kLds) {
+    // a wave whose union does not fit the LDS copy: the per-lane ring search over global memory (near
+    // rows first, row pruning by the shrinking k-th distance), then pass 2 with tau fixed
+    if (live) ring_search(g, q.x, q.y, q.z, v1, 0);
+    lg.qx = q.x; lg.qy = q.y; lg.qz = q.z;
+    lg.tau = v1.key[K - 1];
+    lg.log = lg_lane;
+    lg.cnt = 0;
+    lg.cap = K + kKnbLogExtra;
+    if (live && !v1.gave_up) ring_search(g, q.x, q.y, q.z, lg, 0);
+    v1.nrange = 1;
+    return;
+  }
   auto t1 = [&](const float4& pt, uint32_t) { v1.test(dist2(q.x, q.y, q.z, pt)); };
   blk_interval<kLds>(g.pts, lp, m0, m1, delta[4], t1);
   blk_interval<kLds>(g.pts, lp, s[4], m0, delta[4], t1);
@@ -1360,6 +1384,9 @@ __global__ __launch_bounds__(64, MGICP_KNNB_MINW) void knn_blk_kernel(GridView g
   const size_t t = static_cast<size_t>(blockIdx.x) * 64 + lane;
   const bool live = t < p1 - p0;
   const size_t p = p0 + (live ? (perm ? perm[t] : t) : 0);
+#if MGICP_KNNB_STATS
+  const unsigned long long kt0 = __builtin_amdgcn_s_memtime();
+#endif
   const float4 q = g.pts[p];
   const int cx = qcell(q.x, g.ox, g.inv_h), cy = qcell(q.y, g.oy, g.inv_h), cz = qcell(q.z, g.oz, g.inv_h);
   const bool blk = live && cx >= 0 && cx < g.nx && cy >= 0 && cy < g.ny && cz >= 0 && cz < g.nz;
@@ -1426,8 +1453,12 @@ __global__ __launch_bounds__(64, MGICP_KNNB_MINW) void knn_blk_kernel(GridView g
   const bool stage = __builtin_amdgcn_ballot_w64(!mono) == 0ull && base <= static_cast<uint32_t>(kKnbCap) &&
                      npc <= static_cast<uint32_t>(kKnbPieces);
 #if MGICP_KNNB_STATS
-  {  // [0] waves [1] staged [2] union points [3] pieces [4] non-monotone waves [5] over the cap
-     // [6] lane block candidates (sum) [7] busiest lane's block candidates (sum over waves)
+  // [0] waves [1] staged [2] union points [3] pieces [4] non-monotone waves [5] over the cap
+  // [6] lane block candidates (sum) [7] busiest lane's block candidates (sum over waves); the atomics
+  // are issued at the end of the kernel (an atomic in flight would be waited on by the next load)
+  unsigned long long st_bs = 0;
+  uint32_t st_bm = 0;
+  {
     uint32_t bc = 0;
 #pragma unroll
     for (int o = 0; o < 9; ++o) bc += e[o] - s[o];
@@ -1438,21 +1469,18 @@ __global__ __launch_bounds__(64, MGICP_KNNB_MINW) void knn_blk_kernel(GridView g
       bm = max(bm, static_cast<uint32_t>(__shfl_xor(static_cast<int>(bm), off, 64)));
       bs += __shfl_xor(bs, off, 64);
     }
-    if (lane == 0) {
-      atomicAdd(&g_corr_phase[0], 1ull);
-      atomicAdd(&g_corr_phase[1], stage ? 1ull : 0ull);
-      atomicAdd(&g_corr_phase[2], static_cast<unsigned long long>(base));
-      atomicAdd(&g_corr_phase[3], static_cast<unsigned long long>(npc));
-      atomicAdd(&g_corr_phase[4], __builtin_amdgcn_ballot_w64(!mono) ? 1ull : 0ull);
-      atomicAdd(&g_corr_phase[5], base > static_cast<uint32_t>(kKnbCap) ? 1ull : 0ull);
-      atomicAdd(&g_corr_phase[6], bs);
-      atomicAdd(&g_corr_phase[7], static_cast<unsigned long long>(bm));
-    }
+    st_bs = bs;
+    st_bm = bm;
   }
+  const bool st_nonmono = __builtin_amdgcn_ballot_w64(!mono) != 0ull;
 #endif
   KthList<K> v1;
   TauLog lg;
   uint32_t* lg_lane = s_log + lane;
+#if MGICP_KNNB_STATS
+  const unsigned long long kt1 = __builtin_amdgcn_s_memtime();
+  unsigned long long kt2 = kt1;
+#endif
   if (stage) {
     __syncthreads();  // the piece table
     // element i = lane + 64 u of the copy: its piece (binary search over the LDS starts)
@@ -1476,11 +1504,22 @@ __global__ __launch_bounds__(64, MGICP_KNNB_MINW) void knn_blk_kernel(GridView g
       if (i < base) s_pts[i] = buf[u];
     }
     __syncthreads();
+#if MGICP_KNNB_STATS
+    kt2 = __builtin_amdgcn_s_memtime();
+#endif
     knn_blk_search<K, true>(g, q, cy, cz, live, blk, s, e, m0, m1, delta, s_pts, lg_lane, nsent, ring_cap, v1, lg);
   } else {
     knn_blk_search<K, false>(g, q, cy, cz, live, blk, s, e, m0, m1, delta, s_pts, lg_lane, nsent, ring_cap, v1, lg);
   }
+#if MGICP_KNNB_STATS
+  const unsigned long long kt3 = __builtin_amdgcn_s_memtime();
+#endif
   if (!live || v1.gave_up) return;  // gave up: the lazy pass computes it if a sweep accepts it
+#if MGICP_KNNB_DIAG == 2  // diagnostic: pass 1 only (tau stored)
+  cov.a[p] = make_double2(static_cast<double>(lg.tau), 0.0);
+  if (ok_out) ok_out[p] = 1;
+  return;
+#endif
   const int kreal = K - nsent;
   const int cnt = lg.cnt;
   bool ok = cnt == kreal;  // (<= K, within the log)
@@ -1522,14 +1561,36 @@ __global__ __launch_bounds__(64, MGICP_KNNB_MINW) void knn_blk_kernel(GridView g
       }
     }
     ok = c0.ok() && c1.ok() && c2.ok() && c00.ok() && c10.ok() && c11.ok() && c20.ok() && c21.ok() && c22.ok();
+#if MGICP_KNNB_DIAG == 1  // diagnostic: no eigen-decomposition (the raw sums are stored)
+    if (ok) {
+      cov.a[p] = make_double2(m0d, a[0][0]);
+      cov.b[p] = make_double2(m1d, a[1][1]);
+      cov.c[p] = make_double2(m2d, a[2][2]);
+    }
+#else
     if (ok) cov_finish(m0d, m1d, m2d, a, static_cast<double>(kreal), eps, cov, p);
+#endif
   }
 #if MGICP_KNNB_STATS
-  {  // [8] lanes past the block (rings >= 2) [9] hand-offs [10] live lanes
+  {  // [8] lanes past the block (rings >= 2) [9] hand-offs [10] live lanes; shader cycles per wave
+     // [11] setup, [12] staging copy, [13] passes 1-2 of staged waves, [15] setup, [16] passes of the others
     const unsigned long long pm = __builtin_amdgcn_ballot_w64(v1.nrange > 0 || !blk);
     const unsigned long long hm = __builtin_amdgcn_ballot_w64(!ok);
     const unsigned long long lm = __builtin_amdgcn_ballot_w64(true);
     if (lane == __builtin_ctzll(lm)) {
+      if (lane == 0) {
+        atomicAdd(&g_corr_phase[0], 1ull);
+        atomicAdd(&g_corr_phase[1], stage ? 1ull : 0ull);
+        atomicAdd(&g_corr_phase[2], static_cast<unsigned long long>(base));
+        atomicAdd(&g_corr_phase[3], static_cast<unsigned long long>(npc));
+        atomicAdd(&g_corr_phase[4], st_nonmono ? 1ull : 0ull);
+        atomicAdd(&g_corr_phase[5], base > static_cast<uint32_t>(kKnbCap) ? 1ull : 0ull);
+        atomicAdd(&g_corr_phase[6], st_bs);
+        atomicAdd(&g_corr_phase[7], static_cast<unsigned long long>(st_bm));
+        atomicAdd(&g_corr_phase[stage ? 11 : 15], kt1 - kt0);
+        if (stage) atomicAdd(&g_corr_phase[12], kt2 - kt1);
+        atomicAdd(&g_corr_phase[stage ? 13 : 16], kt3 - kt2);
+      }
       atomicAdd(&g_corr_phase[8], static_cast<unsigned long long>(__builtin_popcountll(pm)));
       atomicAdd(&g_corr_phase[9], static_cast<unsigned long long>(__builtin_popcountll(hm)));
       atomicAdd(&g_corr_phase[10], static_cast<unsigned long long>(__builtin_popcountll(lm)));
@@ -1540,6 +1601,8 @@ __global__ __launch_bounds__(64, MGICP_KNNB_MINW) void knn_blk_kernel(GridView g
   if (!ok) fb[atomicAdd(fb_count, 1u)] = static_cast<uint32_t>(p);
   if (ok_out) ok_out[p] = 1;
 }
+
+#endif  // MGICP_KNN_BLK
 
 // ------------------------------------------------------------------------------------
 // correspondence + Mahalanobis

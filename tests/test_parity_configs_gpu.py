@@ -46,14 +46,34 @@ CONFIGS = {
 }
 
 
-def _run_pair(name):
+_ORACLE = {}
+
+
+def _clouds_and_oracle(name):
+    """the config's clouds and the oracle's align on them (cached: C4F serves two tests)"""
+    if name in _ORACLE:
+        return _ORACLE[name]
     from leica_point_cloud_processing_amd import synth
-    from leica_point_cloud_processing_amd.engine import GICPEngine
     from oracle import ref
 
+    _ORACLE.clear()  # one config's clouds at a time (C5: 25M points)
     c = CONFIGS[name]
     scan, cad, T_true = synth.scan_vs_cad(c["n"], c["nt"], occlusion=c["occlusion"], clutter=c.get("clutter", 0.0),
                                           debris=c.get("debris", 0))
+    o = ref.RefGICP(max_iterations=c["max_iter"], fixed_iterations=c["fixed"], threads=ORACLE_THREADS)
+    o.set_source(scan)
+    o.set_target(cad)
+    with heartbeat(f"oracle {name}"):
+        T_ref, info = o.align(want_trace=True)
+    _ORACLE[name] = (scan, cad, T_true, T_ref, info)
+    return _ORACLE[name]
+
+
+def _run_pair(name):
+    from leica_point_cloud_processing_amd.engine import GICPEngine
+
+    c = CONFIGS[name]
+    scan, cad, T_true, T_ref, info = _clouds_and_oracle(name)
     e = GICPEngine(max_iter=c["max_iter"], fixed_iterations=int(c["fixed"]))
     e.set_source_xyz(scan)
     e.set_target_xyz(cad)
@@ -62,11 +82,6 @@ def _run_pair(name):
     res = dict(e.last_result)
     conv = e.hasConverged()
     e.close()
-    o = ref.RefGICP(max_iterations=c["max_iter"], fixed_iterations=c["fixed"], threads=ORACLE_THREADS)
-    o.set_source(scan)
-    o.set_target(cad)
-    with heartbeat(f"oracle {name}"):
-        T_ref, info = o.align(want_trace=True)
     return T_gpu, tr_gpu, res, conv, T_ref, info, T_true
 
 
@@ -94,6 +109,43 @@ def test_config_final_transform_vs_oracle(name):
     assert err <= FROB_TOL
     # the synthetic perturbation is recovered to PCL's stopping accuracy
     assert np.abs(T_gpu.astype(np.float64) @ T_true - np.eye(4)).max() < 0.05
+
+
+def test_c4f_steady_state_cell_lists_vs_oracle():
+    """the production path at full size -- the target's 1-NN cell lists with the
+    fused compaction, which the bench's timed aligns run -- against the oracle.  Five aligns on one
+    engine at C4F (gate rejections): aligns 1-2 run the cold sweep, 3-4 build the lists, 5 finds
+    them built; every align's T, iterations and last-sweep correspondence count equal the oracle's,
+    and a sweep at the final T through the lists equals the cold sweep's (debug option "vlist" 0)
+    index for index and matrix for matrix."""
+    from leica_point_cloud_processing_amd.engine import GICPEngine
+
+    c = CONFIGS["C4F"]
+    scan, cad, _, T_ref, info = _clouds_and_oracle("C4F")
+    e = GICPEngine(max_iter=c["max_iter"])
+    e.set_source_xyz(scan)
+    e.set_target_xyz(cad)
+    for k in range(5):
+        T = e.align()
+        r = e.last_result
+        err = frob(T, T_ref)
+        print(f"C4F align {k + 1}: iterations {r['iterations']} (oracle {info['iterations']}), n_corr {r['n_corr']} "
+              f"(oracle {info['n_corr_last']}), frob {err:.3e}, lists {e.vlist_stats()['lists']}")
+        assert r["iterations"] == info["iterations"] and r["n_corr"] == info["n_corr_last"]
+        assert err <= FROB_TOL
+    st = e.vlist_stats()
+    print("C4F lists after five aligns:", st)
+    assert st["lists"] > 0 and st["requested"] <= 0.001 * len(scan), st  # the fifth align ran on built lists
+    m, tj, M = e.debug_correspondences(T_ref.astype(np.float32), len(scan))
+    e0 = GICPEngine(max_iter=c["max_iter"], options={"vlist": 0})
+    e0.set_source_xyz(scan)
+    e0.set_target_xyz(cad)
+    m0, tj0, M0 = e0.debug_correspondences(T_ref.astype(np.float32), len(scan))
+    assert m == m0 and m < len(scan)
+    np.testing.assert_array_equal(tj, tj0)
+    np.testing.assert_array_equal(M, M0)
+    e.close()
+    e0.close()
 
 
 def test_state_machine_identical_clouds_known_answer():
