@@ -9,9 +9,10 @@ GICPAlignment::iterate(), /root/reference/src/GICPAlignment.cpp:111-121) over cl
 in HBM whose grids and covariances are cached (the first align, in warmup, builds them and is
 reported separately as ms_to_converge_first).  value = outer GICP iterations of all timed
 steps / timed seconds.  With N GPUs the same 5M <-> 5M problem is sharded by source point
-ranges (strong scaling); every rank runs the resident pass server and the per-pass sums travel
-through a node-wide shared-memory segment of super rows (--transport shm, default) or one RCCL
-all-gather per pass (--transport rccl).
+ranges (strong scaling); every rank runs the resident pass server and the per-pass super rows go
+into every rank's IPC-mapped device buffer over xGMI, where a totaler wave per rank takes the
+fixed-order total (--transport xgmi, default, r05), or through a node-wide shared-memory segment
+that every host totals (--transport shm), or one RCCL all-gather per pass (--transport rccl).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--n-source S] [--n-target T]
        (N > 1: this script starts its own N ranks, or runs under torch.distributed.run)
@@ -97,9 +98,10 @@ def parse():
     ap.add_argument("--c5-leg", type=int, default=1,
                     help="C4 only: the in-align pass roofline at C5 (20M scan: the streams exceed the 256 MiB "
                          "Infinity Cache) measured in this run (0 = skip)")
-    ap.add_argument("--transport", default="shm", choices=["shm", "rccl"],
-                    help="N > 1: per-pass sums through the node-wide shared row segment (resident pass "
-                         "server on every rank, no collective per pass) or one RCCL all-gather per pass")
+    ap.add_argument("--transport", default="xgmi", choices=["xgmi", "shm", "rccl"],
+                    help="N > 1: per-pass super rows into every rank's IPC-mapped device buffer over xGMI with a "
+                         "totaler wave per rank (r05 default), or through the node-wide shared host segment "
+                         "(every host totals), or one RCCL all-gather per pass")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
     args.n_source = args.n_source or cfg["n_source"]
@@ -326,7 +328,7 @@ def main():
         uid = pg.broadcast(GICPEngine.unique_id() if rank == 0 else None)
         eng.comm_init(world, rank, uid)
         transport = "rccl"
-        if args.transport == "shm":
+        if args.transport in ("shm", "xgmi"):
             # the node-wide row segment: every rank's resident server writes its supers there, every
             # host takes the fixed-order total (no collective per pass); RCCL keeps the one-time
             # target-covariance all-gather.  Any rank failing to attach -> every rank stays on RCCL.
@@ -344,6 +346,20 @@ def main():
                 transport = f"rccl (shared segment unavailable: {err or 'on another rank'})"
             else:
                 transport = "shm rows + rccl (target covariances)"
+                if args.transport == "xgmi":
+                    # the rows over xGMI (the segment stays as its rendezvous and for the once-per-iteration
+                    # gathers); any rank failing -> every rank keeps the host segment
+                    xerr = None
+                    try:
+                        eng.attach_xgmi()
+                    except Exception as exc:  # noqa: BLE001 -- reported in the JSON line
+                        xerr = str(exc)
+                    if pg.allreduce_max(1.0 if xerr else 0.0) > 0:
+                        if not xerr:
+                            eng.attach_xgmi(False)
+                        transport = f"shm rows (xGMI exchange unavailable: {xerr or 'on another rank'}) + rccl"
+                    else:
+                        transport = "xGMI row exchange + device totals; shm rendezvous/gathers; rccl (target covariances)"
     eng.set_source_xyz(scan)
     eng.set_target_xyz(cad)
 

@@ -174,6 +174,15 @@ int mgicp_comm_init(mgicp_ctx* ctx, int nranks, int rank, const unsigned char id
  * run the same sequence of align / fitness calls.  MGICP_E_COMM: segment or peers unavailable (the
  * context keeps its previous transport).  name = NULL detaches (back to RCCL / local). */
 int mgicp_comm_attach_shm(mgicp_ctx* ctx, const char* name, size_t max_source_points);
+/* r05: per-pass super rows over xGMI instead of host memory (needs mgicp_comm_attach_shm first: the
+ * segment carries the IPC rendezvous; every rank calls this in the same sequence).  on = 1: this rank
+ * allocates a device exchange buffer, publishes its IPC handle and opens every other rank's; from then
+ * on the resident server's super reducers store each row into every rank's buffer (peer device memory,
+ * xGMI) and a one-wave totaler per rank takes the fixed-order total on the device -- the host reads one
+ * 32-word row per pass instead of every rank's rows.  Sums, iterations and T stay bitwise those of one
+ * GPU.  The server leaves one CU to the totaler; a pass that cannot run on the server (another context
+ * holds the device's server slot, profiling) returns MGICP_E_COMM.  on = 0 detaches. */
+int mgicp_comm_attach_xgmi(mgicp_ctx* ctx, int on);
 
 /* ---- introspection for parity tests (original point order) ---- */
 /* covariances of the source (which = 0) or target (which = 1): n x {c00,c01,c02,c11,c12,c22} */

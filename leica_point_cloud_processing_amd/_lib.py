@@ -91,6 +91,7 @@ _SIGNATURES = {
     "mgicp_get_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
     "mgicp_comm_init": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]),
     "mgicp_comm_attach_shm": (ctypes.c_int, [_P, ctypes.c_char_p, _SZ]),
+    "mgicp_comm_attach_xgmi": (ctypes.c_int, [_P, ctypes.c_int]),
     "mgicp_debug_pass_stats": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_longlong)]),
     "mgicp_debug_server_time": (ctypes.c_int, [_P, _DP, ctypes.POINTER(ctypes.c_longlong),
                                                ctypes.POINTER(ctypes.c_longlong), ctypes.c_int]),

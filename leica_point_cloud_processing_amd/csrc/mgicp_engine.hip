@@ -266,7 +266,8 @@ enum {
   kStTakeover,       // server passes that missed their deadline and were re-run as launched passes
   kStBar,            // 1: the server reads its commands from device memory written through the BAR
   kStRowsAlloc,      // private host-row buffer allocations
-  kStTransport,      // 0 local, 1 RCCL, 2 shared segment, 3 shared segment + RCCL (bulk all-gathers)
+  kStTransport,      // 0 local, 1 RCCL, 2 shared segment, 3 shared segment + RCCL (bulk all-gathers),
+                     // 4 xGMI row exchange (+ segment), 5 xGMI row exchange + RCCL
   kStSrvDenied,      // server launches refused because another context of this process held the device
   kStCount
 };
@@ -410,6 +411,20 @@ struct mgicp_ctx {
   // node-wide transport (mgicp_comm_attach_shm)
   bool have_shm = false;
   shm::Segment shm;
+  // r05 xGMI row exchange (mgicp_comm_attach_xgmi, needs the segment for its rendezvous): every rank's
+  // super reducers store their rows into this rank's exchange buffer (xrows: 2 parity buffers of
+  // max_sup rows, device memory) and into every other rank's, mapped by IPC over xGMI; a one-wave
+  // totaler per rank takes the fixed-order total on the device and stores it as one stamped host row
+  bool have_xgmi = false;
+  DevBuf<unsigned long long> xrows;
+  std::vector<void*> xpeer;               // the other ranks' exchange buffers (IPC mappings), rank order
+  unsigned long long* h_xtot = nullptr;   // the totaler's stamped row (32 words; host / device views)
+  unsigned long long* d_xtot = nullptr;
+  unsigned int* h_xgen = nullptr;         // generation word: a totaler exits when it changes
+  unsigned int* d_xgen = nullptr;
+  unsigned int xgen = 0;
+  unsigned long long xseq = 0;            // attaches so far (the segment's publication flag value)
+  hipStream_t xstream = nullptr;
   unsigned char* shm_d = nullptr;       // device view of the segment (hipHostRegister'ed)
   long long st[kStCount] = {};          // pass-path counters
   // the resident server as the aligns run it (mgicp_debug_server_time): two events per launch
@@ -606,10 +621,27 @@ void publish_cmd(mgicp_ctx* ctx, unsigned long long seq, unsigned int op, int re
   for (int i = 0; i < kCmdWords; ++i) __atomic_store_n(&ctx->h_cmd->h[i], stamp | w[i], __ATOMIC_RELEASE);
 }
 
+// r05 xGMI: end the running totaler (if any) -- it exits when the generation word changes
+void xgmi_cancel(mgicp_ctx* ctx) {
+  if (ctx->have_xgmi && ctx->h_xgen) __atomic_store_n(ctx->h_xgen, ++ctx->xgen, __ATOMIC_RELEASE);
+}
+
+// r05: drop the xGMI row exchange (stream drained first: no totaler, no server writes into it)
+void xgmi_detach(mgicp_ctx* ctx) {
+  if (!ctx->have_xgmi) return;
+  xgmi_cancel(ctx);
+  if (ctx->xstream) (void)hipStreamSynchronize(ctx->xstream);
+  for (void* p : ctx->xpeer) (void)hipIpcCloseMemHandle(p);
+  ctx->xpeer.clear();
+  ctx->xrows.release();
+  ctx->have_xgmi = false;
+}
+
 // release a queued gated pass (or the resident server) without running it (end of a BFGS run,
 // any stream drain)
 void cancel_gated(mgicp_ctx* ctx) {
   if (ctx->srv_live) {
+    xgmi_cancel(ctx);
     publish_cmd(ctx, ctx->srv_next, kPassCancel, 0, nullptr);
     ctx->pass_seq = std::max(ctx->pass_seq, ctx->srv_next);  // its sequence number is spent
     ctx->srv_live = false;
@@ -670,6 +702,12 @@ int reset_stamps(mgicp_ctx* ctx) {
     HIPCK(hipStreamSynchronize(ctx->stream));
   }
   if (ctx->h_rows) std::memset(ctx->h_rows, 0, 2 * ctx->rows_cap * shm::kRowWords * sizeof(unsigned long long));
+  if (ctx->have_xgmi) {  // stamps restart: no stale row of the exchange buffer may validate
+    if (ctx->xstream) HIPCK(hipStreamSynchronize(ctx->xstream));
+    HIPCK(hipMemsetAsync(ctx->xrows.p, 0, ctx->xrows.cap * sizeof(unsigned long long), ctx->stream));
+    HIPCK(hipStreamSynchronize(ctx->stream));
+    std::memset(ctx->h_xtot, 0, shm::kRowWords * sizeof(unsigned long long));
+  }
   ctx->pass_idx = 0;
   ctx->gather_idx = 0;
   return MGICP_OK;
@@ -1422,6 +1460,18 @@ int wait_rows(mgicp_ctx* ctx, unsigned int rstamp, const Xf34& A, double out[kRe
   return MGICP_OK;
 }
 
+// r05 xGMI: the pass total the rank's totaler stored (every rank's rows arrived in its buffer)
+int wait_xtot(mgicp_ctx* ctx, unsigned int rstamp, double out[kRedVals]) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const uint64_t* row = reinterpret_cast<const uint64_t*>(ctx->h_xtot);
+  for (unsigned spins = 0; !shm::row_complete(row, rstamp); ++spins) {
+    if ((spins & 1023u) == 1023u && shm::elapsed_s(t0) > ctx->remote_deadline_s)
+      return fail(ctx, MGICP_E_COMM, "xGMI row exchange: the pass total did not complete (a rank stopped publishing)");
+  }
+  shm::row_decode(row, out);
+  return MGICP_OK;
+}
+
 int ensure_iter_buffers(mgicp_ctx* ctx) {
   const size_t ns = ctx->shard_p1() - ctx->shard_p0();
   const size_t nch = static_cast<size_t>(chunk_count(ns));
@@ -1832,7 +1882,8 @@ struct DeviceFunctor {
     const CorrSoA c = corr_soa(ctx);
     const bool want_srv = ctx->resident && !ctx->srv_degraded && !ctx->profiling && !ctx->fdf_diag &&
                           (gate || (shm_rows && ctx->poll));
-    const int cap = ctx->srv_cus > 0 ? std::min(ctx->srv_cus, ctx->cus) : ctx->cus;
+    int cap = ctx->srv_cus > 0 ? std::min(ctx->srv_cus, ctx->cus) : ctx->cus;
+    if (ctx->have_xgmi) cap = std::min(cap, ctx->cus - 1);  // one CU left to the totaler wave
     int nsrv = want_srv ? fdf_server_blocks(ns, cap, ctx->srv_waves) : 0;
     // the host rows first: a failure here (e.g. a source larger than the shared segment) must not
     // leave the device's server slot taken
@@ -1846,12 +1897,25 @@ struct DeviceFunctor {
       }
     }
     const bool rows = shm_rows || (nsrv > 0 && ctx->host_rows);
+    const bool xg = ctx->have_xgmi;
+    if (xg && nsrv <= 0)
+      return fail(ctx, MGICP_E_COMM, "xGMI row exchange needs the resident pass server on every rank (the device's "
+                                     "server slot is held by another context, or profiling is on)");
     if (nsrv > 0) {
       // the resident server runs every pass of this BFGS run: start it with the first one
       if (!ctx->srv_live) {
         cancel_gated(ctx);
         ctx->ht_last_rows = 0;  // host-view diagnostics: a new BFGS run, not a host step
         const RowView rv = row_view(ctx);
+        // xGMI: rows into this rank's exchange buffer and every peer's, at the global super index
+        PeerRows pr{};
+        unsigned long long* xr = nullptr;
+        if (xg) {
+          xr = ctx->xrows.p + static_cast<size_t>(rv.first) * shm::kRowWords;
+          pr.n = static_cast<int>(ctx->xpeer.size());
+          for (int r = 0; r < pr.n; ++r)
+            pr.p[r] = static_cast<unsigned long long*>(ctx->xpeer[r]) + static_cast<size_t>(rv.first) * shm::kRowWords;
+        }
         hipEvent_t ea = ev_get(ctx);
         hipError_t e = hipEventRecord(ea, ctx->stream);
         if (e == hipSuccess) e = hipMemsetAsync(ctx->tickets.p, 0, ctx->tickets_n * sizeof(unsigned int), ctx->stream);
@@ -1860,9 +1924,16 @@ struct DeviceFunctor {
           if (e == hipSuccess)
             e = launch_fdf_server(c, ctx->ccnt.p, ns, ctx->partial.p, ctx->spart.p, ctx->tickets.p,
                                   out, ctx->d_flag, seq, ctx->bar_cmd ? ctx->bar_cmd : ctx->d_cmd, ctx->mail,
-                                  ctx->gate_timeout, ctx->d_ptimes, 0, Ax, rows ? rv.dev_rows(0) : nullptr, rv.stride,
-                                  nsrv, ctx->srv_waves, ctx->bar_cmd ? nsrv : 1, ctx->stall_pass,
-                                  ctx->srv_tagged ? ctx->tpart.p : nullptr, ctx->stream);
+                                  ctx->gate_timeout, ctx->d_ptimes, 0, Ax, xg ? xr : (rows ? rv.dev_rows(0) : nullptr),
+                                  rv.stride, nsrv, ctx->srv_waves, ctx->bar_cmd ? nsrv : 1, ctx->stall_pass,
+                                  ctx->srv_tagged ? ctx->tpart.p : nullptr, ctx->stream, xg ? &pr : nullptr);
+          // the totaler of this BFGS run (its own stream; exits on the generation change of the cancel)
+          if (e == hipSuccess && xg) {
+            const unsigned int gen = ++ctx->xgen;
+            __atomic_store_n(ctx->h_xgen, gen, __ATOMIC_RELEASE);
+            e = launch_xgmi_total(ctx->xrows.p, rv.stride, rv.ntot, rstamp, ctx->d_xtot, ctx->d_xgen, gen,
+                                  ctx->gate_timeout, ctx->xstream);
+          }
         }
         hipEvent_t eb = nullptr;
         if (e == hipSuccess) {
@@ -1891,7 +1962,9 @@ struct DeviceFunctor {
       publish_cmd(ctx, seq, kPassRun, 0, &Ax, rstamp);
       ctx->srv_next = seq + 1;
       ctx->st[kStSrvPass]++;
-      if (rows) {
+      if (xg) {
+        if ((rc = wait_xtot(ctx, rstamp, sums))) return rc;
+      } else if (rows) {
         if ((rc = wait_rows(ctx, rstamp, Ax, sums, true))) return rc;
         if (ctx->h_ptimes) {
           ctx->ht_last_rows = now_ms();
@@ -2323,6 +2396,9 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   if (ctx->h_gtrace) (void)hipHostFree(ctx->h_gtrace);
   if (ctx->h_ptimes) (void)hipHostFree(ctx->h_ptimes);
   if (ctx->h_rows) (void)hipHostFree(ctx->h_rows);
+  xgmi_detach(ctx);
+  if (ctx->xstream) (void)hipStreamDestroy(ctx->xstream);
+  if (ctx->h_xtot) (void)hipHostFree(ctx->h_xtot);
   if (ctx->have_shm) {
     (void)hipHostUnregister(ctx->shm.base);
     shm::detach(ctx->shm);
@@ -2840,6 +2916,62 @@ int mgicp_comm_init(mgicp_ctx* ctx, int nranks, int rank, const unsigned char id
   return MGICP_OK;
 }
 
+int mgicp_comm_attach_xgmi(mgicp_ctx* ctx, int on) {
+  if (!ctx) return MGICP_E_INVALID;
+  HIPCK(hipSetDevice(ctx->device));
+  int rc = cov_join_all(ctx);
+  if (rc || (rc = sync(ctx))) return rc;
+  xgmi_detach(ctx);
+  if (!on) return reset_stamps(ctx);
+  if (!ctx->have_shm)
+    return fail(ctx, MGICP_E_INVALID, "xGMI row exchange: attach the shared segment first (its rendezvous)");
+  if (ctx->nranks - 1 > kMaxPeers) return fail(ctx, MGICP_E_INVALID, "xGMI row exchange: at most 9 ranks");
+  // host words of the totaler (pinned, mapped) and its stream, once per context
+  if (!ctx->h_xtot) {
+    HIPCK(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_xtot), shm::kRowWords * sizeof(unsigned long long) + 64,
+                        hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCK(hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->d_xtot), ctx->h_xtot, 0));
+    std::memset(ctx->h_xtot, 0, shm::kRowWords * sizeof(unsigned long long) + 64);
+    ctx->h_xgen = reinterpret_cast<unsigned int*>(ctx->h_xtot + shm::kRowWords);
+    ctx->d_xgen = reinterpret_cast<unsigned int*>(ctx->d_xtot + shm::kRowWords);
+  }
+  if (!ctx->xstream) HIPCK(hipStreamCreateWithFlags(&ctx->xstream, hipStreamNonBlocking));
+  // this rank's exchange buffer, zeroed (stamp 0 is never a pass stamp), published by IPC handle
+  const size_t words = 2 * static_cast<size_t>(ctx->shm.max_sup) * shm::kRowWords;
+  HIPCK(ctx->xrows.reserve(words));
+  HIPCK(hipMemset(ctx->xrows.p, 0, ctx->xrows.cap * sizeof(unsigned long long)));
+  hipIpcMemHandle_t h;
+  static_assert(sizeof(hipIpcMemHandle_t) <= 64, "IPC handle slot");
+  HIPCK(hipIpcGetMemHandle(&h, ctx->xrows.p));
+  const uint64_t seq = ++ctx->xseq;  // every rank attaches in the same sequence
+  std::memcpy(ctx->shm.ipc_handle(ctx->rank), &h, sizeof(h));
+  ctx->shm.ipc_flag(ctx->rank)->store(seq, std::memory_order_release);
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int r = 0; r < ctx->nranks; ++r) {
+    while (ctx->shm.ipc_flag(r)->load(std::memory_order_acquire) < seq) {
+      if (shm::elapsed_s(t0) > ctx->remote_deadline_s)
+        return fail(ctx, MGICP_E_COMM, "xGMI row exchange: another rank did not publish its buffer");
+      std::this_thread::sleep_for(std::chrono::microseconds(100));
+    }
+  }
+  for (int r = 0; r < ctx->nranks; ++r) {
+    if (r == ctx->rank) continue;
+    hipIpcMemHandle_t hr;
+    std::memcpy(&hr, ctx->shm.ipc_handle(r), sizeof(hr));
+    void* p = nullptr;
+    hipError_t e = hipIpcOpenMemHandle(&p, hr, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) {
+      for (void* q : ctx->xpeer) (void)hipIpcCloseMemHandle(q);
+      ctx->xpeer.clear();
+      return fail(ctx, MGICP_E_HIP, std::string("xGMI row exchange: hipIpcOpenMemHandle: ") + hipGetErrorString(e));
+    }
+    ctx->xpeer.push_back(p);
+  }
+  ctx->have_xgmi = true;
+  ctx->st[kStTransport] = ctx->comm ? 5 : 4;
+  return reset_stamps(ctx);  // every rank restarts its pass stamps with the transport
+}
+
 int mgicp_comm_attach_shm(mgicp_ctx* ctx, const char* name, size_t max_source_points) {
   if (!ctx) return MGICP_E_INVALID;
   HIPCK(hipSetDevice(ctx->device));
@@ -2848,6 +2980,7 @@ int mgicp_comm_attach_shm(mgicp_ctx* ctx, const char* name, size_t max_source_po
   rc = reset_stamps(ctx);  // the stamp count restarts with the transport on every rank
   if (rc) return rc;
   if (ctx->have_shm) {
+    xgmi_detach(ctx);  // its rendezvous (and the peers' buffers) go with the segment
     (void)hipHostUnregister(ctx->shm.base);
     shm::detach(ctx->shm);
     ctx->have_shm = false;

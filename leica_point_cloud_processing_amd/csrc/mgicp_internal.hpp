@@ -240,7 +240,15 @@ int        fdf_grid_blocks(size_t ns, int max_blocks = 2048);
 // ... each run on the command with that stamp, until a cancel (or a later command); bench_passes > 0
 // (timing): that many passes of A back to back without commands.  fdf_server_blocks: its grid for a
 // shard of ns positions on `cus` CUs (0: not servable, use the launched passes)
-int        fdf_server_blocks(size_t ns, int cus, int waves /*4 or 8 per CU*/);
+int        fdf_server_blocks(size_t ns, int cus, int waves /*4 per CU*/);
+// r05, N > 1 over xGMI: the other ranks' exchange buffers (IPC-mapped device memory), at this rank's
+// first super; a super's reducer stores its row into its own buffer (host_rows) and into every one of
+// these, so each rank's buffer receives every rank's rows
+constexpr int kMaxPeers = 8;
+struct PeerRows {
+  unsigned long long* p[kMaxPeers];
+  int n;
+};
 hipError_t launch_fdf_server(const CorrSoA& c, const uint32_t* ccnt, size_t ns, double* partial,
                              double* spart, unsigned int* tickets, double* out, unsigned long long* done_flag,
                              unsigned long long seq0, const PassCmd* cmd, PassCmd* mail,
@@ -251,7 +259,15 @@ hipError_t launch_fdf_server(const CorrSoA& c, const uint32_t* ccnt, size_t ns, 
                              int waves, int pollers /*blocks reading cmd themselves (1 or nb)*/,
                              int stall_pass /*tests: -1, or the pass the last block withholds*/,
                              unsigned long long* tpart /*nullable: stamped chunk partials, 32 words per chunk (r03)*/,
-                             hipStream_t s);
+                             hipStream_t s, const PeerRows* peers = nullptr);
+// r05 xGMI totaler (one wave, persistent for a BFGS run): for passes stamp0, stamp0 + 1, ... waits until
+// all nsup rows of the pass in this rank's exchange buffer (rows0, parity buffers `stride` words apart)
+// carry the pass's stamp, takes the fixed-order total (shm::fixed_total's tree) and stores it as one
+// stamped 32-word row at `out` (mapped host memory); exits when *gen_word != gen or after
+// `timeout_ticks` without a complete pass
+hipError_t launch_xgmi_total(const unsigned long long* rows0, size_t stride, long long nsup, unsigned int stamp0,
+                             unsigned long long* out, const unsigned int* gen_word, unsigned int gen,
+                             unsigned long long timeout_ticks, hipStream_t s);
 
 // super partials of nch chunk partials of nv (kRedVals or kMomVals) values
 hipError_t launch_super_reduce(const double* chunk, int nch, int nv, double* sup, hipStream_t s);

@@ -3527,7 +3527,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void fdf_server_kernel(
     double* __restrict__ out, unsigned long long* done_flag, unsigned long long seq0, const PassCmd* cmd,
     PassCmd* mail, unsigned long long timeout, unsigned long long* ptimes, int bench_passes, Xf34 Abench,
     unsigned long long* host_rows, size_t rows_stride, int pollers, int stall_pass,
-    unsigned long long* __restrict__ tpart) {
+    unsigned long long* __restrict__ tpart, PeerRows peers) {
   constexpr int kR = SrvShape<kWaves>::kReg, kL = SrvShape<kWaves>::kLds;
   static_assert(kR <= 4 && (kR == 4 || kR + kL <= 4), "resident groups: chunk 0, then chunk 1 only after a full chunk 0");
   __shared__ float4 lf[kWaves][kL][6][64];
@@ -3700,6 +3700,11 @@ __global__ __launch_bounds__(64 * kWaves, 1) void fdf_server_kernel(
             asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1" ::"v"(rows + static_cast<size_t>(w0) * 32 + lane),
                          "v"(w)
                          : "memory");
+            // r05 xGMI: the same row into every other rank's exchange buffer (peer device memory)
+            for (int r = 0; r < peers.n; ++r) {
+              unsigned long long* pr = peers.p[r] + (rstamp & 1u) * rows_stride + static_cast<size_t>(w0) * 32 + lane;
+              asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1" ::"v"(pr), "v"(w) : "memory");
+            }
           }
           if (kBench) {  // timing form: the reducer of the last super forwards the next command
             int lastc = 0;
@@ -4368,8 +4373,11 @@ hipError_t launch_fdf_server(const CorrSoA& c, const uint32_t* ccnt, size_t ns, 
                              unsigned long long seq0, const PassCmd* cmd, PassCmd* mail,
                              unsigned long long timeout_ticks, unsigned long long* ptimes, int bench_passes,
                              Xf34 A, unsigned long long* host_rows, size_t rows_stride, int nb, int waves,
-                             int pollers, int stall_pass, unsigned long long* tpart, hipStream_t s) {
+                             int pollers, int stall_pass, unsigned long long* tpart, hipStream_t s,
+                             const PeerRows* peers) {
   int nch = chunk_count(ns);
+  if (peers && (peers->n < 0 || peers->n > kMaxPeers || (peers->n > 0 && (!host_rows || !tpart))))
+    return hipErrorInvalidValue;  // peer rows go with the tagged tail's host rows only
   // one shape: 4 waves per CU (the 8-wave shape, 2 waves per SIMD with less residency, measured
   // 57.7-58.0 vs 50.2-50.3 us per pass, profiles/r03/srv8, is not built)
   if (nch == 0 || nb <= 0 || waves != 4) return hipErrorInvalidValue;
@@ -4388,13 +4396,80 @@ hipError_t launch_fdf_server(const CorrSoA& c, const uint32_t* ccnt, size_t ns, 
   if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   if (e != hipSuccess) return e;
   if (per_cu < 1 || static_cast<long long>(per_cu) * cus < nb) return hipErrorCooperativeLaunchTooLarge;
+  PeerRows pr{};
+  if (peers) pr = *peers;
 #define MGICP_SRV_LAUNCH(B, W)                                                                                  \
   fdf_server_kernel<B, W><<<nb, 64 * (W), 0, s>>>(c, ccnt, nch, partial, spart, tickets, out, done_flag, \
                                                   seq0, cmd, mail, timeout_ticks, ptimes, bench_passes, A, host_rows, \
-                                                  rows_stride, pollers, stall_pass, tpart)
+                                                  rows_stride, pollers, stall_pass, tpart, pr)
   if (b) MGICP_SRV_LAUNCH(true, 4);
   else MGICP_SRV_LAUNCH(false, 4);
 #undef MGICP_SRV_LAUNCH
+  return hipGetLastError();
+}
+
+// system-scope load (bypasses the caches): rows other GPUs store into this GPU's memory over xGMI
+__device__ __forceinline__ unsigned long long ld_sys_u64(const unsigned long long* p) {
+  return __hip_atomic_load(const_cast<unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// r05 xGMI totaler: one wave per rank for a BFGS run (see launch_xgmi_total in mgicp_internal.hpp).
+// Rows are stamped halves (word 2v, 2v + 1 of a row = value v's low / high half, high 32 bits of each
+// word = the pass stamp), written by every rank's super reducers into this rank's buffer over xGMI.
+// The total is shm::fixed_total's: lane l sums supers l, l + 64, ... from 0.0, then wave_sum's tree.
+__global__ __launch_bounds__(64) void xgmi_total_kernel(const unsigned long long* __restrict__ rows0, size_t stride,
+                                                         long long nsup, unsigned int stamp0,
+                                                         unsigned long long* __restrict__ out,
+                                                         const unsigned int* __restrict__ gen_word, unsigned int gen,
+                                                         unsigned long long timeout) {
+  const int lane = threadIdx.x;
+  for (unsigned int st = stamp0;; ++st) {
+    const unsigned long long* buf = rows0 + (st & 1u) * stride;
+    const unsigned long long t0 = wall_clock64();
+    double acc[16];
+    // one pass over the rows both checks the stamps and sums the values (lane l: supers l, l + 64, ...
+    // in order from 0.0); any stale word and the poll starts over
+    for (;;) {
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[v] = 0.0;
+      bool ok = true;
+      for (long long sg = lane; sg < nsup; sg += 64) {
+        const unsigned long long* row = buf + static_cast<size_t>(sg) * 32;
+        unsigned long long w[32];
+#pragma unroll
+        for (int k = 0; k < 32; ++k) w[k] = ld_sys_u64(row + k);
+#pragma unroll
+        for (int k = 0; k < 32; ++k) ok = ok && static_cast<unsigned int>(w[k] >> 32) == st;
+#pragma unroll
+        for (int v = 0; v < 16; ++v)
+          acc[v] += mk64(static_cast<unsigned int>(w[2 * v]), static_cast<unsigned int>(w[2 * v + 1]));
+      }
+      if (__builtin_amdgcn_ballot_w64(!ok) == 0ull) break;
+      const unsigned int g = __hip_atomic_load(const_cast<unsigned int*>(gen_word), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_SYSTEM);
+      if (g != gen || wall_clock64() - t0 > timeout) return;  // cancelled (BFGS run over) or nothing arrives
+      __builtin_amdgcn_s_sleep(1);
+    }
+    double tot = 0.0;  // lane v < 16: total v
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const double t = __shfl(wave_sum(acc[v]), 0, 64);
+      if ((lane >> 1) == v) tot = t;
+    }
+    if (lane < 32) {
+      const long long bits = __double_as_longlong(tot);
+      const unsigned int half = static_cast<unsigned int>((lane & 1) ? (bits >> 32) : bits);
+      const unsigned long long w = (static_cast<unsigned long long>(st) << 32) | half;
+      asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1" ::"v"(out + lane), "v"(w) : "memory");
+    }
+  }
+}
+
+hipError_t launch_xgmi_total(const unsigned long long* rows0, size_t stride, long long nsup, unsigned int stamp0,
+                             unsigned long long* out, const unsigned int* gen_word, unsigned int gen,
+                             unsigned long long timeout_ticks, hipStream_t s) {
+  if (!rows0 || !out || !gen_word || nsup < 1) return hipErrorInvalidValue;
+  xgmi_total_kernel<<<1, 64, 0, s>>>(rows0, stride, nsup, stamp0, out, gen_word, gen, timeout_ticks);
   return hipGetLastError();
 }
 

@@ -14,6 +14,8 @@
 //   rows   2 x max_sup x 256   pass rows: 32 words per super, word (stamp << 32 | 32-bit half);
 //                              the pass with row stamp s writes buffer s & 1
 //   gath   2 x max_sup x 640   generic gathers (<= 80 doubles per super); gather g uses buffer g & 1
+//   ipc    64 x 128            r05: per rank a 64-byte hipIpcMemHandle_t of its xGMI row-exchange buffer
+//                              and a 64-bit publication flag (mgicp_comm_attach_xgmi)
 //
 // Why two buffers make reuse safe: a rank writes pass s + 2 into the buffer of pass s only after
 // its host saw every row of pass s + 1, i.e. after every rank's host published s + 1's command,
@@ -42,6 +44,7 @@ constexpr size_t kHeader = 4096;
 constexpr size_t kFlagLine = 64;
 constexpr size_t kRowWords = 32;   // 16 doubles as stamped halves
 constexpr int kGathVals = 80;      // largest nv of a generic gather (Gauss-Newton moments)
+constexpr size_t kIpcLine = 128;   // r05: IPC handle (64 B) + flag (8 B) per rank
 
 struct Header {
   uint64_t magic;
@@ -55,7 +58,7 @@ struct Header {
 
 inline size_t segment_bytes(long long max_sup) {
   return kHeader + kMaxRanks * kFlagLine + 2 * static_cast<size_t>(max_sup) * kRowWords * 8 +
-         2 * static_cast<size_t>(max_sup) * kGathVals * 8;
+         2 * static_cast<size_t>(max_sup) * kGathVals * 8 + kMaxRanks * kIpcLine;
 }
 
 struct Segment {
@@ -74,6 +77,15 @@ struct Segment {
   }
   size_t rows_offset_bytes() const { return kHeader + kMaxRanks * kFlagLine; }
   size_t rows_stride_words() const { return static_cast<size_t>(max_sup) * kRowWords; }
+  // r05: rank r's IPC handle slot (64 bytes) and its publication flag
+  unsigned char* ipc_handle(int r) const {
+    return static_cast<unsigned char*>(base) + kHeader + kMaxRanks * kFlagLine +
+           2 * static_cast<size_t>(max_sup) * kRowWords * 8 + 2 * static_cast<size_t>(max_sup) * kGathVals * 8 +
+           static_cast<size_t>(r) * kIpcLine;
+  }
+  std::atomic<uint64_t>* ipc_flag(int r) const {
+    return reinterpret_cast<std::atomic<uint64_t>*>(ipc_handle(r) + 64);
+  }
   double* gath(int p) const {
     return reinterpret_cast<double*>(static_cast<char*>(base) + kHeader + kMaxRanks * kFlagLine +
                                      2 * static_cast<size_t>(max_sup) * kRowWords * 8) +

@@ -280,6 +280,10 @@ class GICPEngine:
         self._check(self._lib.mgicp_comm_attach_shm(self._h, name.encode(), int(max_source_points)),
                     "comm_attach_shm")
 
+    def attach_xgmi(self, on: bool = True):
+        """per-pass super rows over xGMI (peer device memory) after attach_shm (mgicp_comm_attach_xgmi)"""
+        self._check(self._lib.mgicp_comm_attach_xgmi(self._h, int(bool(on))), "mgicp_comm_attach_xgmi")
+
     def detach_shm(self):
         """Back to the previous transport (RCCL or local)."""
         self._check(self._lib.mgicp_comm_attach_shm(self._h, None, 0), "comm_attach_shm(detach)")

@@ -641,6 +641,7 @@ def _quit_rank(name, world, rank, n, env, q):
     try:
         env = dict(env)
         opts = {"srv_cus": int(env.pop("srv_cus"))} if "srv_cus" in env else {}
+        xgmi = env.pop("xgmi", "0") == "1"
         os.environ.update(env)
         from leica_point_cloud_processing_amd import _lib, synth
         from leica_point_cloud_processing_amd.engine import GICPEngine
@@ -649,6 +650,8 @@ def _quit_rank(name, world, rank, n, env, q):
         e = GICPEngine(device=0, options=opts)
         e.comm_init(world, rank, None)
         e.attach_shm(name, n)
+        if xgmi:
+            e.attach_xgmi()
         e.set_source_xyz(scan)
         e.set_target_xyz(cad)
         t0 = _t.perf_counter()
@@ -667,20 +670,23 @@ def _quit_rank(name, world, rank, n, env, q):
 
 
 @pytest.mark.gpu
-def test_shm_rank_quits_mid_align_others_fail_fast():
+@pytest.mark.parametrize("xgmi", [0, 1])
+def test_shm_rank_quits_mid_align_others_fail_fast(xgmi):
     """a rank that stops publishing its super rows mid-align (MGICP_DEBUG_QUIT_PASS
     on rank 1: its host gives up at pass 5, cancels its server and closes).  The surviving rank
     returns MGICP_E_COMM within the remote deadline (3 s here) -- no hang -- and its context closes at
-    once (its server was cancelled, not left waiting for commands)."""
+    once (its server was cancelled, not left waiting for commands).  xgmi = 1 (r05): the rows travel
+    through the ranks' IPC-mapped exchange buffers; the survivor's totaler never completes the pass
+    and is cancelled with its server."""
     from leica_point_cloud_processing_amd import _lib
 
     n = 200_000
-    name = f"/mgicp_quit_{os.getpid()}"
+    name = f"/mgicp_quit_{os.getpid()}_{xgmi}"
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = []
     for r in range(2):
-        env = {"srv_cus": "80", "MGICP_REMOTE_DEADLINE_S": "3"}
+        env = {"srv_cus": "80", "MGICP_REMOTE_DEADLINE_S": "3", "xgmi": str(xgmi)}
         if r == 1:
             env["MGICP_DEBUG_QUIT_PASS"] = "5"
         procs.append(ctx.Process(target=_quit_rank, args=(name, 2, r, n, env, q)))
@@ -705,6 +711,7 @@ def _shm_rank(name, world, rank, n, solver, env, q):
     try:
         env = dict(env)
         opts = {"srv_cus": int(env.pop("srv_cus"))} if "srv_cus" in env else {}
+        xgmi = env.pop("xgmi", "0") == "1"
         os.environ.update(env)
         from leica_point_cloud_processing_amd import synth
         from leica_point_cloud_processing_amd.engine import GICPEngine
@@ -713,6 +720,8 @@ def _shm_rank(name, world, rank, n, solver, env, q):
         e = GICPEngine(device=0, solver=solver, options=opts)
         e.comm_init(world, rank, None)
         e.attach_shm(name, n)
+        if xgmi:
+            e.attach_xgmi()
         e.set_source_xyz(scan)
         e.set_target_xyz(cad)
         T = e.align()
@@ -727,15 +736,19 @@ def _shm_rank(name, world, rank, n, solver, env, q):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,solver,stall", [(1, 0, -1), (2, 0, -1), (2, 0, 1), (3, 1, -1)])
-def test_shared_rows_multiprocess_bitwise_single(world, solver, stall):
+@pytest.mark.parametrize("world,solver,stall,xgmi", [(1, 0, -1, 0), (2, 0, -1, 0), (2, 0, 1, 0), (3, 1, -1, 0),
+                                                     (1, 0, -1, 1), (2, 0, -1, 1), (3, 0, -1, 1), (2, 1, -1, 1)])
+def test_shared_rows_multiprocess_bitwise_single(world, solver, stall, xgmi):
     """the resident server for N > 1 without a collective.  `world` processes on
     the ONE device of this box (servers capped at 80 CUs each so they fit side by side; RCCL refuses
     two ranks on one GPU, so the ranks are RCCL-free detached shards joined by the shared segment):
     each rank's server writes its supers' rows into the segment, every host takes the fixed-order
     total.  T (first align and iterate()), iterations, passes and fitness are bitwise those of one
     context; with stall >= 0 rank 1 takes one pass over per align.  solver 1: the GN mode's
-    moments (and the fitness) gather through the segment."""
+    moments (and the fitness) gather through the segment.  xgmi = 1 (r05): the
+    per-pass rows travel through every rank's IPC-mapped device exchange buffer (the path xGMI carries
+    between GPUs; here the ranks share one GPU) and each rank's totaler wave takes the total on the
+    device -- bitwise the same."""
     from leica_point_cloud_processing_amd import synth
     from leica_point_cloud_processing_amd.engine import GICPEngine
 
@@ -748,12 +761,14 @@ def test_shared_rows_multiprocess_bitwise_single(world, solver, stall):
     res_ref = (ref.last_result["iterations"], ref.last_result["n_evals"])
     fit_ref = ref.getFitnessScore()
     ref.close()
-    name = f"/mgicp_gpu_{os.getpid()}_{world}_{solver}_{stall}"
+    name = f"/mgicp_gpu_{os.getpid()}_{world}_{solver}_{stall}_{xgmi}"
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = []
     for r in range(world):
-        env = {"srv_cus": "80", "MGICP_ROW_DEADLINE_MS": "100"}
+        env = {"srv_cus": "80", "MGICP_ROW_DEADLINE_MS": "100", "xgmi": str(xgmi)}
+        if xgmi:
+            env["MGICP_REMOTE_DEADLINE_S"] = "20"  # a missing row fails the test, not a 120 s wait
         if stall >= 0 and r == 1:
             env["MGICP_SRV_STALL_PASS"] = str(stall)
         procs.append(ctx.Process(target=_shm_rank, args=(name, world, r, n, solver, env, q)))
@@ -769,7 +784,7 @@ def test_shared_rows_multiprocess_bitwise_single(world, solver, stall):
         np.testing.assert_array_equal(T2, T_ref)
         assert res == res_ref
         assert fit == fit_ref
-        assert st["transport"] == 2, st
+        assert st["transport"] == (4 if xgmi else 2), st
         if solver == 0:
             assert st["server_passes"] > 0, st
             assert st["takeovers"] == (2 if (stall >= 0 and rank == 1) else 0), st
