@@ -478,7 +478,8 @@ def main():
     if rank == 0 and world == 1:
         # wall time as a caller sees it (no instrumentation: the profiling mode turns the resident
         # pass server off), then the covariance kernels' times from a profiled repeat
-        eng2 = GICPEngine(device=local, max_iter=args.max_iter, fixed_iterations=int(args.fixed))
+        eng2 = GICPEngine(device=local, max_iter=args.max_iter, fixed_iterations=int(args.fixed),
+                          options={"target_cache": 0})  # new clouds: no target state from earlier engines
         t_n = time.perf_counter()
         eng2.set_target_xyz(cad)  # r04: uploads, builds the grid, starts the covariances (2nd stream)
         t_t = time.perf_counter()
@@ -507,7 +508,9 @@ def main():
     if rank == 0 and world == 1 and args.cold_pairs > 0:
         reps = []
         for _ in range(args.cold_pairs):
-            e4 = GICPEngine(device=local, max_iter=args.max_iter, fixed_iterations=int(args.fixed))
+            # cold: the target cache off (no state from an earlier engine: see gicpstate_cycles for it on)
+            e4 = GICPEngine(device=local, max_iter=args.max_iter, fixed_iterations=int(args.fixed),
+                            options={"target_cache": 0})
             t_a = time.perf_counter()
             e4.set_source_xyz(scan)
             t_b = time.perf_counter()
@@ -546,6 +549,50 @@ def main():
             "ms_to_converge_pair": med(lambda r: r["ms_to_converge_first"] + r["align"][1]["ms_wall"]),
             "median_of": len(reps),
             "repeats": reps,
+        }
+
+    # r05: the same call pattern as GICPState runs it scan after scan -- a fresh engine per cycle, the same
+    # CAD target every time -- with the library's target cache (default on): cycle 1 builds the target's
+    # grid and covariances, cycle 2 adopts them (and builds the 1-NN cell lists in its two aligns), cycles
+    # 3+ adopt grid, covariances and lists.  A new scan's (source's) upload, grid and covariances are
+    # paid every cycle.
+    gicpstate = None
+    if rank == 0 and world == 1 and args.cold_pairs > 0:
+        GICPEngine.release_cache()
+        cyc = []
+        for c in range(5):
+            e6 = GICPEngine(device=local, max_iter=args.max_iter, fixed_iterations=int(args.fixed))
+            t_a = time.perf_counter()
+            e6.set_source_xyz(scan)
+            e6.set_target_xyz(cad)
+            t_b = time.perf_counter()
+            adopted = e6.cache_stats()["adopted"]
+            al = []
+            for _a in range(2):
+                t_0 = time.perf_counter()
+                T_c = e6.align()
+                t_1 = time.perf_counter()
+                lr = e6.last_result
+                al.append({"ms_wall": round(1e3 * (t_1 - t_0), 3), "ms_loop": round(lr["ms_loop"], 3),
+                           "iterations": lr["iterations"],
+                           "loop_iterations_per_s": round(lr["iterations"] / (lr["ms_loop"] * 1e-3), 2)})
+            e6.close()
+            cyc.append({"cycle": c + 1, "target_adopted": bool(adopted), "ms_set_clouds": round(1e3 * (t_b - t_a), 3),
+                        "ms_to_converge_first": round(1e3 * (t_b - t_a) + al[0]["ms_wall"], 3), "align": al,
+                        "frob_vs_timed": float(np.linalg.norm(T_c.astype(np.float64) -
+                                                              eng.getFinalTransformation().astype(np.float64)))})
+        GICPEngine.release_cache()
+        steady = cyc[2:]
+        gicpstate = {
+            "pattern": ("GICPState scan after scan (LeicaStateMachine.cpp:141-150): a fresh engine per cycle, "
+                        "set_source + set_target (the same CAD points every cycle), align + iterate; the library's "
+                        "target cache hands the CAD cloud's grid, covariances and 1-NN cell lists from one cycle's "
+                        "engine to the next (adopted only when the uploaded points are equal bit for bit)"),
+            "steady_first_align_ms_loop": round(float(np.median([c["align"][0]["ms_loop"] for c in steady])), 3),
+            "steady_first_align_loop_iterations_per_s": round(float(np.median(
+                [c["align"][0]["loop_iterations_per_s"] for c in steady])), 2),
+            "steady_ms_to_converge_first": round(float(np.median([c["ms_to_converge_first"] for c in steady])), 3),
+            "cycles": cyc,
         }
 
     # the in-align pass past the Infinity Cache: at C4 ~248 MB of streamed bytes
@@ -805,6 +852,7 @@ def main():
         "ms_to_converge_first_detail": {k: round(first[k], 3) for k in ("ms_upload", "ms_prep", "ms_loop")},
         "ms_to_converge_cached": round(1e3 * dt / args.steps, 3),
         "cold_pair": cold_pair,
+        "gicpstate_cycles": gicpstate,
         "frob_vs_oracle": full["frob_vs_oracle"] if full else None,
         "parity_full_size": full,
         "frob_vs_oracle_sample": frob_sample,

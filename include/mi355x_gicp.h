@@ -80,6 +80,11 @@ int         mgicp_create(mgicp_ctx** ctx, const mgicp_params* p);
 int         mgicp_set_params(mgicp_ctx* ctx, const mgicp_params* p);
 const char* mgicp_last_error(const mgicp_ctx* ctx);
 void        mgicp_destroy(mgicp_ctx* ctx);
+/* r05 target cache: mgicp_destroy leaves a single-rank context's target state (grid, covariances,
+ * 1-NN cell lists; ~2-3.5 GB at 5M points) in a process-wide cache, one entry per device; a later
+ * set_target whose points equal the cached ones bit for bit (compared on the device) adopts it instead
+ * of rebuilding -- results are those of a rebuild bit for bit.  This frees every cached entry. */
+void        mgicp_release_cache(void);
 int         mgicp_device_count(int* n);
 
 /* ---- inputs (Registration::setInputTarget / setInputSource) ----
@@ -270,10 +275,14 @@ int mgicp_set_profiling(mgicp_ctx* ctx, int on);
 /* test / diagnostic forms of the engine, set explicitly on one context (never through the
  * environment): "resident", "host_rows", "srv_cus", "fused_finish", "gated", "bar_cmd" (the
  * objective-pass path), "async_cov", "lazy_src_cov", "knn_logged" (covariances), "vlist",
- * "vlist_cold", "vlist_eager", "vlist_stats", "fuse_compact" (1-NN cell lists), "grid_occ" (grid
+ * "vlist_cold", "vlist_eager", "vlist_stats", "fuse_compact" (1-NN cell lists), "target_cache", "grid_occ" (grid
  * sizing of the next set_*).  Every form gives the default path's results bit for bit (the GPU tests
  * that pin each one: INTEGRATION.md "Debug options"); MGICP_E_INVALID for an unknown name. */
 int mgicp_debug_option(mgicp_ctx* ctx, const char* name, double value);
+/* target cache (mgicp_release_cache): out[0] the current target was adopted from the cache, out[1]
+ * adoptions and out[2] donations on this device so far, out[3] an entry is cached on this device.
+ * Debug option "target_cache" 0: this context neither adopts nor leaves a target. */
+int mgicp_debug_cache_stats(mgicp_ctx* ctx, long long out[4]);
 
 #ifdef __cplusplus
 }

@@ -112,6 +112,8 @@ _SIGNATURES = {
     "mgicp_debug_kernel_times": (ctypes.c_int, [_P, _DP, _IP]),
     "mgicp_set_profiling": (ctypes.c_int, [_P, ctypes.c_int]),
     "mgicp_debug_option": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_double]),
+    "mgicp_debug_cache_stats": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_longlong)]),
+    "mgicp_release_cache": (None, []),
 }
 
 _lib = None

@@ -248,6 +248,8 @@ struct Cloud {
   bool drop_nonfinite = false; // build the grid over the finite points only (KdTreeFLANN semantics)
   double occupancy = 0;        // grid sizing target (points per non-empty cell); 0 = context default
   size_t n_built = 0;          // points of the last grid built in this slot (cell-size hint)
+  bool fresh_grid = false;     // the grid was sized from the 3-D guess (not from an earlier grid of the slot):
+                               // exactly the grid a fresh context builds for these points (target cache)
   DevBuf<double2> cov;        // 3 * cov_stride
   size_t cov_stride = 0;      // entries per covariance array (n, or the padded all-gather size)
   float lo[3] = {0.f, 0.f, 0.f}, hi[3] = {0.f, 0.f, 0.f};  // bounding box (original coordinates)
@@ -276,6 +278,48 @@ enum {
 // per CU, 512 registers per lane), so a second context aligning on the same device at the same
 // time runs launched passes instead of a second server.
 std::atomic<int> g_srv_busy[64];
+
+template <class T>
+void swap_buf(DevBuf<T>& a, DevBuf<T>& b) {  // the device memory changes hands; each side keeps its graveyard
+  std::swap(a.p, b.p);
+  std::swap(a.cap, b.cap);
+}
+
+// r05 target cache: one entry per device (its DevBufs belong to no context: grave = nullptr)
+struct TargetCache {
+  std::mutex mu;
+  bool valid = false;
+  Cloud t;
+  int k = 0;
+  double eps = 0, occupancy = 0;
+  float vlist_cell = 0.f;
+  bool vl_valid = false, vl_alloc = false, vl_off = false;
+  VListView vl{};
+  size_t vl_ncells = 0;
+  uint32_t vl_epoch = 0;
+  int vl_groups = 0;
+  DevBuf<uint32_t> vl_cell;
+  DevBuf<float4> vl_pool;
+  DevBuf<unsigned int> vl_ctr;
+  long long hits = 0, donations = 0;
+};
+TargetCache g_tcache[64];
+
+// the target's device state: every buffer a grid, its covariances and its cell lists live in
+template <class F>
+void each_target_buf(Cloud& a, Cloud& b, F&& f) {
+  f(a.orig, b.orig); f(a.pts, b.pts); f(a.perm, b.perm); f(a.cell_start, b.cell_start);
+  f(a.empty_dist, b.empty_dist); f(a.seed, b.seed); f(a.seed_scratch, b.seed_scratch); f(a.boxes, b.boxes);
+  f(a.pairs, b.pairs); f(a.cov, b.cov);
+}
+void tcache_clear_locked(TargetCache& c) {
+  Cloud none;
+  each_target_buf(c.t, none, [](auto& x, auto&) { x.release(); });
+  c.vl_cell.release();
+  c.vl_pool.release();
+  c.vl_ctr.release();
+  c.valid = false;
+}
 
 }  // namespace
 
@@ -503,6 +547,12 @@ struct mgicp_ctx {
   // eagerly or ~15 ms spread over two aligns lazily at C4, so the reference's align + iterate pair on
   // one cloud pair (GICPAlignment.cpp:96, :116) runs both aligns without them (r04, profiles/r04/policy)
   int vl_cold_groups = 2;
+  // r05 target cache (process-wide, one entry per device): a destroyed context leaves its target's grid,
+  // covariances and 1-NN cell lists there; a later context whose set_target uploads the same points
+  // (compared on the device, bit for bit) adopts them instead of rebuilding -- GICPState constructs a
+  // fresh GICPAlignment per scan against the same CAD cloud (LeicaStateMachine.cpp:149-150)
+  bool tcache_on = true;                // debug option "target_cache"
+  bool tcache_adopted = false;          // the current target came from the cache
   // multi-GPU
   int nranks = 1, rank = 0;
   ncclComm_t comm = nullptr;
@@ -849,6 +899,124 @@ int upload_cloud(mgicp_ctx* ctx, Cloud& cl, const float* xyz, size_t n, size_t s
   return MGICP_OK;
 }
 
+// r05 target cache.  A single-rank context leaves its target at destroy when the grid is the one a fresh
+// context would build for those points (fresh_grid: sized from the 3-D guess, so the source grid, which
+// starts from the target's cell size, and every sum come out the same -- DESIGN.md "Target cache").
+void tcache_donate(mgicp_ctx* ctx, bool cov_complete) {
+  Cloud& t = ctx->tgt;
+  if (!ctx->tcache_on || ctx->nranks != 1 || ctx->comm || ctx->have_shm || t.dirty || t.n == 0 || t.n_built != t.n ||
+      !t.fresh_grid)
+    return;
+  TargetCache& c = g_tcache[ctx->device & 63];
+  std::lock_guard<std::mutex> lk(c.mu);
+  tcache_clear_locked(c);
+  each_target_buf(c.t, t, [](auto& x, auto& y) { swap_buf(x, y); });
+  c.t.n = t.n;
+  c.t.have_cov = cov_complete && (!t.have_cov || (t.cov_p0 == 0 && t.cov_p1 == t.n)) && t.cov_stride == t.n;
+  c.t.cov_p0 = 0;
+  c.t.cov_p1 = t.n;
+  c.t.cov_stride = t.cov_stride;
+  c.t.want_empty_map = t.want_empty_map;
+  c.t.want_seed_map = t.want_seed_map;
+  c.t.want_boxes = t.want_boxes;
+  c.t.want_pairs = t.want_pairs;
+  c.t.drop_nonfinite = t.drop_nonfinite;
+  c.t.occupancy = t.occupancy;
+  c.t.n_built = t.n_built;
+  c.t.fresh_grid = true;
+  std::memcpy(c.t.lo, t.lo, sizeof(t.lo));
+  std::memcpy(c.t.hi, t.hi, sizeof(t.hi));
+  c.t.view = t.view;
+  c.t.ncells = t.ncells;
+  c.k = ctx->prm.k;
+  c.eps = ctx->prm.gicp_eps;
+  c.occupancy = t.occupancy > 0 ? t.occupancy : ctx->occupancy;
+  // the cell lists travel with the target once built (the donor ran 3+ aligns on it).  The list policy
+  // itself does not go on across contexts: GICPState's engines run 2 aligns each, and building the lists
+  // in a later cycle cost 39 + 151 ms at C4 (profiles/r05/check5) against ~1.6 ms saved per cycle
+  c.vl_valid = ctx->vl_valid && ctx->vl_alloc;
+  if (c.vl_valid) {
+    if (ctx->vl_alloc) {
+      swap_buf(c.vl_cell, ctx->vl_cell);
+      swap_buf(c.vl_pool, ctx->vl_pool);
+      swap_buf(c.vl_ctr, ctx->vl_ctr);
+    }
+    c.vl = ctx->vl;
+    c.vl_alloc = ctx->vl_alloc;
+    c.vl_off = ctx->vl_off;
+    c.vl_ncells = ctx->vl_ncells;
+    c.vl_epoch = ctx->vl_epoch;
+    c.vl_groups = ctx->vl_groups;
+    c.vlist_cell = ctx->vlist_cell;
+  }
+  c.valid = true;
+  c.donations++;
+}
+
+// After set_target's upload: the cached state when the uploaded points equal the cached ones bit for bit
+// (original order, w = original index).  The context's previous target buffers go to its graveyard.
+int tcache_adopt(mgicp_ctx* ctx) {
+  ctx->tcache_adopted = false;
+  Cloud& t = ctx->tgt;
+  if (!ctx->tcache_on || ctx->nranks != 1 || ctx->comm || ctx->have_shm) return MGICP_OK;
+  TargetCache& c = g_tcache[ctx->device & 63];
+  std::lock_guard<std::mutex> lk(c.mu);
+  const double occ = t.occupancy > 0 ? t.occupancy : ctx->occupancy;
+  if (!c.valid || c.t.n != t.n || c.occupancy != occ || c.t.drop_nonfinite != t.drop_nonfinite ||
+      c.t.want_pairs != t.want_pairs || c.t.want_boxes != t.want_boxes)
+    return MGICP_OK;
+  unsigned int* diff = reinterpret_cast<unsigned int*>(ctx->d_small);
+  HIPCK(launch_equal(t.orig.p, c.t.orig.p, t.n, diff, ctx->stream));
+  int rc = sync(ctx);
+  if (rc) return rc;
+  unsigned int d = 1;
+  std::memcpy(&d, ctx->h_small, sizeof(d));
+  if (d != 0) return MGICP_OK;
+  each_target_buf(t, c.t, [](auto& x, auto& y) { swap_buf(x, y); });
+  t.dirty = false;
+  t.have_cov = c.t.have_cov && c.k == ctx->prm.k && c.eps == ctx->prm.gicp_eps;
+  t.cov_p0 = 0;
+  t.cov_p1 = t.have_cov ? t.n : 0;
+  t.cov_stride = c.t.cov_stride;
+  t.n_built = c.t.n_built;
+  t.fresh_grid = true;
+  std::memcpy(t.lo, c.t.lo, sizeof(t.lo));
+  std::memcpy(t.hi, c.t.hi, sizeof(t.hi));
+  t.view = c.t.view;  // the same device memory, now this context's
+  t.ncells = c.t.ncells;
+  ctx->vl_valid = false;
+  if (c.vl_valid && c.vlist_cell == ctx->vlist_cell) {
+    if (c.vl_alloc) {
+      swap_buf(ctx->vl_cell, c.vl_cell);
+      swap_buf(ctx->vl_pool, c.vl_pool);
+      swap_buf(ctx->vl_ctr, c.vl_ctr);
+    }
+    ctx->vl = c.vl;
+    ctx->vl_valid = true;
+    ctx->vl_alloc = c.vl_alloc;
+    ctx->vl_off = c.vl_off;
+    ctx->vl_ncells = c.vl_ncells;
+    ctx->vl_epoch = c.vl_epoch;
+    ctx->vl_groups = c.vl_groups;
+  }
+  // the cache now holds this context's previous target buffers: to the graveyard (freed at a quiet point)
+  Cloud none;
+  each_target_buf(c.t, none, [&](auto& x, auto&) {
+    if (x.p) ctx->grave->v.push_back(x.p);
+    x.p = nullptr;
+    x.cap = 0;
+  });
+  for (void* p : {static_cast<void*>(c.vl_cell.p), static_cast<void*>(c.vl_pool.p), static_cast<void*>(c.vl_ctr.p)})
+    if (p) ctx->grave->v.push_back(p);
+  c.vl_cell.p = nullptr; c.vl_cell.cap = 0;
+  c.vl_pool.p = nullptr; c.vl_pool.cap = 0;
+  c.vl_ctr.p = nullptr; c.vl_ctr.cap = 0;
+  c.valid = false;
+  c.hits++;
+  ctx->tcache_adopted = true;
+  return MGICP_OK;
+}
+
 // Build the row-sorted uniform grid of a cloud (one-time per set_*).
 int build_grid(mgicp_ctx* ctx, Cloud& cl) {
   const size_t n = cl.n;
@@ -916,6 +1084,8 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
     return nc;
   };
   double h = maxext > 0.f ? static_cast<double>(maxext) / std::cbrt(static_cast<double>(n)) : 1.0;
+  const bool fresh = !(cl.view.h > 0.f && cl.n_built > 0) && !(&cl == &ctx->src && ctx->tgt.view.h > 0.f &&
+                                                               ctx->tgt.n_built > 0);
   // a cell size that already fitted a cloud of the same scene is a better start than the 3-D
   // guess: this cloud's previous grid, else (source) the target's, scaled as a surface (sqrt n).
   // The source's grid -- its sorted order, so the fixed reduction tree of every objective pass --
@@ -1051,6 +1221,7 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
   }
   cl.ncells = nc;
   cl.n_built = n;
+  cl.fresh_grid = fresh;
   cl.dirty = false;
   cl.have_cov = false;
   if (&cl == &ctx->tgt) ctx->vl_valid = false;  // the 1-NN cell lists index the old target
@@ -2360,9 +2531,12 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   cancel_gated(ctx);
   if (ctx->aux_stream) (void)hipStreamSynchronize(ctx->aux_stream);
+  // a head-start launch chain that ran to its end on the aux stream completed the target's covariances
+  const bool tgt_cov_done = ctx->tgt.have_cov || (ctx->tgt_cov_pending && !ctx->tgt.dirty);
   ctx->tgt_cov_pending = ctx->src_cov_pending = false;
   (void)hipStreamSynchronize(ctx->stream);
   srv_release(ctx);
+  tcache_donate(ctx, tgt_cov_done);  // r05: the target's grid, covariances and lists outlive the context
   ctx->f_flags.release(); ctx->f_pos.release(); ctx->f_rgba_in.release(); ctx->f_rgba.release();
   ctx->f_rgba2.release(); ctx->f_vox.release(); ctx->f_vox2.release(); ctx->f_keep.release();
   ctx->f_count.release();
@@ -2421,7 +2595,8 @@ void mgicp_destroy(mgicp_ctx* ctx) {
 int mgicp_set_target(mgicp_ctx* ctx, const float* xyz, size_t n, size_t stride) {
   if (!ctx) return MGICP_E_INVALID;
   HIPCK(hipSetDevice(ctx->device));
-  const int rc = upload_cloud(ctx, ctx->tgt, xyz, n, stride, false);
+  int rc = upload_cloud(ctx, ctx->tgt, xyz, n, stride, false);
+  if (!rc) rc = tcache_adopt(ctx);
   return rc ? rc : cov_prep_async_all(ctx);
 }
 int mgicp_set_source(mgicp_ctx* ctx, const float* xyz, size_t n, size_t stride) {
@@ -2433,7 +2608,8 @@ int mgicp_set_source(mgicp_ctx* ctx, const float* xyz, size_t n, size_t stride) 
 int mgicp_set_target_device(mgicp_ctx* ctx, const float* d_xyz, size_t n, size_t stride) {
   if (!ctx) return MGICP_E_INVALID;
   HIPCK(hipSetDevice(ctx->device));
-  const int rc = upload_cloud(ctx, ctx->tgt, d_xyz, n, stride, true);
+  int rc = upload_cloud(ctx, ctx->tgt, d_xyz, n, stride, true);
+  if (!rc) rc = tcache_adopt(ctx);
   return rc ? rc : cov_prep_async_all(ctx);
 }
 int mgicp_set_source_device(mgicp_ctx* ctx, const float* d_xyz, size_t n, size_t stride) {
@@ -3400,6 +3576,32 @@ int mgicp_set_profiling(mgicp_ctx* ctx, int on) {
   return MGICP_OK;
 }
 
+// r05 target cache: [0] the current target was adopted from the cache, [1] adoptions and [2] donations
+// on this device so far (process-wide), [3] an entry is cached on this device
+int mgicp_debug_cache_stats(mgicp_ctx* ctx, long long out[4]) {
+  if (!ctx || !out) return MGICP_E_INVALID;
+  TargetCache& c = g_tcache[ctx->device & 63];
+  std::lock_guard<std::mutex> lk(c.mu);
+  out[0] = ctx->tcache_adopted ? 1 : 0;
+  out[1] = c.hits;
+  out[2] = c.donations;
+  out[3] = c.valid ? 1 : 0;
+  return MGICP_OK;
+}
+
+void mgicp_release_cache(void) {
+  int dev = 0;
+  const bool have = hipGetDevice(&dev) == hipSuccess;
+  for (int d = 0; d < 64; ++d) {
+    TargetCache& c = g_tcache[d];
+    std::lock_guard<std::mutex> lk(c.mu);
+    if (!c.valid && !c.t.orig.p && !c.vl_pool.p) continue;
+    (void)hipSetDevice(d);
+    tcache_clear_locked(c);
+  }
+  if (have) (void)hipSetDevice(dev);
+}
+
 // Test / diagnostic forms of the engine (INTEGRATION.md "Debug options"): explicit per-context calls,
 // never environment variables, so a deployment cannot switch a kernel by accident.
 // Pending covariance launches are joined and the stream drained first; list-related options drop the
@@ -3431,6 +3633,7 @@ int mgicp_debug_option(mgicp_ctx* ctx, const char* name, double value) {
   else if (n == "vlist_eager") ctx->vl_eager = on, ctx->vl_valid = false;
   else if (n == "vlist_stats") ctx->vl_stats = on;      // per-sweep list statistics on stderr
   else if (n == "fuse_compact") ctx->fuse_compact = on; // compaction fused into listed sweeps
+  else if (n == "target_cache") ctx->tcache_on = on;    // adopt / leave the target state (process cache)
   else if (n == "grid_occ") {                           // grid sizing (points per non-empty cell), next set_*
     if (!(value >= 1.0 && value <= 256.0)) return fail(ctx, MGICP_E_INVALID, "grid_occ must be in [1, 256]");
     ctx->occupancy = value;

@@ -330,6 +330,8 @@ size_t scan_scratch_bytes(size_t n);
 hipError_t launch_exclusive_scan(void* scratch, size_t scratch_bytes, const uint32_t* in,
                                  uint32_t* out, size_t n, hipStream_t s);
 hipError_t launch_iota(uint32_t* v, size_t n, hipStream_t s);
+// r05 target cache: *diff = 1 when a[0..n) and b[0..n) differ in any bit (else 0)
+hipError_t launch_equal(const float4* a, const float4* b, size_t n, unsigned int* diff, hipStream_t s);
 // resolve all kernels once (moves the code-object loading cost into mgicp_create)
 // and exercise both copy directions once, small and large (pinned: pinned host scratch)
 hipError_t preload_kernels(void* pinned, size_t pinned_bytes, hipStream_t s);

@@ -4129,6 +4129,25 @@ hipError_t launch_cell_boxes(const float4* pts, const uint32_t* cell_start, size
   return hipGetLastError();
 }
 
+// r05 target cache: *diff |= 1 when the two arrays differ in any bit
+__global__ __launch_bounds__(256) void equal_kernel(const uint4* __restrict__ a, const uint4* __restrict__ b, size_t n,
+                                                    unsigned int* __restrict__ diff) {
+  bool d = false;
+  for (size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<size_t>(gridDim.x) * blockDim.x) {
+    const uint4 x = a[i], y = b[i];
+    d = d || x.x != y.x || x.y != y.y || x.z != y.z || x.w != y.w;
+  }
+  if (__builtin_amdgcn_ballot_w64(d) != 0ull && (threadIdx.x & 63) == 0) atomicOr(diff, 1u);
+}
+
+hipError_t launch_equal(const float4* a, const float4* b, size_t n, unsigned int* diff, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(diff, 0, sizeof(unsigned int), s);
+  if (e != hipSuccess || n == 0) return e;
+  equal_kernel<<<2048, 256, 0, s>>>(reinterpret_cast<const uint4*>(a), reinterpret_cast<const uint4*>(b), n, diff);
+  return hipGetLastError();
+}
+
 hipError_t launch_iota(uint32_t* v, size_t n, hipStream_t s) {
   if (!n) return hipSuccess;
   iota_kernel<<<nblk(n), 256, 0, s>>>(v, n);

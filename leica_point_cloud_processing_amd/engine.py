@@ -44,6 +44,10 @@ def _dp(a):
 
 
 class GICPEngine:
+    # mgicp_debug_option forms applied to every new engine before its own `options` (the GPU test suite
+    # sets {"target_cache": 0} so engines of different tests never adopt each other's targets)
+    DEFAULT_OPTIONS: dict = {}
+
     def __init__(self, device: int = -1, options: dict | None = None, **params):
         """params: mgicp_params fields; options: mgicp_debug_option forms (tests / diagnostics only)"""
         self._lib = _lib.load()
@@ -62,8 +66,19 @@ class GICPEngine:
         self._converged = False
         self._final = np.eye(4, dtype=np.float32)
         self.last_result = None
-        for k, v in (options or {}).items():
+        for k, v in {**GICPEngine.DEFAULT_OPTIONS, **(options or {})}.items():
             self.debug_option(k, v)
+
+    def cache_stats(self) -> dict:
+        """The process-wide target cache (mgicp_debug_cache_stats)."""
+        out = (ctypes.c_longlong * 4)()
+        self._check(self._lib.mgicp_debug_cache_stats(self._h, out), "cache_stats")
+        return {"adopted": int(out[0]), "hits": int(out[1]), "donations": int(out[2]), "cached": int(out[3])}
+
+    @staticmethod
+    def release_cache():
+        """Free the process-wide target cache (mgicp_release_cache)."""
+        _lib.load().mgicp_release_cache()
 
     def debug_option(self, name: str, value):
         """mgicp_debug_option: a test / diagnostic form of the engine on this context only"""
