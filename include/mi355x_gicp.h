@@ -280,9 +280,11 @@ int mgicp_set_profiling(mgicp_ctx* ctx, int on);
  * that pin each one: INTEGRATION.md "Debug options"); MGICP_E_INVALID for an unknown name. */
 int mgicp_debug_option(mgicp_ctx* ctx, const char* name, double value);
 /* target cache (mgicp_release_cache): out[0] the current target was adopted from the cache, out[1]
- * adoptions and out[2] donations on this device so far, out[3] an entry is cached on this device.
+ * adoptions and out[2] donations on this device so far, out[3] an entry is cached on this device,
+ * out[4] a source set before any target started its grid from the cached target's cell size: 0 no,
+ * 1 pending, 2 kept (the target set next had that cell size), 3 discarded and rebuilt.
  * Debug option "target_cache" 0: this context neither adopts nor leaves a target. */
-int mgicp_debug_cache_stats(mgicp_ctx* ctx, long long out[4]);
+int mgicp_debug_cache_stats(mgicp_ctx* ctx, long long out[5]);
 
 #ifdef __cplusplus
 }

@@ -553,6 +553,11 @@ struct mgicp_ctx {
   // fresh GICPAlignment per scan against the same CAD cloud (LeicaStateMachine.cpp:149-150)
   bool tcache_on = true;                // debug option "target_cache"
   bool tcache_adopted = false;          // the current target came from the cache
+  // r05: a source set before any target sized its grid from the cached target's cell size (spec_h,
+  // spec_n); checked against the target set_target brings: 1 pending, 2 kept, 3 discarded (rebuilt)
+  int src_spec = 0;
+  float spec_h = 0.f;
+  size_t spec_n = 0;
   // multi-GPU
   int nranks = 1, rank = 0;
   ncclComm_t comm = nullptr;
@@ -834,10 +839,50 @@ int cov_prep_async(mgicp_ctx* ctx, bool tgt) {
                        capped ? ctx->async_ring_cap : -1, capped ? ctx->cov_ok.p : nullptr,
                        ctx->knn_logged ? 2 * std::max(ctx->cus, 1) : 0));
   HIPCK(hipEventRecord(ctx->aux_ev[tgt ? 0 : 1], ctx->aux_stream));
+  MGICP_TRACE_AT(tgt ? "head start: target k-NN queued" : "head start: source k-NN queued");
   (tgt ? ctx->tgt_cov_pending : ctx->src_cov_pending) = true;
   // r05: the source's 1-NN query order (a Morton sort of the shard) now, on the main stream beside the
   // covariances -- not inside the first align's loop
   if (!tgt) (void)query_perm(ctx);
+  return MGICP_OK;
+}
+
+// r05: GICPState sets the source before the target (GICPAlignment.cpp:89-90), so a fresh context's source
+// grid -- which starts from the target's cell size -- had to wait for set_target, and its covariances ran
+// into the first align.  When the device's target cache holds a target, the source grid starts from THAT
+// target's cell size at set_source; spec_check confirms it once the real target's grid exists (the same
+// cell size and point count: the grid, every sorted order and sum are those of the synchronous path) or
+// throws the source's grid and covariances away and rebuilds them from the real target.
+bool spec_from_cache(mgicp_ctx* ctx) {
+  if (!ctx->tcache_on || !ctx->async_tgt || !ctx->aux_stream || ctx->nranks != 1 || ctx->comm || ctx->have_shm ||
+      ctx->profiling || ctx->src.n_built > 0)
+    return false;
+  TargetCache& c = g_tcache[ctx->device & 63];
+  std::lock_guard<std::mutex> lk(c.mu);
+  if (!c.valid || !(c.t.view.h > 0.f) || c.t.n_built == 0) return false;
+  ctx->spec_h = c.t.view.h;
+  ctx->spec_n = c.t.n_built;
+  ctx->src_spec = 1;
+  return true;
+}
+int spec_check(mgicp_ctx* ctx) {
+  if (ctx->src_spec != 1 || ctx->tgt.dirty || ctx->tgt.n_built == 0) return MGICP_OK;
+  if (ctx->tgt.view.h == ctx->spec_h && ctx->tgt.n_built == ctx->spec_n) {
+    ctx->src_spec = 2;
+    return MGICP_OK;
+  }
+  ctx->src_spec = 3;
+  if (int rc = cov_join(ctx, false)) return rc;  // its k-NN launch reads the grid about to be rebuilt
+  Cloud& s = ctx->src;
+  s.dirty = true;
+  s.have_cov = false;
+  s.view.h = 0.f;  // no previous grid: the rebuild starts from the real target's cell size
+  s.n_built = 0;
+  ctx->qperm_valid = false;
+  ctx->src_lazy_ready = false;
+  ctx->src_async_lazy = false;
+  ctx->have_corr = false;
+  ctx->seed_valid = false;
   return MGICP_OK;
 }
 
@@ -850,7 +895,11 @@ int cov_prep_async(mgicp_ctx* ctx, bool tgt) {
 int cov_prep_async_all(mgicp_ctx* ctx) {
   int rc = MGICP_OK;
   if (ctx->tgt.dirty && (rc = cov_prep_async(ctx, true))) return rc;
-  if (ctx->src.dirty && !ctx->tgt.dirty && ctx->tgt.n_built > 0) rc = cov_prep_async(ctx, false);
+  if ((rc = spec_check(ctx))) return rc;
+  if (ctx->src.dirty && !ctx->tgt.dirty && ctx->tgt.n_built > 0)
+    rc = cov_prep_async(ctx, false);
+  else if (ctx->src.dirty && ctx->tgt.n_built == 0 && !ctx->tgt.dirty && spec_from_cache(ctx))
+    rc = cov_prep_async(ctx, false);  // GICPState's order: the source first, its target most likely cached
   return rc;
 }
 
@@ -863,6 +912,11 @@ int upload_cloud(mgicp_ctx* ctx, Cloud& cl, const float* xyz, size_t n, size_t s
   if (&cl == &ctx->tgt || &cl == &ctx->src) {  // an async covariance launch still reads the old cloud
     const int rj = cov_join(ctx, &cl == &ctx->tgt);
     if (rj) return rj;
+  }
+  if (&cl == &ctx->src && ctx->src_spec == 1) {  // a speculative grid is no "previous grid" of the new source
+    cl.view.h = 0.f;
+    cl.n_built = 0;
+    ctx->src_spec = 0;
   }
   const double t0 = now_ms();
   MGICP_TRACE_AT("upload: begin");
@@ -966,9 +1020,11 @@ int tcache_adopt(mgicp_ctx* ctx) {
       c.t.want_pairs != t.want_pairs || c.t.want_boxes != t.want_boxes)
     return MGICP_OK;
   unsigned int* diff = reinterpret_cast<unsigned int*>(ctx->d_small);
+  MGICP_TRACE_AT("adopt: compare");
   HIPCK(launch_equal(t.orig.p, c.t.orig.p, t.n, diff, ctx->stream));
   int rc = sync(ctx);
   if (rc) return rc;
+  MGICP_TRACE_AT("adopt: compared");
   unsigned int d = 1;
   std::memcpy(&d, ctx->h_small, sizeof(d));
   if (d != 0) return MGICP_OK;
@@ -1096,6 +1152,8 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
     h = static_cast<double>(cl.view.h) * std::sqrt(static_cast<double>(cl.n_built) / n);
   else if (&cl == &ctx->src && ctx->tgt.view.h > 0.f && ctx->tgt.n_built > 0)
     h = static_cast<double>(ctx->tgt.view.h) * std::sqrt(static_cast<double>(ctx->tgt.n_built) / n);
+  else if (&cl == &ctx->src && ctx->src_spec == 1)  // the cached target's (spec_check confirms it)
+    h = static_cast<double>(ctx->spec_h) * std::sqrt(static_cast<double>(ctx->spec_n) / n);
   h = std::max(h, 1e-6);
   int nd[3];
   double h_prev = 0, occ_prev = 0;
@@ -1359,6 +1417,7 @@ int prepare(mgicp_ctx* ctx, bool need_cov) {
                 "a cloud has fewer points than k_correspondences (PCL computeCovariances)");
   int rc;
   if (ctx->tgt.dirty && (rc = build_grid(ctx, ctx->tgt))) return rc;
+  if ((rc = spec_check(ctx))) return rc;
   if (ctx->src.dirty && (rc = build_grid(ctx, ctx->src))) return rc;
   if (!need_cov) return MGICP_OK;
   // set_target's covariances still running count as current: the first sweep runs beside them and
@@ -3577,8 +3636,9 @@ int mgicp_set_profiling(mgicp_ctx* ctx, int on) {
 }
 
 // r05 target cache: [0] the current target was adopted from the cache, [1] adoptions and [2] donations
-// on this device so far (process-wide), [3] an entry is cached on this device
-int mgicp_debug_cache_stats(mgicp_ctx* ctx, long long out[4]) {
+// on this device so far (process-wide), [3] an entry is cached on this device, [4] the source grid's start
+// from the cached target's cell size (0 none, 1 pending, 2 kept, 3 discarded and rebuilt)
+int mgicp_debug_cache_stats(mgicp_ctx* ctx, long long out[5]) {
   if (!ctx || !out) return MGICP_E_INVALID;
   TargetCache& c = g_tcache[ctx->device & 63];
   std::lock_guard<std::mutex> lk(c.mu);
@@ -3586,6 +3646,7 @@ int mgicp_debug_cache_stats(mgicp_ctx* ctx, long long out[4]) {
   out[1] = c.hits;
   out[2] = c.donations;
   out[3] = c.valid ? 1 : 0;
+  out[4] = ctx->src_spec;
   return MGICP_OK;
 }
 
@@ -3624,7 +3685,7 @@ int mgicp_debug_option(mgicp_ctx* ctx, const char* name, double value) {
     ctx->lazy_src_cov = on;
     ctx->src.have_cov = false;
     ctx->src_lazy_ready = false;
-  } else if (n == "knn_logged") {                       // k-NN kernel: wave-staged (1) or register-list only (0)
+  } else if (n == "knn_logged") {                       // k-NN: the logged kernel + hand-off (1) or the register-list kernel only (0)
     ctx->knn_logged = on;
     ctx->src.have_cov = ctx->tgt.have_cov = false;
     ctx->src_lazy_ready = false;

@@ -71,9 +71,10 @@ class GICPEngine:
 
     def cache_stats(self) -> dict:
         """The process-wide target cache (mgicp_debug_cache_stats)."""
-        out = (ctypes.c_longlong * 4)()
+        out = (ctypes.c_longlong * 5)()
         self._check(self._lib.mgicp_debug_cache_stats(self._h, out), "cache_stats")
-        return {"adopted": int(out[0]), "hits": int(out[1]), "donations": int(out[2]), "cached": int(out[3])}
+        return {"adopted": int(out[0]), "hits": int(out[1]), "donations": int(out[2]), "cached": int(out[3]),
+                "source_spec": ("none", "pending", "kept", "discarded")[int(out[4])]}
 
     @staticmethod
     def release_cache():

@@ -59,6 +59,7 @@ def test_adopted_target_aligns_like_a_rebuild():
     ea.close()  # leaves its target (lists built by aligns 3-5)
     b, cs_b, vs_b, eb = _cycle(ON, scan, cad, aligns=5)
     assert cs_b["adopted"] == 1 and cs_b["cached"] == 0, cs_b
+    assert cs_a["source_spec"] == "none" and cs_b["source_spec"] == "kept", (cs_a, cs_b)
     assert vs_b["lists"] > 0, vs_b  # the lists came with the target
     _same(a, ref)
     _same(b, ref)
@@ -118,3 +119,36 @@ def test_cache_release_and_multirank_contexts_skip_it():
     f = GICPEngine(options=ON)
     assert f.cache_stats()["cached"] == 0
     f.close()
+
+
+def test_source_grid_started_from_cached_target_is_checked():
+    """GICPState sets the source first: its grid starts from the cached target's cell size at set_source.
+    The target set next confirms it (kept) or the source's grid and covariances are rebuilt from the real
+    target (discarded); a second set_source before any target starts over.  Every form aligns exactly like
+    a cache-off engine."""
+    from leica_point_cloud_processing_amd.engine import GICPEngine
+
+    scan, cad, _ = _clouds()
+    _, _, _, x = _cycle(ON, scan, cad, aligns=1)
+    x.close()  # the cache holds cad
+    small = np.ascontiguousarray(cad[: len(cad) * 3 // 4])  # another target: other point count, other cell size
+    got, cs, _, y = _cycle(ON, scan, small)
+    assert cs["adopted"] == 0 and cs["source_spec"] == "discarded", cs
+    ref, _, _, z = _cycle(OFF, scan, small)
+    _same(got, ref)
+    y.close()  # the cache now holds `small`
+    z.close()
+    # two set_source calls before the target (the second one a different scan), then the cached target
+    e = GICPEngine(options=ON)
+    e.set_source_xyz(np.ascontiguousarray(scan[::2]))
+    e.set_source_xyz(scan)
+    e.set_target_xyz(small)
+    cs = e.cache_stats()
+    assert cs["adopted"] == 1 and cs["source_spec"] == "kept", cs
+    got = []
+    for _ in range(2):
+        T = e.align()
+        r = e.last_result
+        got.append((T, r["iterations"], r["n_evals"], r["n_corr"]))
+    e.close()
+    _same(got, ref)
