@@ -512,7 +512,11 @@ struct mgicp_ctx {
   // one stream for both clouds' launches: with a stream each the process exceeds its hardware queues
   // (GPU_MAX_HW_QUEUES, 4) and the main stream ends up sharing one with them (profiles/r04/prep7)
   hipStream_t aux_stream = nullptr;
-  hipEvent_t aux_ev[2] = {nullptr, nullptr};  // completion of the target's [0] / source's [1] launch
+  hipEvent_t aux_ev[3] = {nullptr, nullptr, nullptr};  // completion of the target's [0] / source's [1] launch,
+                                                       // [2] the source's Morton order sorted on the aux stream
+  bool qperm_aux = false;                    // qperm is being sorted on the aux stream (aux_ev[2])
+  DevBuf<uint32_t> aq_keys, aq_keys_sorted, aq_vals;  // its sort buffers (the main stream's may be busy)
+  DevBuf<unsigned char> aq_scratch;
   DevBuf<unsigned int> aux_cnt;     // their hand-off counts: [0] target, [1] source
   DevBuf<uint32_t> knn_fb2;         // the source's hand-off list
   bool knn_logged = true;           // wave-staged k-NN kernel + hand-off (debug option "knn_logged" 0: register-list only)
@@ -771,6 +775,7 @@ int reset_stamps(mgicp_ctx* ctx) {
 // Upload strided host records (or copy device records) and pack to float4 (original order).
 int build_grid(mgicp_ctx* ctx, Cloud& cl);
 const uint32_t* query_perm(mgicp_ctx* ctx);
+bool morton_perm(mgicp_ctx* ctx, const Cloud& c, size_t p0, size_t n, DevBuf<uint32_t>& out, bool aux);
 
 // the covariances started by cov_prep_async: wait for the aux stream, then hand the points the
 // logged kernel left (log overflow, ties at the k-th distance) to the register-list kernel on the
@@ -833,6 +838,17 @@ int cov_prep_async(mgicp_ctx* ctx, bool tgt) {
     HIPCK(hipMemsetAsync(ctx->aux_cnt.p + (tgt ? 0 : 1), 0, sizeof(unsigned int), ctx->stream));
   }
   HIPCK(hipStreamSynchronize(ctx->stream));  // the grid (and the count) before the aux stream reads them
+  // r05, the source guessed from the cached target (GICPState's order): its Morton query order is sorted
+  // on the aux stream ahead of its k-NN, so the main stream stays empty for set_target's upload (queued
+  // behind a main-stream sort that shares the CUs with the k-NN, the target's copies waited ~2 ms)
+  if (!tgt && ctx->src_spec == 1 && ctx->query_order && !ctx->qperm_valid && !ctx->qperm_aux) {
+    const size_t p0 = ctx->shard_p0(), ns = ctx->shard_p1() - p0;
+    if (ns > 0 && morton_perm(ctx, c, p0, ns, ctx->qperm, true)) {
+      HIPCK(hipEventRecord(ctx->aux_ev[2], ctx->aux_stream));
+      ctx->qperm_valid = true;
+      ctx->qperm_aux = true;
+    }
+  }
   HIPCK(launch_knn_cov(c.view, ctx->prm.k, ctx->prm.gicp_eps, 0, c.n, c.cov3(), nullptr,
                        ctx->knn_logged ? (tgt ? ctx->knn_fb.p : ctx->knn_fb2.p) : nullptr,
                        ctx->knn_logged ? ctx->aux_cnt.p + (tgt ? 0 : 1) : nullptr, ctx->aux_stream,
@@ -843,7 +859,7 @@ int cov_prep_async(mgicp_ctx* ctx, bool tgt) {
   (tgt ? ctx->tgt_cov_pending : ctx->src_cov_pending) = true;
   // r05: the source's 1-NN query order (a Morton sort of the shard) now, on the main stream beside the
   // covariances -- not inside the first align's loop
-  if (!tgt) (void)query_perm(ctx);
+  if (!tgt && !ctx->qperm_aux) (void)query_perm(ctx);
   return MGICP_OK;
 }
 
@@ -1294,27 +1310,34 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
 // Morton order of points [p0, p0 + n) of a grid-sorted cloud: a stable sort of 30-bit Morton codes
 // over the cloud's bbox.  Query order of the k-NN / 1-NN kernels (a wave's queries then form a
 // compact 3-D patch); results stay indexed by grid-sorted position.  false on failure.
-bool morton_perm(mgicp_ctx* ctx, const Cloud& c, size_t p0, size_t n, DevBuf<uint32_t>& out) {
-  hipStream_t s = ctx->stream;
+bool morton_perm(mgicp_ctx* ctx, const Cloud& c, size_t p0, size_t n, DevBuf<uint32_t>& out, bool aux) {
+  hipStream_t s = aux ? ctx->aux_stream : ctx->stream;
+  DevBuf<uint32_t>& keys = aux ? ctx->aq_keys : ctx->keys;
+  DevBuf<uint32_t>& keys_sorted = aux ? ctx->aq_keys_sorted : ctx->keys_sorted;
+  DevBuf<uint32_t>& vals = aux ? ctx->aq_vals : ctx->vals;
+  DevBuf<unsigned char>& scratch = aux ? ctx->aq_scratch : ctx->scratch;
   float ext = 0.f;
   for (int d = 0; d < 3; ++d) ext = std::max(ext, c.hi[d] - c.lo[d]);
   const float inv = ext > 0.f ? 1024.0f / (ext * 1.0001f) : 0.f;
-  if (out.reserve(n) != hipSuccess || ctx->keys.reserve(n) != hipSuccess ||
-      ctx->keys_sorted.reserve(n) != hipSuccess || ctx->vals.reserve(n) != hipSuccess)
+  if (out.reserve(n) != hipSuccess || keys.reserve(n) != hipSuccess ||
+      keys_sorted.reserve(n) != hipSuccess || vals.reserve(n) != hipSuccess)
     return false;
   const size_t sb = sort_scratch_bytes(n, 30);
-  if (ctx->scratch.reserve(sb) != hipSuccess) return false;
-  return launch_morton_keys(c.pts.p, p0, n, c.lo, inv, ctx->keys.p, ctx->vals.p, s) == hipSuccess &&
-         launch_sort_pairs(ctx->scratch.p, sb, ctx->keys.p, ctx->keys_sorted.p, ctx->vals.p, out.p, n, 30,
-                           s) == hipSuccess;
+  if (scratch.reserve(sb) != hipSuccess) return false;
+  return launch_morton_keys(c.pts.p, p0, n, c.lo, inv, keys.p, vals.p, s) == hipSuccess &&
+         launch_sort_pairs(scratch.p, sb, keys.p, keys_sorted.p, vals.p, out.p, n, 30, s) == hipSuccess;
 }
 
 // query order of the shard's 1-NN sweeps and source covariances (once per source cloud and shard)
 const uint32_t* query_perm(mgicp_ctx* ctx) {
   if (!ctx->query_order) return nullptr;
+  if (ctx->qperm_aux) {  // sorted on the aux stream at set_source: the main stream waits for it on the device
+    ctx->qperm_aux = false;
+    if (hipStreamWaitEvent(ctx->stream, ctx->aux_ev[2], 0) != hipSuccess) ctx->qperm_valid = false;
+  }
   if (ctx->qperm_valid) return ctx->qperm.p;
   const size_t p0 = ctx->shard_p0(), ns = ctx->shard_p1() - p0;
-  if (ns == 0 || !morton_perm(ctx, ctx->src, p0, ns, ctx->qperm)) return nullptr;
+  if (ns == 0 || !morton_perm(ctx, ctx->src, p0, ns, ctx->qperm, false)) return nullptr;
   ctx->qperm_valid = true;
   return ctx->qperm.p;
 }
@@ -2556,7 +2579,8 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
   if (ctx->async_tgt) se = hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking);
   if (ctx->async_tgt && (se != hipSuccess ||
                          hipEventCreateWithFlags(&ctx->aux_ev[0], hipEventDisableTiming) != hipSuccess ||
-                         hipEventCreateWithFlags(&ctx->aux_ev[1], hipEventDisableTiming) != hipSuccess)) {
+                         hipEventCreateWithFlags(&ctx->aux_ev[1], hipEventDisableTiming) != hipSuccess ||
+                         hipEventCreateWithFlags(&ctx->aux_ev[2], hipEventDisableTiming) != hipSuccess)) {
     if (ctx->aux_stream) (void)hipStreamDestroy(ctx->aux_stream);
     for (hipEvent_t& ev : ctx->aux_ev)
       if (ev) (void)hipEventDestroy(ev), ev = nullptr;
@@ -2606,6 +2630,7 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   }
   ctx->src_out.release();
   ctx->qperm.release();
+  ctx->aq_keys.release(); ctx->aq_keys_sorted.release(); ctx->aq_vals.release(); ctx->aq_scratch.release();
   ctx->partial.release(); ctx->red.release(); ctx->mpartial.release(); ctx->mred.release(); ctx->counts.release(); ctx->keys.release();
   ctx->keys_sorted.release(); ctx->vals.release(); ctx->scratch.release(); ctx->u64.release();
   ctx->fpartial.release();
