@@ -320,6 +320,10 @@ def main():
     scan, cad, T_true = gen_clouds(args)
     t_gen = time.time() - t_gen
 
+    if world > 1:
+        # a rank whose exchange never delivers fails the align within 30 s (library default 120 s), so the
+        # xGMI probe below can fall back to the host segment within the run
+        os.environ.setdefault("MGICP_REMOTE_DEADLINE_S", "30")
     t_c = time.perf_counter()
     eng = GICPEngine(device=local, max_iter=args.max_iter, fixed_iterations=int(args.fixed))
     ms_create = 1e3 * (time.perf_counter() - t_c)
@@ -360,6 +364,21 @@ def main():
                         transport = f"shm rows (xGMI exchange unavailable: {xerr or 'on another rank'}) + rccl"
                     else:
                         transport = "xGMI row exchange + device totals; shm rendezvous/gathers; rccl (target covariances)"
+                        # probe: one align on a strided 1/20 sample of the clouds through the exchange.  The
+                        # exchange has run only as processes sharing one GPU (no multi-GPU box was available
+                        # to this project): if rows written into peer GPUs' memory never show up there, every
+                        # rank falls back to the host segment (the same sums) instead of failing the run
+                        perr = None
+                        try:
+                            eng.set_source_xyz(np.ascontiguousarray(scan[::20]))
+                            eng.set_target_xyz(np.ascontiguousarray(cad[::20]))
+                            eng.align()
+                        except Exception as exc:  # noqa: BLE001 -- reported in the JSON line
+                            perr = str(exc)
+                        if pg.allreduce_max(1.0 if perr else 0.0) > 0:
+                            eng.attach_xgmi(False)
+                            transport = (f"shm rows (xGMI probe align failed: {perr or 'on another rank'}) + rccl "
+                                         "(target covariances)")
     eng.set_source_xyz(scan)
     eng.set_target_xyz(cad)
 

@@ -2045,7 +2045,20 @@ int correspond(mgicp_ctx* ctx, const Mat4& T, const Mat4& G, bool seed) {
                  1e3 * ctx->vl.c, ctx->vl.nx, ctx->vl.ny, ctx->vl.nz, c3[1], c3[2], st[0], hist_mean, p95, st[2], st[3],
                  c3[0], ctx->vl.pool_cap);
   }
-#if defined(MGICP_CORR_PHASES) && MGICP_CORR_PHASES
+#if defined(MGICP_VL_DIAG) && MGICP_VL_DIAG
+  {
+    unsigned long long ph[24];
+    HIPCK(hipStreamSynchronize(s));
+    HIPCK(corr_phase_take(ph));
+    const double c = ph[0] ? static_cast<double>(ph[0]) : 1.0;
+    if (ph[0] && sweep_listed(ctx))
+      std::fprintf(stderr, "[vl-build] cells %llu | per cell: candidates %.1f, stage-1 survivors %.1f, kept %.1f | cycles/cell "
+                   "gather %.0f, stage 1 %.0f, stage 2 %.0f | survivors <=8 %llu <=16 %llu <=32 %llu <=64 %llu <=128 %llu "
+                   "<=256 %llu >256 %llu | stage-2 cycles of cells with > 64 survivors: %.1f %%\n",
+                   ph[0], ph[1] / c, ph[2] / c, ph[3] / c, ph[4] / c, ph[5] / c, ph[6] / c, ph[9], ph[10], ph[11], ph[12],
+                   ph[13], ph[14], ph[8], ph[6] ? 100.0 * ph[15] / ph[6] : 0.0);
+  }
+#elif defined(MGICP_CORR_PHASES) && MGICP_CORR_PHASES
   {
     unsigned long long ph[24];
     HIPCK(hipStreamSynchronize(s));

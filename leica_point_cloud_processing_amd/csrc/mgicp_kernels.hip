@@ -59,6 +59,9 @@
 #ifndef MGICP_PACKED_RESID
 #define MGICP_PACKED_RESID 0  // 1: objective-pass residuals two per packed fp32 instruction (A/B: no gain, more spills; profiles/r02/ab_server)
 #endif
+#ifndef MGICP_VL_DIAG
+#define MGICP_VL_DIAG 0  // 1 (with MGICP_CORR_PHASES): per-stage counters and shader clocks of vl_build_kernel
+#endif
 #ifndef MGICP_CORR_PHASES
 #define MGICP_CORR_PHASES 0  // 1: per-phase shader-clock totals of the wave 1-NN sweep (diagnostic builds only)
 #endif
@@ -2386,6 +2389,9 @@ __global__ __launch_bounds__(64 * kVlWaves) void vl_build_kernel(GridView tg, VL
       if (lane == 0) v.cell[ci] = kVlReject;
       continue;
     }
+#if MGICP_VL_DIAG
+    unsigned long long vt0 = __builtin_amdgcn_s_memtime();
+#endif
     uint32_t ix, iy, iz;
     vl_cell_xyz(v, ci, ix, iy, iz);
     const uint32_t ii[3] = {ix, iy, iz};
@@ -2488,6 +2494,17 @@ __global__ __launch_bounds__(64 * kVlWaves) void vl_build_kernel(GridView tg, VL
       continue;
     }
     lds_wave_sync();
+#if MGICP_VL_DIAG
+    // [0] cells [1] candidates [2] stage-1 survivors [3] kept [4..7] cycles gather / stage 1 / stage 2 /
+    // write [8] survivors > 256 [9..14] survivors <= 8, 16, 32, 64, 128, 256 [15] stage-2 cycles of cells
+    // with > 64 survivors [16] rows scanned
+    unsigned long long vt1 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) {
+      atomicAdd(&g_corr_phase[0], 1ull);
+      atomicAdd(&g_corr_phase[1], static_cast<unsigned long long>(nc));
+      atomicAdd(&g_corr_phase[4], vt1 - vt0);
+    }
+#endif
     // anchors: the nearest candidate of each grown corner (box-centred float coordinates suffice:
     // any real point is a valid anchor) and the centre's 1-NN
     unsigned long long ak[8];
@@ -2561,6 +2578,15 @@ __global__ __launch_bounds__(64 * kVlWaves) void vl_build_kernel(GridView tg, VL
       ns += __builtin_popcountll(m);
       lds_wave_sync();
     }
+#if MGICP_VL_DIAG
+    unsigned long long vt2 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) {
+      atomicAdd(&g_corr_phase[2], static_cast<unsigned long long>(ns));
+      atomicAdd(&g_corr_phase[5], vt2 - vt1);
+      const int b = ns <= 8 ? 9 : ns <= 16 ? 10 : ns <= 32 ? 11 : ns <= 64 ? 12 : ns <= 128 ? 13 : ns <= 256 ? 14 : 8;
+      atomicAdd(&g_corr_phase[b], 1ull);
+    }
+#endif
     // stage 2: survivors against each other (up to 256 survivors; more are kept as they are, in a
     // long list)
     const bool pair = ns <= 256;
@@ -2598,6 +2624,14 @@ __global__ __launch_bounds__(64 * kVlWaves) void vl_build_kernel(GridView tg, VL
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) cntl += __shfl_xor(cntl, o, 64);
     cntl = __builtin_amdgcn_readfirstlane(cntl);
+#if MGICP_VL_DIAG
+    unsigned long long vt3 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) {
+      atomicAdd(&g_corr_phase[3], static_cast<unsigned long long>(cntl));
+      atomicAdd(&g_corr_phase[6], vt3 - vt2);
+      if (ns > 64) atomicAdd(&g_corr_phase[15], vt3 - vt2);
+    }
+#endif
     const bool lng = cntl >= static_cast<unsigned int>(kVlLong);
     const unsigned int cnt4 = ((cntl + 3u) & ~3u) + (lng ? 4u : 0u);
     // pool head: no reservation once the head has passed the cap, so the head exceeds the cap by at
