@@ -929,6 +929,8 @@ int upload_cloud(mgicp_ctx* ctx, Cloud& cl, const float* xyz, size_t n, size_t s
     const int rj = cov_join(ctx, &cl == &ctx->tgt);
     if (rj) return rj;
   }
+  if (&cl == &ctx->src && ctx->qperm_aux)  // the aux stream's Morton sort still reads the source's grid
+    HIPCK(hipStreamWaitEvent(ctx->stream, ctx->aux_ev[2], 0));
   if (&cl == &ctx->src && ctx->src_spec == 1) {  // a speculative grid is no "previous grid" of the new source
     cl.view.h = 0.f;
     cl.n_built = 0;
