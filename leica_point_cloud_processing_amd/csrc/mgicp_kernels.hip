@@ -1036,6 +1036,82 @@ struct SumCert {
 #ifndef MGICP_KNN_MINW
 #define MGICP_KNN_MINW 1  // A/B: resident waves per SIMD requested for the logged k-NN kernel (VGPR cap)
 #endif
+#ifndef MGICP_KNN_FLAT
+#define MGICP_KNN_FLAT 0  // r05 A/B (measured 1.856 vs 1.870 ms per 5M cloud, VALU -1.4 %: not kept as default)
+#endif
+
+#if MGICP_KNN_FLAT
+// r05: rings 0 and 1 of the logged k-NN search as ONE per-lane stream.  ring_search walks a ring's row
+// ranges one after the other, each in guarded batches of 8 to the wave's longest lane (MGICP_KNN_DIV:
+// 142 test iterations per wave for 71 tests per lane); here every lane loads the bounds of the 3 x 3 x 3
+// block's 9 rows at once (one round trip), keeps the non-empty ones, and walks them in batches of 8 at
+// its own pace -- the wave runs to the lane with the most batches, not to the sum of per-row maxima.
+// Candidates ring_search would prune by the current k-th distance are tested instead (they fail the
+// threshold): the k-NN set, the log's final selection and every covariance are unchanged.  The caller
+// continues with ring_search from ring 2 (which first checks whether ring 1 already proves the result).
+template <int K>
+__device__ __forceinline__ void knn_ring1_flat(const GridView& g, float qx, float qy, float qz, KthVisitor<K>& vis) {
+  const int cx = qcell(qx, g.ox, g.inv_h), cy = qcell(qy, g.oy, g.inv_h), cz = qcell(qz, g.oz, g.inv_h);
+  const int x0 = max(cx - 1, 0), x1 = min(cx + 1, g.nx - 1);
+  const int zdn = near_side(qz, g.oz, g.h, cz), ydn = near_side(qy, g.oy, g.h, cy);
+  // near-first row order: the query's own row, its face neighbours, then the edge rows
+  const int oz[9] = {0, 0, zdn, 0, -zdn, zdn, zdn, -zdn, -zdn};
+  const int oy[9] = {0, ydn, 0, -ydn, 0, ydn, -ydn, ydn, -ydn};
+  uint32_t ra[9], re[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const int z = cz + oz[k], y = cy + oy[k];
+    const bool in = z >= 0 && z < g.nz && y >= 0 && y < g.ny;
+    const uint32_t* row = g.cell_start + (static_cast<size_t>(in ? z : cz) * g.ny + (in ? y : cy)) * g.nx;
+    const uint32_t a = row[x0], b = row[x1 + 1];
+    ra[k] = in ? a : 0u;
+    re[k] = in ? b : 0u;
+  }
+  // the non-empty rows, compacted to the front (static register indexing only)
+  uint32_t ca[9], ce[9];
+  int nr = 0;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    ca[k] = 0u;
+    ce[k] = 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const bool ne = re[k] > ra[k];
+#pragma unroll
+    for (int t = 0; t <= k; ++t)
+      if (ne && nr == t) {
+        ca[t] = ra[k];
+        ce[t] = re[k];
+      }
+    nr += ne ? 1 : 0;
+  }
+  int r = 0;
+  uint32_t j = ca[0], e = ce[0];
+  for (;;) {
+    const bool act = r < nr;
+    if (__builtin_amdgcn_ballot_w64(act) == 0ull) break;
+    if (act) {
+      float4 pb[MGICP_KNN_RANGE_BATCH];
+#pragma unroll
+      for (int u = 0; u < MGICP_KNN_RANGE_BATCH; ++u) pb[u] = g.pts[min(j + u, e - 1)];
+#pragma unroll
+      for (int u = 0; u < MGICP_KNN_RANGE_BATCH; ++u)
+        if (j + u < e) vis.test(dist2(qx, qy, qz, pb[u]), pb[u].w, j + u);
+      j += MGICP_KNN_RANGE_BATCH;
+      if (j >= e) {
+        ++r;
+#pragma unroll
+        for (int t = 1; t < 9; ++t)
+          if (r == t) {
+            j = ca[t];
+            e = ce[t];
+          }
+      }
+    }
+  }
+}
+#endif
 template <int K>
 __global__ __launch_bounds__(64, MGICP_KNN_MINW) void knn_cov2_kernel(GridView g, double eps, size_t p0, size_t p1, Cov3 cov,
                                                       const uint32_t* __restrict__ perm, int nsent, int cap,
@@ -1055,7 +1131,12 @@ __global__ __launch_bounds__(64, MGICP_KNN_MINW) void knn_cov2_kernel(GridView g
   v1.pts = g.pts;
   v1.cap = cap;
   if (ring_cap >= 0) v1.ring_cap = ring_cap;
+#if MGICP_KNN_FLAT
+  knn_ring1_flat(g, q.x, q.y, q.z, v1);
+  ring_search(g, q.x, q.y, q.z, v1, 2);
+#else
   ring_search(g, q.x, q.y, q.z, v1);
+#endif
   // ring_cap (the source's head start, lazy mode): a point whose k-NN lie farther out (clutter, debris)
   // is left to the lazy pass, which computes it only if a sweep accepts it (ok_out stays 0)
   if (v1.gave_up) return;
