@@ -59,6 +59,9 @@
 #ifndef MGICP_PACKED_RESID
 #define MGICP_PACKED_RESID 0  // 1: objective-pass residuals two per packed fp32 instruction (A/B: no gain, more spills; profiles/r02/ab_server)
 #endif
+#ifndef MGICP_SRV_PREFETCH
+#define MGICP_SRV_PREFETCH 0  // r05 A/B: streamed-first server waves load their first group before the gate
+#endif
 #ifndef MGICP_VL_DIAG
 #define MGICP_VL_DIAG 0  // 1 (with MGICP_CORR_PHASES): per-stage counters and shader clocks of vl_build_kernel
 #endif
@@ -3647,6 +3650,9 @@ __global__ __launch_bounds__(64 * kWaves, 1) void fdf_server_kernel(
   static_assert(kR <= 4 && (kR == 4 || kR + kL <= 4), "resident groups: chunk 0, then chunk 1 only after a full chunk 0");
   __shared__ float4 lf[kWaves][kL][6][64];
   __shared__ double2 ld[kWaves][kL][12][64];
+#if MGICP_SRV_PREFETCH == 2
+  __shared__ float4 pf_lds[kWaves][64];  // dummy destination of the cache-warming LDS-DMA loads
+#endif
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int nw = gridDim.x * kWaves;
   const int w0 = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x * kWaves + wid));
@@ -3693,9 +3699,46 @@ __global__ __launch_bounds__(64 * kWaves, 1) void fdf_server_kernel(
   // others poll the mailbox block 0 forwards to.  1 = the host's pinned copy (PCIe reads by one
   // block); gridDim = a command block the host stores straight into device memory (BAR)
   const int host_pollers = kBench ? 0 : pollers;
+#if MGICP_SRV_PREFETCH
+  // r05 A/B: a wave that starts a pass with a streamed chunk (stagger) loads that chunk's first group
+  // before it waits at the gate, so the load's latency falls into the host round trip between passes
+  // (the streams do not change during a BFGS run; the group is only loaded early, the sums are the same)
+  const int nst_pf = w1 + nw < nch ? (nch - w1 - 1) / nw : 0;
+  const int split_pf = MGICP_SRV_STAGGER == 2 ? (wid * nst_pf + kWaves / 2) / kWaves
+                                              : (MGICP_SRV_STAGGER == 1 && (wid & 1) ? nst_pf : 0);
+  const int wpf = w1 + nw;
+#if MGICP_SRV_PREFETCH == 1
+  const uint32_t ipf = wpf < nch ? chunk_g0(wpf) + lane : 0u;
+  const bool pf_ok = split_pf > 0 && wpf < nch && ipf < chunk_g1(ccnt, wpf);
+  CorrGroup pf;
+#endif
+#endif
   for (unsigned long long seq = seq0;; ++seq) {
     Xf34 A = Abench;
     int rev = 0;
+#if MGICP_SRV_PREFETCH == 1
+    if (pf_ok) load_group(c, ipf, pf);
+#elif MGICP_SRV_PREFETCH == 2
+    // mode 2: warm the caches with the group through LDS-DMA loads into a dummy LDS row (no VGPRs: the
+    // server's 512 registers are taken by its resident groups)
+#if defined(__HIP_DEVICE_COMPILE__)  // (the builtin exists in the device pass only)
+    if (split_pf > 0 && wpf < nch) {  // (recomputed per pass: no register held across the loop)
+      uint32_t lo = static_cast<uint32_t>(lane);
+      asm volatile("" : "+v"(lo));  // the addresses are formed here each pass, not hoisted out of the loop
+      const uint32_t ipf = chunk_g0(wpf) + lo;
+      const float* fs[6] = {c.sx, c.sy, c.sz, c.qx, c.qy, c.qz};
+      const double* ms[6] = {c.m00, c.m01, c.m02, c.m11, c.m12, c.m22};
+#pragma unroll
+      for (int e = 0; e < 6; ++e)
+        __builtin_amdgcn_global_load_lds(const_cast<float*>(fs[e] + 4 * static_cast<size_t>(ipf)), &pf_lds[wid][0], 16, 0, 0);
+#pragma unroll
+      for (int e = 0; e < 6; ++e) {
+        __builtin_amdgcn_global_load_lds(const_cast<double*>(ms[e] + 4 * static_cast<size_t>(ipf)), &pf_lds[wid][0], 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(const_cast<double*>(ms[e] + 4 * static_cast<size_t>(ipf) + 2), &pf_lds[wid][0], 16, 0, 0);
+      }
+    }
+#endif
+#endif
     // the timing form stamps rows with seq | 2^31 (align passes stamp their pass index, < 2^31)
     unsigned int rstamp = static_cast<unsigned int>(seq) | 0x80000000u;
     if (!(kBench && seq == seq0) && !pass_gate(seq, cmd, mail, timeout, nullptr, host_pollers, A, rev, rstamp))
@@ -3723,9 +3766,18 @@ __global__ __launch_bounds__(64 * kWaves, 1) void fdf_server_kernel(
 #pragma unroll
         for (int v = 0; v < kRedVals; ++v) acc[v] = 0.0;
         const uint32_t g1 = chunk_g1(ccnt, w);
+#if MGICP_SRV_PREFETCH == 1
+        bool first = w == wpf && pf_ok;
+#endif
         for (uint32_t i = chunk_g0(w) + lane; i < g1; i += 64) {
           CorrGroup g;
+#if MGICP_SRV_PREFETCH == 1
+          if (first) g = pf;
+          else load_group(c, i, g);
+          first = false;
+#else
           load_group(c, i, g);
+#endif
           fdf_group(A, g, acc);
         }
         store(w, acc);
