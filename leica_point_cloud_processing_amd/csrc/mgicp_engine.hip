@@ -48,6 +48,9 @@ double now_ms() {
       .count();
 }
 
+#ifndef MGICP_ASYNC_RING_CAP
+#define MGICP_ASYNC_RING_CAP 4  // rings the lazy source's head-start k-NN searches before leaving a point to the lazy pass
+#endif
 #ifndef MGICP_PASS_DIAG
 #define MGICP_PASS_DIAG 0
 #endif
@@ -508,7 +511,7 @@ struct mgicp_ctx {
   bool tgt_cov_pending = false;     // the aux stream's covariance launches not joined yet
   bool src_cov_pending = false;
   bool src_async_lazy = false;      // the source's launch was ring-capped (lazy mode): the rest stays lazy
-  int async_ring_cap = 4;           // rings the source's head start searches (lazy mode)
+  int async_ring_cap = MGICP_ASYNC_RING_CAP;  // rings the source's head start searches (lazy mode)
   // one stream for both clouds' launches: with a stream each the process exceeds its hardware queues
   // (GPU_MAX_HW_QUEUES, 4) and the main stream ends up sharing one with them (profiles/r04/prep7)
   hipStream_t aux_stream = nullptr;

@@ -237,6 +237,25 @@ __device__ __forceinline__ void ring_search(const GridView& g, float qx, float q
   }
 }
 
+// r05: true when the grid's empty-space map proves that no point lies within sqrt(thr) of q -- the bound
+// ring_search checks first (rings closer than the nearest non-empty cell hold no point; L = the distance
+// to the faces of that empty box, shrunk by the same margins), so a query the gate must reject (scan
+// clutter centimetres off the part) skips its seeds and the gate-sized ball search of the 1-NN sweeps
+__device__ __forceinline__ bool empty_reject(const GridView& g, float qx, float qy, float qz, double thr) {
+  if (!g.empty_dist) return false;
+  const int cx = qcell(qx, g.ox, g.inv_h), cy = qcell(qy, g.oy, g.inv_h), cz = qcell(qz, g.oz, g.inv_h);
+  int r = max(max(dist_out(cx, g.nx), dist_out(cy, g.ny)), dist_out(cz, g.nz));
+  if (r == 0)
+    r = g.empty_dist[static_cast<size_t>(cx) +
+                     static_cast<size_t>(g.nx) * (static_cast<size_t>(cy) + static_cast<size_t>(g.ny) * cz)];
+  if (r <= 0) return false;
+  const float L = fminf(fminf(axis_bound(qx, g.ox, g.h, cx, r - 1, g.nx), axis_bound(qy, g.oy, g.h, cy, r - 1, g.ny)),
+                        axis_bound(qz, g.oz, g.h, cz, r - 1, g.nz));
+  if (L == INFINITY) return true;  // every cell lies in the empty box: the grid holds no point at all
+  const float Ls = L * 0.99999f - g.slop;
+  return Ls > 0.f && static_cast<double>(Ls) * static_cast<double>(Ls) >= thr;
+}
+
 // lower bound of the distance from q to a point box [lo, hi] (component-wise, each gap shrunk by
 // the rounding slop); an empty cell's sentinel box (lo = +INF, hi = -INF) gives +INF
 __device__ __forceinline__ float box_gap2(float qx, float qy, float qz, const float4& lo, const float4& hi,
@@ -1832,11 +1851,12 @@ __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_wave_kernel(
     xform(T, s.x, s.y, s.z, qx, qy, qz);
   }
   vis.init(qx, qy, qz, thr);
-  if (live) seed_query(tg, seeded, seeded ? nn_pos[p - p0] : 0xffffffffu, qx, qy, qz, vis);
+  const bool rej = live && empty_reject(tg, qx, qy, qz, thr);  // no candidate, no union box, no finish
+  if (live && !rej) seed_query(tg, seeded, seeded ? nn_pos[p - p0] : 0xffffffffu, qx, qy, qz, vis);
   MGICP_PH(0);
   // ---- the union box of the included lanes' seed balls
   const float bd0 = vis.prune2();
-  bool incl = live && bd0 <= rcap2;
+  bool incl = live && !rej && bd0 <= rcap2;
   int zl = INT_MAX, zh = INT_MIN, yl = INT_MAX, yh = INT_MIN, xl = INT_MAX, xh = INT_MIN;
   float rsum = 0.f;
   if (incl) {
@@ -2047,7 +2067,7 @@ __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_wave_kernel(
   MGICP_PH(3);
   // ---- lanes the union scan did not settle (not included, or a tie between two distinct points
   // at the scan minimum): the per-lane exact search from their best
-  const bool fin = live && (!incl || tie);
+  const bool fin = live && !rej && (!incl || tie);
 #if MGICP_CORR_PHASES
   {
     const int nf = __builtin_popcountll(__builtin_amdgcn_ballot_w64(fin));
@@ -2762,9 +2782,11 @@ __global__ __launch_bounds__(256) void vl_fallback_kernel(GridView tg, VListView
     xform(T, s.x, s.y, s.z, qx, qy, qz);
     NnVisitor vis;
     vis.init(qx, qy, qz, thr);
-    seed_query(tg, seeded, seeded ? nn_pos[k] : 0xffffffffu, qx, qy, qz, vis);
-    if (vis.best != ~0ull) box_search(tg, qx, qy, qz, vis);
-    else ring_search(tg, qx, qy, qz, vis);
+    if (!empty_reject(tg, qx, qy, qz, thr)) {  // r05: no point within the gate: rejected without a search
+      seed_query(tg, seeded, seeded ? nn_pos[k] : 0xffffffffu, qx, qy, qz, vis);
+      if (vis.best != ~0ull) box_search(tg, qx, qy, qz, vis);
+      else ring_search(tg, qx, qy, qz, vis);
+    }
     const bool ok = vis.best != ~0ull &&
                     static_cast<double>(__uint_as_float(static_cast<uint32_t>(vis.best >> 32))) < thr;
     nn_pos[k] = ok ? vis.pos : 0xffffffffu;

@@ -1,6 +1,6 @@
 """r05: the reference's call pattern at C4 -- a fresh context, set_source, set_target, align, align
 (GICPState's cycle + the unit test's iterate()) -- repeated; per align the loop time and iterations.
-usage: [MGICP_LIB_NAME=...] python3 scripts/r05/cold_pair.py [reps]"""
+usage: [MGICP_LIB_NAME=...] python3 scripts/r05/cold_pair.py [reps] [C4F]"""
 import os, sys, time, json
 sys.path.insert(0, os.getcwd())
 import numpy as np
@@ -8,7 +8,8 @@ from leica_point_cloud_processing_amd import synth
 from leica_point_cloud_processing_amd.engine import GICPEngine
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 4
-scan, cad, _ = synth.scan_vs_cad(5_000_000, 5_000_000)
+c4f = len(sys.argv) > 2 and sys.argv[2] == "C4F"  # the gate-rejecting workload (clutter + debris)
+scan, cad, _ = synth.scan_vs_cad(5_000_000, 5_000_000, clutter=0.04 if c4f else 0.0, debris=40_000 if c4f else 0)
 out = []
 for r in range(reps):
     e = GICPEngine()

@@ -1,0 +1,11 @@
+# r05: empty-space early rejection in the 1-NN sweeps -- the sweep / parity tests, then C4F and C4 GICPState cycles
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/r05/${1:-rej}; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests/test_gicp_gpu.py tests/test_full_size_gpu.py tests/test_parity_configs_gpu.py tests/test_target_cache.py -x -v --timeout 300 --timeout-method thread -m gpu -k "vlist or c4f or C4F or C2F or gate or correspond or sweep or brute or fused or cache or oracle or lazy" > $O/pytest.log 2>&1 || { echo "pytest failed"; grep -E "FAILED|Error" $O/pytest.log | head; tail -20 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+for w in C4F C4; do
+  timeout -k 10 200 python scripts/r05/cold_pair.py 3 $w > $O/cold_$w.txt 2>&1 || { echo "cold $w failed"; tail -20 $O/cold_$w.txt; exit 1; }
+  echo "$w: $(head -1 $O/cold_$w.txt)"
+  echo "$w: $(tail -1 $O/cold_$w.txt)"
+done
