@@ -48,6 +48,9 @@ double now_ms() {
       .count();
 }
 
+#ifndef MGICP_CORR_FAR_SPLIT
+#define MGICP_CORR_FAR_SPLIT 0  // r05 A/B (debug option "corr_far_split"): far stragglers of in-place waves to the finish kernel
+#endif
 #ifndef MGICP_ASYNC_RING_CAP
 #define MGICP_ASYNC_RING_CAP 4  // rings the lazy source's head-start k-NN searches before leaving a point to the lazy pass
 #endif
@@ -437,6 +440,7 @@ struct mgicp_ctx {
   int corr_split = 0;                   // waves of the wave sweep with <= this many stragglers hand them to a kernel of
                                         // their own (MGICP_CORR_SPLIT; 0 = every straggler finishes in place)
   float corr_rcap = 5.f;                // cells: lanes with a larger seed bound search alone (MGICP_CORR_RCAP)
+  bool corr_far_split = MGICP_CORR_FAR_SPLIT;  // r05: far stragglers of in-place waves to the finish kernel
   // r03 A/B (profiles/r03/corrsweep): union boxes of <= 96 rows and 16 cells along x, for waves whose
   // mean seed bound is >= 1.25 cells (the first sweep mostly): 2455 -> 2300 us per C4 align's sweeps
   int corr_max_rows = 96;               // union boxes with more rows / x cells: per-lane search
@@ -1977,7 +1981,7 @@ hipError_t launch_sweep(mgicp_ctx* ctx, const Mat4& T, double thr, bool seeded, 
   if (ctx->corr_wave && g.pairs) {
     const float rc = ctx->corr_rcap * g.h;
     void* work = nullptr;
-    if (ctx->corr_split > 0) {
+    if (ctx->corr_split > 0 || ctx->corr_far_split) {
       hipError_t e = ctx->nn_work.reserve(nn_work_bytes(p1 - p0));
       if (e == hipSuccess) e = ctx->nn_work_n.reserve(1);
       if (e != hipSuccess) return e;
@@ -1985,7 +1989,8 @@ hipError_t launch_sweep(mgicp_ctx* ctx, const Mat4& T, double thr, bool seeded, 
     }
     return launch_correspond_wave(g, ctx->d_out, p0, p1, T.xf(), thr, seeded ? 1 : 0, ctx->prev_pos.p,
                                   ctx->flags.p, qp, rc * rc, ctx->corr_max_rows, ctx->corr_max_x, ctx->corr_union_min_r,
-                                  work, ctx->nn_work_n.p, ctx->corr_split, ctx->corr_lds_pts, ctx->stream);
+                                  work, ctx->nn_work_n.p, ctx->corr_split, ctx->corr_lds_pts, ctx->stream,
+                                  ctx->corr_far_split ? 1 : 0);
   }
   return launch_correspond(g, ctx->d_out, p0, p1, T.xf(), thr, seeded ? 1 : 0, ctx->prev_pos.p, ctx->flags.p, qp,
                            ctx->stream);
@@ -3738,6 +3743,7 @@ int mgicp_debug_option(mgicp_ctx* ctx, const char* name, double value) {
   else if (n == "vlist_stats") ctx->vl_stats = on;      // per-sweep list statistics on stderr
   else if (n == "fuse_compact") ctx->fuse_compact = on; // compaction fused into listed sweeps
   else if (n == "target_cache") ctx->tcache_on = on;    // adopt / leave the target state (process cache)
+  else if (n == "corr_far_split") ctx->corr_far_split = on;  // far stragglers of the cold sweep to the finish kernel
   else if (n == "grid_occ") {                           // grid sizing (points per non-empty cell), next set_*
     if (!(value >= 1.0 && value <= 256.0)) return fail(ctx, MGICP_E_INVALID, "grid_occ must be in [1, 256]");
     ctx->occupancy = value;

@@ -1832,7 +1832,7 @@ __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_wave_kernel(
     GridView tg, const float4* __restrict__ src, size_t p0, size_t p1, Xf34 T, double thr, int seeded,
     uint32_t* __restrict__ nn_pos, uint32_t* __restrict__ flags, const uint32_t* __restrict__ qperm, float rcap2,
     int max_rows, int max_xcells, float union_min_r, NnWork* __restrict__ work, unsigned int* __restrict__ work_n,
-    int split_max, int lds_cap) {
+    int split_max, int lds_cap, int far_split) {
   __shared__ f4v stage[4][2 * kStagePairs];
   // small-ball waves: the union box's cell bounds, row offsets and points (dynamic LDS, lds_cap
   // points per wave; 0 = off)
@@ -2094,11 +2094,25 @@ __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_wave_kernel(
     MGICP_PH(4);
     if (!live || fin) return;
   } else {
-    if (fin) {
+    // r05 (far_split): a wave finishing in place hands its FAR stragglers (bound beyond rcap: scan debris
+    // and clutter a few centimetres off the part, which the gate may still accept) to the finish kernel,
+    // so its near lanes do not wait for their ball searches; the far ones run there in waves of their own
+    const bool far = far_split && work && fin && vis.prune2() > rcap2;
+    const unsigned long long farm = __builtin_amdgcn_ballot_w64(far);
+    if (farm) {
+      unsigned int base = 0;
+      if (lane == 0) base = atomicAdd(work_n, static_cast<unsigned int>(__builtin_popcountll(farm)));
+      base = __builtin_amdgcn_readfirstlane(base);
+      const unsigned int off = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned int>(farm >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo(static_cast<unsigned int>(farm), 0u));
+      if (far) work[base + off] = NnWork{static_cast<uint32_t>(p - p0), vis.pos, vis.best};
+    }
+    if (fin && !far) {
       if (vis.best != ~0ull) box_search(tg, qx, qy, qz, vis);
       else ring_search(tg, qx, qy, qz, vis);
     }
     MGICP_PH(4);
+    if (far) return;
   }
   if (!live) return;
   const bool ok = vis.best != ~0ull &&
@@ -4491,7 +4505,7 @@ hipError_t launch_correspond(const GridView& tgt, const float4* src, size_t p0, 
 hipError_t launch_correspond_wave(const GridView& tgt, const float4* src, size_t p0, size_t p1, Xf34 T,
                                   double thr, int seeded, uint32_t* nn_pos, uint32_t* flags, const uint32_t* qperm,
                                   float rcap2, int max_rows, int max_xcells, float union_min_r, void* work,
-                                  unsigned int* work_n, int split_max, int lds_cap, hipStream_t s) {
+                                  unsigned int* work_n, int split_max, int lds_cap, hipStream_t s, int far_split) {
   if (p1 <= p0) return hipSuccess;
   if (!tgt.pairs || (work && !work_n)) return hipErrorInvalidValue;
   NnWork* w = static_cast<NnWork*>(work);
@@ -4503,7 +4517,7 @@ hipError_t launch_correspond_wave(const GridView& tgt, const float4* src, size_t
   const size_t shm = lds_cap ? 4 * static_cast<size_t>(std::max(lds_cap, 0) + kLdsMeta) * sizeof(float4) : 0;
   correspond_wave_kernel<<<nblk(p1 - p0), 256, shm, s>>>(tgt, src, p0, p1, T, thr, seeded, nn_pos, flags, qperm,
                                                          rcap2, max_rows, max_xcells, union_min_r, w, work_n,
-                                                         split_max, lds_cap);
+                                                         split_max, lds_cap, far_split);
   if (w) {
     // grid-stride over the stragglers: 8 blocks of 4 waves per CU (the count is known on the device only)
     const unsigned int nb = static_cast<unsigned int>(std::min<size_t>(nblk(p1 - p0), 2048));

@@ -12,7 +12,9 @@ c4f = len(sys.argv) > 2 and sys.argv[2] == "C4F"  # the gate-rejecting workload 
 scan, cad, _ = synth.scan_vs_cad(5_000_000, 5_000_000, clutter=0.04 if c4f else 0.0, debris=40_000 if c4f else 0)
 out = []
 for r in range(reps):
-    e = GICPEngine()
+    # MGICP_COLD_OPTS="name=value,...": debug options of the engines (A/B runs)
+    opts = {k: float(v) for k, v in (kv.split("=") for kv in os.environ.get("MGICP_COLD_OPTS", "").split(",") if kv)}
+    e = GICPEngine(options=opts)
     t0 = time.perf_counter()
     e.set_source_xyz(scan)
     t1 = time.perf_counter()

@@ -695,3 +695,36 @@ def test_growing_clouds_reuse_buffers_bitwise(engine_mod):
         assert e.last_result["iterations"] == f.last_result["iterations"]
         f.close()
     e.close()
+
+
+def test_far_straggler_handoff_matches_in_place(engine_mod, part_small):
+    """r05: the cold sweep hands the far stragglers of in-place waves (seed bound beyond rcap: debris and
+    clutter centimetres off the part) to the finish kernel.  Seeded and unseeded cold sweeps at several
+    transforms (far-off, converged) and two aligns equal the all-in-place form (debug option
+    "corr_far_split" 0) index for index and matrix for matrix; the clutter case has gate rejections."""
+    name, src, tgt, Ttrue = _vlist_cases(part_small)[1]  # clutter + debris: gate rejections
+    Tinv = np.linalg.inv(Ttrue).astype(np.float32)
+    I = np.eye(4, dtype=np.float32)
+    off = np.eye(4, dtype=np.float32)
+    off[:3, 3] = [0.004, -0.003, 0.02]
+    res = {}
+    for split in (1, 0):
+        e = engine_mod(options={"vlist": 0, "corr_far_split": split})
+        e.set_target_xyz(tgt)
+        e.set_source_xyz(src)
+        sweeps = [e.debug_correspondences(T, len(src)) for T in (I, off, Tinv)]
+        sweeps += [e.debug_correspondences_seeded(T, len(src)) for T in (off, Tinv, I)]
+        aligns = []
+        for _ in range(2):
+            T = e.align()
+            aligns.append((T, e.last_result["iterations"], e.last_result["n_evals"], e.last_result["n_corr"]))
+        e.close()
+        res[split] = (sweeps, aligns)
+    assert any(m < len(src) for m, _, _ in res[1][0])  # the gate rejects points in these sweeps
+    for (ma, ta, Ma), (mb, tb, Mb) in zip(res[1][0], res[0][0]):
+        assert ma == mb
+        np.testing.assert_array_equal(ta, tb)
+        np.testing.assert_array_equal(Ma, Mb)
+    for (Ta, *ra), (Tb, *rb) in zip(res[1][1], res[0][1]):
+        np.testing.assert_array_equal(Ta, Tb)
+        assert ra == rb
