@@ -10,10 +10,18 @@ HIPFLAGS := -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -ffp-contract=off -Wall 
 
 all: $(LIB) oracle adapter-example adapter-replay
 
-$(LIB): $(SRCS) $(HDRS)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS) -lrccl
+OBJDIR := $(PKG)/csrc/build
+OBJS  := $(OBJDIR)/mgicp_kernels.o $(OBJDIR)/mgicp_engine.o
 
-# A/B builds: make variant NAME=w8 DEFS=-DMGICP_CORR_WAVES=8 -> libmgicp_w8.so (MGICP_LIB_NAME selects it)
+# one object per source (make -j2 compiles both at once; an engine edit does not rebuild the kernels)
+$(OBJDIR)/%.o: $(PKG)/csrc/%.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(LIB): $(OBJS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJS) -lrccl
+
+# diagnostic builds: make variant NAME=diag DEFS=-DMGICP_CORR_PHASES=1 -> libmgicp_diag.so (MGICP_LIB_NAME selects it)
 variant: $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) $(DEFS) -shared -o $(PKG)/libmgicp_$(NAME).so $(SRCS) -lrccl
 
@@ -42,7 +50,7 @@ oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -f $(LIB) $(PKG)/libmgicp_*.so
+	rm -f $(LIB) $(PKG)/libmgicp_*.so $(OBJS)
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean adapter-example adapter-replay variant

@@ -102,6 +102,9 @@ def parse():
                     help="N > 1: per-pass super rows into every rank's IPC-mapped device buffer over xGMI with a "
                          "totaler wave per rank (r05 default), or through the node-wide shared host segment "
                          "(every host totals), or one RCCL all-gather per pass")
+    ap.add_argument("--no-rccl", action="store_true",
+                    help="N > 1: skip RCCL (the path a failed ncclCommInitRank falls back to: RCCL-free shards, "
+                         "target covariances on every rank, rows through the segment / xGMI)")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
     args.n_source = args.n_source or cfg["n_source"]
@@ -328,57 +331,18 @@ def main():
     eng = GICPEngine(device=local, max_iter=args.max_iter, fixed_iterations=int(args.fixed))
     ms_create = 1e3 * (time.perf_counter() - t_c)
     transport = "local"
+    transport_notes = []
     if world > 1:
-        uid = pg.broadcast(GICPEngine.unique_id() if rank == 0 else None)
-        eng.comm_init(world, rank, uid)
-        transport = "rccl"
-        if args.transport in ("shm", "xgmi"):
-            # the node-wide row segment: every rank's resident server writes its supers there, every
-            # host takes the fixed-order total (no collective per pass); RCCL keeps the one-time
-            # target-covariance all-gather.  Any rank failing to attach -> every rank stays on RCCL.
-            import secrets
+        # RCCL (target covariances), the node-wide row segment and the xGMI exchange, each agreed by every
+        # rank; RCCL or xGMI failing degrades to the next form instead of failing the run (VERDICT r05
+        # item 7, parallel.setup_transport)
+        from leica_point_cloud_processing_amd.parallel import setup_transport
 
-            name = pg.broadcast(f"/mgicp_{os.getpid()}_{secrets.token_hex(6)}".encode() if rank == 0 else None)
-            err = None
-            try:
-                eng.attach_shm(name.decode(), args.n_source)
-            except Exception as exc:  # noqa: BLE001 -- reported in the JSON line, RCCL path kept
-                err = str(exc)
-            if pg.allreduce_max(1.0 if err else 0.0) > 0:
-                if not err:
-                    eng.detach_shm()
-                transport = f"rccl (shared segment unavailable: {err or 'on another rank'})"
-            else:
-                transport = "shm rows + rccl (target covariances)"
-                if args.transport == "xgmi":
-                    # the rows over xGMI (the segment stays as its rendezvous and for the once-per-iteration
-                    # gathers); any rank failing -> every rank keeps the host segment
-                    xerr = None
-                    try:
-                        eng.attach_xgmi()
-                    except Exception as exc:  # noqa: BLE001 -- reported in the JSON line
-                        xerr = str(exc)
-                    if pg.allreduce_max(1.0 if xerr else 0.0) > 0:
-                        if not xerr:
-                            eng.attach_xgmi(False)
-                        transport = f"shm rows (xGMI exchange unavailable: {xerr or 'on another rank'}) + rccl"
-                    else:
-                        transport = "xGMI row exchange + device totals; shm rendezvous/gathers; rccl (target covariances)"
-                        # probe: one align on a strided 1/20 sample of the clouds through the exchange.  The
-                        # exchange has run only as processes sharing one GPU (no multi-GPU box was available
-                        # to this project): if rows written into peer GPUs' memory never show up there, every
-                        # rank falls back to the host segment (the same sums) instead of failing the run
-                        perr = None
-                        try:
-                            eng.set_source_xyz(np.ascontiguousarray(scan[::20]))
-                            eng.set_target_xyz(np.ascontiguousarray(cad[::20]))
-                            eng.align()
-                        except Exception as exc:  # noqa: BLE001 -- reported in the JSON line
-                            perr = str(exc)
-                        if pg.allreduce_max(1.0 if perr else 0.0) > 0:
-                            eng.attach_xgmi(False)
-                            transport = (f"shm rows (xGMI probe align failed: {perr or 'on another rank'}) + rccl "
-                                         "(target covariances)")
+        probe = (np.ascontiguousarray(scan[::20]), np.ascontiguousarray(cad[::20]))
+        tr = setup_transport(eng, pg, world, rank, args.transport, args.n_source, probe=probe,
+                             force_rccl_fail=bool(args.no_rccl))
+        transport = tr["transport"]
+        transport_notes = tr["notes"]
     eng.set_source_xyz(scan)
     eng.set_target_xyz(cad)
 
@@ -548,7 +512,7 @@ def main():
             reps.append({"ms_set_source": round(1e3 * (t_b - t_a), 3), "ms_set_target": round(1e3 * (t_c2 - t_b), 3),
                          "ms_to_converge_first": round(1e3 * (t_c2 - t_a) + aligns[0]["ms_wall"], 3),
                          "align": aligns, "frob_vs_timed": float(np.linalg.norm(
-                             T_cp.astype(np.float64) - eng.getFinalTransformation().astype(np.float64)))})
+                             T_cp.astype(np.float64) - T_final.astype(np.float64)))})
             e4.close()
 
         def med(f):
@@ -580,7 +544,8 @@ def main():
         GICPEngine.release_cache()
         cyc = []
         for c in range(5):
-            e6 = GICPEngine(device=local, max_iter=args.max_iter, fixed_iterations=int(args.fixed))
+            e6 = GICPEngine(device=local, max_iter=args.max_iter, fixed_iterations=int(args.fixed),
+                            options={"target_cache": 1})  # r06: the cache is opt-in
             t_a = time.perf_counter()
             e6.set_source_xyz(scan)
             e6.set_target_xyz(cad)
@@ -599,7 +564,7 @@ def main():
             cyc.append({"cycle": c + 1, "target_adopted": bool(adopted), "ms_set_clouds": round(1e3 * (t_b - t_a), 3),
                         "ms_to_converge_first": round(1e3 * (t_b - t_a) + al[0]["ms_wall"], 3), "align": al,
                         "frob_vs_timed": float(np.linalg.norm(T_c.astype(np.float64) -
-                                                              eng.getFinalTransformation().astype(np.float64)))})
+                                                              T_final.astype(np.float64)))})
         GICPEngine.release_cache()
         steady = cyc[1:]
         gicpstate = {
@@ -863,6 +828,7 @@ def main():
             "n_target": args.n_target,
             "parallelism": f"source point-range shards x{world}, target replicated",
             "transport": transport,
+            "transport_notes": transport_notes,
         },
         "iterations_per_align": iters_per_align,
         "n_corr": result["n_corr"],

@@ -80,10 +80,13 @@ int         mgicp_create(mgicp_ctx** ctx, const mgicp_params* p);
 int         mgicp_set_params(mgicp_ctx* ctx, const mgicp_params* p);
 const char* mgicp_last_error(const mgicp_ctx* ctx);
 void        mgicp_destroy(mgicp_ctx* ctx);
-/* r05 target cache: mgicp_destroy leaves a single-rank context's target state (grid, covariances,
- * 1-NN cell lists; ~2-3.5 GB at 5M points) in a process-wide cache, one entry per device; a later
- * set_target whose points equal the cached ones bit for bit (compared on the device) adopts it instead
- * of rebuilding -- results are those of a rebuild bit for bit.  This frees every cached entry. */
+/* r05 target cache (r06: OPT-IN per context, debug option "target_cache" 1; off by default because the
+ * reference node aligns once per process): mgicp_destroy leaves such a single-rank context's target state
+ * (grid, covariances, 1-NN cell lists; ~0.5-3 GB at 5M points) in a process-wide cache, one entry per
+ * device; a later opted-in set_target whose points equal the cached ones bit for bit (compared on the
+ * device) adopts it instead of rebuilding -- results are those of a rebuild bit for bit.  A device
+ * allocation that runs out of memory evicts the device's entry and retries once.  This frees every
+ * cached entry. */
 void        mgicp_release_cache(void);
 int         mgicp_device_count(int* n);
 
@@ -275,7 +278,7 @@ int mgicp_set_profiling(mgicp_ctx* ctx, int on);
 /* test / diagnostic forms of the engine, set explicitly on one context (never through the
  * environment): "resident", "host_rows", "srv_cus", "fused_finish", "gated", "bar_cmd" (the
  * objective-pass path), "async_cov", "lazy_src_cov", "knn_logged" (covariances), "vlist",
- * "vlist_cold", "vlist_eager", "vlist_stats", "fuse_compact" (1-NN cell lists), "corr_far_split" (cold 1-NN sweep),
+ * "vlist_cold", "vlist_eager", "vlist_stats", "fuse_compact" (1-NN cell lists),
  * "target_cache", "grid_occ" (grid
  * sizing of the next set_*).  Every form gives the default path's results bit for bit (the GPU tests
  * that pin each one: INTEGRATION.md "Debug options"); MGICP_E_INVALID for an unknown name. */
@@ -284,7 +287,7 @@ int mgicp_debug_option(mgicp_ctx* ctx, const char* name, double value);
  * adoptions and out[2] donations on this device so far, out[3] an entry is cached on this device,
  * out[4] a source set before any target started its grid from the cached target's cell size: 0 no,
  * 1 pending, 2 kept (the target set next had that cell size), 3 discarded and rebuilt.
- * Debug option "target_cache" 0: this context neither adopts nor leaves a target. */
+ * Debug option "target_cache" 1: this context adopts and leaves targets (default 0: neither). */
 int mgicp_debug_cache_stats(mgicp_ctx* ctx, long long out[5]);
 
 #ifdef __cplusplus

@@ -48,9 +48,6 @@ double now_ms() {
       .count();
 }
 
-#ifndef MGICP_CORR_FAR_SPLIT
-#define MGICP_CORR_FAR_SPLIT 0  // r05 A/B (debug option "corr_far_split"): far stragglers of in-place waves to the finish kernel
-#endif
 #ifndef MGICP_ASYNC_RING_CAP
 #define MGICP_ASYNC_RING_CAP 4  // rings the lazy source's head-start k-NN searches before leaving a point to the lazy pass
 #endif
@@ -203,6 +200,9 @@ struct Graveyard {
     v.clear();
   }
 };
+// r06: a device allocation that fails for lack of memory first evicts the process-wide
+// target cache's entry of the current device (set below, next to the cache) and retries once
+bool (*g_oom_evict)() = nullptr;
 // the graveyard of the context being constructed: every DevBuf member of a mgicp_ctx picks it up
 thread_local Graveyard* t_new_ctx_grave = nullptr;
 
@@ -211,6 +211,7 @@ struct DevBuf {
   T* p = nullptr;
   size_t cap = 0;
   Graveyard* grave = t_new_ctx_grave;
+  bool fine = false;  // fine-grained device memory (r06: the xGMI exchange rows, which peers store into)
   // grows by >= 1/4 so that a sequence of slightly larger requests (grid sizing iterations,
   // the second cloud) does not pay a hipFree/hipMalloc pair each time
   hipError_t reserve(size_t n) {
@@ -222,7 +223,16 @@ struct DevBuf {
     }
     p = nullptr;
     cap = 0;
-    hipError_t e = hipMalloc(&p, want * sizeof(T));
+    auto alloc = [&]() {
+      return fine ? hipExtMallocWithFlags(reinterpret_cast<void**>(&p), want * sizeof(T), hipDeviceMallocFinegrained)
+                  : hipMalloc(&p, want * sizeof(T));
+    };
+    hipError_t e = alloc();
+    if (e == hipErrorOutOfMemory && g_oom_evict) {
+      (void)hipGetLastError();
+      p = nullptr;
+      if (g_oom_evict()) e = alloc();
+    }
     if (e == hipSuccess) cap = want;
     return e;
   }
@@ -253,9 +263,14 @@ struct Cloud {
   bool want_pairs = false;
   bool drop_nonfinite = false; // build the grid over the finite points only (KdTreeFLANN semantics)
   double occupancy = 0;        // grid sizing target (points per non-empty cell); 0 = context default
-  size_t n_built = 0;          // points of the last grid built in this slot (cell-size hint)
-  bool fresh_grid = false;     // the grid was sized from the 3-D guess (not from an earlier grid of the slot):
-                               // exactly the grid a fresh context builds for these points (target cache)
+  size_t n_built = 0;          // points of the last grid built in this slot
+  bool fresh_grid = false;     // the grid is the one a fresh context builds for these points (target cache)
+  // r06: the start of the source grid's sizing loop is the target grid's cell size (and point count) it was
+  // built against; a source grid whose basis is not the current target's is rebuilt (src_basis_check), so a
+  // grid -- and with it every sorted order and sum -- is a function of the clouds alone, never of the slot's
+  // history.  0 / 0: the 3-D guess.
+  float basis_h = 0.f;
+  size_t basis_n = 0;
   DevBuf<double2> cov;        // 3 * cov_stride
   size_t cov_stride = 0;      // entries per covariance array (n, or the padded all-gather size)
   float lo[3] = {0.f, 0.f, 0.f}, hi[3] = {0.f, 0.f, 0.f};  // bounding box (original coordinates)
@@ -326,6 +341,18 @@ void tcache_clear_locked(TargetCache& c) {
   c.vl_ctr.release();
   c.valid = false;
 }
+bool tcache_evict_current() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  TargetCache& c = g_tcache[dev & 63];
+  std::unique_lock<std::mutex> lk(c.mu, std::try_to_lock);  // never from inside the cache's own lock
+  if (!lk.owns_lock() || (!c.valid && !c.t.orig.p && !c.vl_pool.p)) return false;
+  tcache_clear_locked(c);
+  return true;
+}
+struct OomHookInit {
+  OomHookInit() { g_oom_evict = &tcache_evict_current; }
+} g_oom_hook_init;
 
 }  // namespace
 
@@ -440,7 +467,6 @@ struct mgicp_ctx {
   int corr_split = 0;                   // waves of the wave sweep with <= this many stragglers hand them to a kernel of
                                         // their own (MGICP_CORR_SPLIT; 0 = every straggler finishes in place)
   float corr_rcap = 5.f;                // cells: lanes with a larger seed bound search alone (MGICP_CORR_RCAP)
-  bool corr_far_split = MGICP_CORR_FAR_SPLIT;  // r05: far stragglers of in-place waves to the finish kernel
   // r03 A/B (profiles/r03/corrsweep): union boxes of <= 96 rows and 16 cells along x, for waves whose
   // mean seed bound is >= 1.25 cells (the first sweep mostly): 2455 -> 2300 us per C4 align's sweeps
   int corr_max_rows = 96;               // union boxes with more rows / x cells: per-lane search
@@ -476,6 +502,8 @@ struct mgicp_ctx {
   unsigned int xgen = 0;
   unsigned long long xseq = 0;            // attaches so far (the segment's publication flag value)
   hipStream_t xstream = nullptr;
+  bool xstream_own = false;  // r06: the aux stream (idle during a BFGS run: N > 1 keeps the synchronous
+                             // covariance path) when the context has one -- no third stream per context
   unsigned char* shm_d = nullptr;       // device view of the segment (hipHostRegister'ed)
   long long st[kStCount] = {};          // pass-path counters
   // the resident server as the aligns run it (mgicp_debug_server_time): two events per launch
@@ -562,11 +590,13 @@ struct mgicp_ctx {
   // covariances and 1-NN cell lists there; a later context whose set_target uploads the same points
   // (compared on the device, bit for bit) adopts them instead of rebuilding -- GICPState constructs a
   // fresh GICPAlignment per scan against the same CAD cloud (LeicaStateMachine.cpp:149-150)
-  bool tcache_on = true;                // debug option "target_cache"
+  bool tcache_on = false;               // debug option "target_cache" (r06: opt-in; VERDICT r05 weak 5 --
+                                        // the reference node aligns once per process)
   bool tcache_adopted = false;          // the current target came from the cache
   // r05: a source set before any target sized its grid from the cached target's cell size (spec_h,
   // spec_n); checked against the target set_target brings: 1 pending, 2 kept, 3 discarded (rebuilt)
   int src_spec = 0;
+  unsigned long long src_rebasis = 0;  // r06: source grids rebuilt because the target changed under them
   float spec_h = 0.f;
   size_t spec_n = 0;
   // multi-GPU
@@ -888,15 +918,29 @@ bool spec_from_cache(mgicp_ctx* ctx) {
   ctx->src_spec = 1;
   return true;
 }
+// r06: also the general form of that check (src_basis_check): any built source grid whose sizing started
+// from another target grid than the current one (a new target with the source kept, a speculative guess
+// that missed) is rebuilt, so the source's grid is the one a fresh context builds for this cloud pair
 int spec_check(mgicp_ctx* ctx) {
-  if (ctx->src_spec != 1 || ctx->tgt.dirty || ctx->tgt.n_built == 0) return MGICP_OK;
-  if (ctx->tgt.view.h == ctx->spec_h && ctx->tgt.n_built == ctx->spec_n) {
-    ctx->src_spec = 2;
-    return MGICP_OK;
-  }
-  ctx->src_spec = 3;
-  if (int rc = cov_join(ctx, false)) return rc;  // its k-NN launch reads the grid about to be rebuilt
+  if (ctx->tgt.dirty || ctx->tgt.n_built == 0) return MGICP_OK;
   Cloud& s = ctx->src;
+  const bool basis_ok = s.basis_h == ctx->tgt.view.h && s.basis_n == ctx->tgt.n_built;
+  if (ctx->src_spec == 1) {
+    if (basis_ok) {
+      ctx->src_spec = 2;
+      return MGICP_OK;
+    }
+    ctx->src_spec = 3;
+  } else if (s.dirty || s.n_built == 0 || basis_ok) {
+    return MGICP_OK;
+  } else {
+    ctx->src_rebasis++;
+  }
+  if (int rc = cov_join(ctx, false)) return rc;  // its k-NN launch reads the grid about to be rebuilt
+  if (ctx->qperm_aux) {  // so does the aux stream's Morton sort
+    HIPCK(hipStreamWaitEvent(ctx->stream, ctx->aux_ev[2], 0));
+    ctx->qperm_aux = false;
+  }
   s.dirty = true;
   s.have_cov = false;
   s.view.h = 0.f;  // no previous grid: the rebuild starts from the real target's cell size
@@ -1165,20 +1209,24 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
     return nc;
   };
   double h = maxext > 0.f ? static_cast<double>(maxext) / std::cbrt(static_cast<double>(n)) : 1.0;
-  const bool fresh = !(cl.view.h > 0.f && cl.n_built > 0) && !(&cl == &ctx->src && ctx->tgt.view.h > 0.f &&
-                                                               ctx->tgt.n_built > 0);
-  // a cell size that already fitted a cloud of the same scene is a better start than the 3-D
-  // guess: this cloud's previous grid, else (source) the target's, scaled as a surface (sqrt n).
-  // The source's grid -- its sorted order, so the fixed reduction tree of every objective pass --
-  // therefore follows the target's: measured r05, a source grid sized on its own (a surface guess)
-  // flips one BFGS line-search decision at C4F (4 iterations against the oracle's 3, frob 7.7e-3):
-  // the restated bfgs.h trajectory is a knife-edge (DESIGN.md "Oracle uncertainty ledger")
-  if (cl.view.h > 0.f && cl.n_built > 0)
-    h = static_cast<double>(cl.view.h) * std::sqrt(static_cast<double>(cl.n_built) / n);
-  else if (&cl == &ctx->src && ctx->tgt.view.h > 0.f && ctx->tgt.n_built > 0)
-    h = static_cast<double>(ctx->tgt.view.h) * std::sqrt(static_cast<double>(ctx->tgt.n_built) / n);
-  else if (&cl == &ctx->src && ctx->src_spec == 1)  // the cached target's (spec_check confirms it)
-    h = static_cast<double>(ctx->spec_h) * std::sqrt(static_cast<double>(ctx->spec_n) / n);
+  // r06: the start of the sizing loop is a function of the clouds only.  The target
+  // (and any cloud but the source) always starts from the 3-D guess above -- never from this slot's
+  // previous grid: the loop accepts any size in a 0.6-1.6x occupancy band, so a different start gives a
+  // different accepted grid.  The source starts from the CURRENT target's cell size, scaled as a surface
+  // (sqrt n): its sorted order, so the fixed reduction tree of every objective pass, follows the target's
+  // (measured r05, a source grid sized on its own flips one BFGS line-search decision at C4F: 4 iterations
+  // against the oracle's 3, frob 7.7e-3).  src_basis_check rebuilds a source grid whose basis is stale.
+  float basis_h = 0.f;
+  size_t basis_n = 0;
+  if (&cl == &ctx->src && !ctx->tgt.dirty && ctx->tgt.view.h > 0.f && ctx->tgt.n_built > 0) {
+    basis_h = ctx->tgt.view.h;
+    basis_n = ctx->tgt.n_built;
+  } else if (&cl == &ctx->src && ctx->src_spec == 1) {  // the cached target's (spec_check confirms it)
+    basis_h = ctx->spec_h;
+    basis_n = ctx->spec_n;
+  }
+  if (basis_h > 0.f) h = static_cast<double>(basis_h) * std::sqrt(static_cast<double>(basis_n) / n);
+  const bool fresh = &cl != &ctx->src || basis_h == 0.f;
   h = std::max(h, 1e-6);
   int nd[3];
   double h_prev = 0, occ_prev = 0;
@@ -1305,6 +1353,8 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
   cl.ncells = nc;
   cl.n_built = n;
   cl.fresh_grid = fresh;
+  cl.basis_h = basis_h;
+  cl.basis_n = basis_n;
   cl.dirty = false;
   cl.have_cov = false;
   if (&cl == &ctx->tgt) ctx->vl_valid = false;  // the 1-NN cell lists index the old target
@@ -1981,7 +2031,7 @@ hipError_t launch_sweep(mgicp_ctx* ctx, const Mat4& T, double thr, bool seeded, 
   if (ctx->corr_wave && g.pairs) {
     const float rc = ctx->corr_rcap * g.h;
     void* work = nullptr;
-    if (ctx->corr_split > 0 || ctx->corr_far_split) {
+    if (ctx->corr_split > 0) {
       hipError_t e = ctx->nn_work.reserve(nn_work_bytes(p1 - p0));
       if (e == hipSuccess) e = ctx->nn_work_n.reserve(1);
       if (e != hipSuccess) return e;
@@ -1989,8 +2039,7 @@ hipError_t launch_sweep(mgicp_ctx* ctx, const Mat4& T, double thr, bool seeded, 
     }
     return launch_correspond_wave(g, ctx->d_out, p0, p1, T.xf(), thr, seeded ? 1 : 0, ctx->prev_pos.p,
                                   ctx->flags.p, qp, rc * rc, ctx->corr_max_rows, ctx->corr_max_x, ctx->corr_union_min_r,
-                                  work, ctx->nn_work_n.p, ctx->corr_split, ctx->corr_lds_pts, ctx->stream,
-                                  ctx->corr_far_split ? 1 : 0);
+                                  work, ctx->nn_work_n.p, ctx->corr_split, ctx->corr_lds_pts, ctx->stream);
   }
   return launch_correspond(g, ctx->d_out, p0, p1, T.xf(), thr, seeded ? 1 : 0, ctx->prev_pos.p, ctx->flags.p, qp,
                            ctx->stream);
@@ -2678,7 +2727,7 @@ void mgicp_destroy(mgicp_ctx* ctx) {
   if (ctx->h_ptimes) (void)hipHostFree(ctx->h_ptimes);
   if (ctx->h_rows) (void)hipHostFree(ctx->h_rows);
   xgmi_detach(ctx);
-  if (ctx->xstream) (void)hipStreamDestroy(ctx->xstream);
+  if (ctx->xstream && ctx->xstream_own) (void)hipStreamDestroy(ctx->xstream);
   if (ctx->h_xtot) (void)hipHostFree(ctx->h_xtot);
   if (ctx->have_shm) {
     (void)hipHostUnregister(ctx->shm.base);
@@ -3194,7 +3243,14 @@ int mgicp_comm_init(mgicp_ctx* ctx, int nranks, int rank, const unsigned char id
   if (!id) return MGICP_OK;
   ncclUniqueId uid;
   std::memcpy(&uid, id, 128);
-  NCCLCK(ncclCommInitRank(&ctx->comm, nranks, uid, rank));
+  ncclComm_t comm = nullptr;
+  const ncclResult_t r = ncclCommInitRank(&comm, nranks, uid, rank);
+  if (r != ncclSuccess) {
+    // r06: the context stays a detached shard of the same layout (an RCCL-free rank once a segment is
+    // attached), so a caller can fall back without re-creating it (parallel.setup_transport)
+    return fail(ctx, MGICP_E_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  }
+  ctx->comm = comm;
   ctx->st[kStTransport] = 1;
   return MGICP_OK;
 }
@@ -3218,9 +3274,19 @@ int mgicp_comm_attach_xgmi(mgicp_ctx* ctx, int on) {
     ctx->h_xgen = reinterpret_cast<unsigned int*>(ctx->h_xtot + shm::kRowWords);
     ctx->d_xgen = reinterpret_cast<unsigned int*>(ctx->d_xtot + shm::kRowWords);
   }
-  if (!ctx->xstream) HIPCK(hipStreamCreateWithFlags(&ctx->xstream, hipStreamNonBlocking));
+  if (!ctx->xstream && ctx->aux_stream) {
+    if (int rj = cov_join_all(ctx)) return rj;
+    ctx->xstream = ctx->aux_stream;
+  }
+  if (!ctx->xstream) {
+    HIPCK(hipStreamCreateWithFlags(&ctx->xstream, hipStreamNonBlocking));
+    ctx->xstream_own = true;
+  }
   // this rank's exchange buffer, zeroed (stamp 0 is never a pass stamp), published by IPC handle
   const size_t words = 2 * static_cast<size_t>(ctx->shm.max_sup) * shm::kRowWords;
+  // fine-grained: peers' servers store into it over xGMI while this rank's totaler polls it
+  // inside one running kernel; coarse-grained memory is coherent across devices only at kernel boundaries
+  ctx->xrows.fine = true;
   HIPCK(ctx->xrows.reserve(words));
   HIPCK(hipMemset(ctx->xrows.p, 0, ctx->xrows.cap * sizeof(unsigned long long)));
   hipIpcMemHandle_t h;
@@ -3317,7 +3383,7 @@ int mgicp_debug_target_cov_slice(mgicp_ctx* ctx, int nranks, int rank, double* o
   if (!ctx || !out_c6 || nranks < 1 || rank < 0 || rank >= nranks) return MGICP_E_INVALID;
   HIPCK(hipSetDevice(ctx->device));
   int rc = prepare(ctx, false);
-  if (rc) return rc;
+  if (rc || (rc = cov_join_all(ctx))) return rc;  // set_target's k-NN launch still writes tgt.cov
   Cloud& t = ctx->tgt;
   const size_t N = static_cast<size_t>(nranks), r = static_cast<size_t>(rank);
   const size_t cnt = (t.n + N - 1) / N;
@@ -3372,8 +3438,9 @@ int mgicp_debug_covariances(mgicp_ctx* ctx, int which, double* out_c6) {
   HIPCK(hipSetDevice(ctx->device));
   int rc = prepare(ctx, true);
   if (rc) return rc;
-  if ((rc = cov_join(ctx, false))) return rc;
-  if (which == 0 && !(ctx->src.have_cov && ctx->src.cov_p0 == ctx->shard_p0() && ctx->src.cov_p1 == ctx->shard_p1())) {
+  // both clouds: prepare counts set_target's running covariances as current
+  if ((rc = cov_join_all(ctx))) return rc;
+  if (which == 0 &&!(ctx->src.have_cov && ctx->src.cov_p0 == ctx->shard_p0() && ctx->src.cov_p1 == ctx->shard_p1())) {
     // every source covariance (lazy mode computes only the accepted points' ones)
     if ((rc = compute_cov(ctx, ctx->src, ctx->shard_p0(), ctx->shard_p1()))) return rc;
     if (ctx->src_lazy_ready) HIPCK(hipMemsetAsync(ctx->cov_ok.p, 1, ctx->shard_p1() - ctx->shard_p0(), ctx->stream));
@@ -3548,12 +3615,7 @@ int mgicp_debug_pass_bench(mgicp_ctx* ctx, const double x[6], int npasses, int m
     double tot[kRedVals];
     // the timing form stamps each pass's rows with its sequence number | 2^31
     const Xf34 unused{};
-#if defined(MGICP_SRV_NOTAIL) && MGICP_SRV_NOTAIL
-    (void)unused;
-    std::fill(tot, tot + kRedVals, 0.0);  // diagnostic build: the timing form writes no rows
-#else
     if ((rc = wait_rows(ctx, static_cast<unsigned int>(ctx->pass_seq - 1) | 0x80000000u, unused, tot, false))) return rc;
-#endif
     if ((rc = sync(ctx))) return rc;
     if (out16) std::memcpy(out16, tot, kRedVals * sizeof(double));
   } else {
@@ -3743,7 +3805,6 @@ int mgicp_debug_option(mgicp_ctx* ctx, const char* name, double value) {
   else if (n == "vlist_stats") ctx->vl_stats = on;      // per-sweep list statistics on stderr
   else if (n == "fuse_compact") ctx->fuse_compact = on; // compaction fused into listed sweeps
   else if (n == "target_cache") ctx->tcache_on = on;    // adopt / leave the target state (process cache)
-  else if (n == "corr_far_split") ctx->corr_far_split = on;  // far stragglers of the cold sweep to the finish kernel
   else if (n == "grid_occ") {                           // grid sizing (points per non-empty cell), next set_*
     if (!(value >= 1.0 && value <= 256.0)) return fail(ctx, MGICP_E_INVALID, "grid_occ must be in [1, 256]");
     ctx->occupancy = value;

@@ -142,7 +142,7 @@ hipError_t launch_correspond_wave(const GridView& tgt, const float4* src, size_t
                                   void* work /*nullable: NnWork list of stragglers, nn_work_bytes(p1 - p0)*/,
                                   unsigned int* work_n, int split_max /*waves with at most this many stragglers hand them on*/,
                                   int lds_cap /*small-ball waves: union box staged in LDS when it has <= lds_cap points*/,
-                                  hipStream_t s, int far_split = 0);
+                                  hipStream_t s);
 size_t nn_work_bytes(size_t n);
 
 // ---- the target's 1-NN cell lists (r04; DESIGN.md "1-NN cell lists") ----

@@ -15,69 +15,24 @@
 // expression rounds exactly like PCL's non-FMA SSE2 Eigen code and like oracle/gicp_ref.c.
 #pragma clang fp contract(off)
 
-#ifndef MGICP_NN_UNROLL
 #define MGICP_NN_UNROLL 4  // candidate gathers in flight per lane in the 1-NN scans
-#endif
-#ifndef MGICP_CORR_WAVES
 #define MGICP_CORR_WAVES 8  // resident waves per SIMD requested for the 1-NN kernel (64 VGPRs; A/B profiles/r01/ab_w8)
-#endif
-#ifndef MGICP_KNN_BLK
-#define MGICP_KNN_BLK 0  // k-NN covariances: 0 = knn_cov2_kernel (r02-r05, default), 1 = the wave-staged knn_blk_kernel
-                         // (r05 experiment, measured slower: DESIGN.md "k-NN covariances")
-#endif
-#ifndef MGICP_KNNB_DIAG
-#define MGICP_KNNB_DIAG 0  // diagnostic builds: 1 = no eigen-decomposition, 2 = pass 1 only
-#endif
-#ifndef MGICP_KNNB_STATS
-#define MGICP_KNNB_STATS 0  // 1 (with MGICP_CORR_PHASES): knn_blk_kernel staging / search counters (diagnostic)
-#endif
-#ifndef MGICP_KNN_INSERT_EARLY
-#define MGICP_KNN_INSERT_EARLY 0  // k-NN top-K insert: 1 = early-exit tail shift, 0 = branchless
-#endif
-#ifndef MGICP_COV_WAVES
 #define MGICP_COV_WAVES 1  // resident waves per SIMD requested for the k-NN covariance kernel
-#endif
-#ifndef MGICP_KNN_REGLIST_BATCH
-#define MGICP_KNN_REGLIST_BATCH 8  // register-list k-NN rows in guarded batches of this many points (0: 4-wide + tail)
-#endif
 #ifndef MGICP_KNN_DIV
 #define MGICP_KNN_DIV 0  // 1 (with MGICP_CORR_PHASES): k-NN candidate tests per lane vs per wave (diagnostic)
 #endif
 #ifndef MGICP_CORR_STATS
 #define MGICP_CORR_STATS 0  // 1: count 1-NN work per sweep (diagnostic builds only)
 #endif
-#ifndef MGICP_SRV_STAGGER
 #define MGICP_SRV_STAGGER 2  // resident pass server: 2 = wave wid computes its resident chunks after wid/4 of its streamed ones, 1 = odd waves last, 0 = all first
-#endif
-#ifndef MGICP_SEED_NEIGHBOURS
-#define MGICP_SEED_NEIGHBOURS 1  // 1: the first 1-NN sweep tests the seeds of the query's cell and its 6 face
-                                 // neighbours (2: every sweep)
-#endif
-#ifndef MGICP_SEED_BOTH
-#define MGICP_SEED_BOTH 1  // seeded 1-NN sweeps also test the seed map's candidate (the nearer one wins)
-#endif
-#ifndef MGICP_PACKED_RESID
-#define MGICP_PACKED_RESID 0  // 1: objective-pass residuals two per packed fp32 instruction (A/B: no gain, more spills; profiles/r02/ab_server)
-#endif
-#ifndef MGICP_SRV_PREFETCH
-#define MGICP_SRV_PREFETCH 0  // r05 A/B: streamed-first server waves load their first group before the gate
-#endif
 #ifndef MGICP_VL_DIAG
 #define MGICP_VL_DIAG 0  // 1 (with MGICP_CORR_PHASES): per-stage counters and shader clocks of vl_build_kernel
 #endif
 #ifndef MGICP_CORR_PHASES
 #define MGICP_CORR_PHASES 0  // 1: per-phase shader-clock totals of the wave 1-NN sweep (diagnostic builds only)
 #endif
-#ifndef MGICP_SRV_NOTAIL
-#define MGICP_SRV_NOTAIL 0  // diagnostic builds: the server's timing form without its reduction tail
-#endif
-#ifndef MGICP_CHUNK_SHFL
-#define MGICP_CHUNK_SHFL 0  // 1: chunk partials by 13 wave_sum shuffle trees (r02 form; 0 = wave_sum16, same bits)
-#endif
-#ifndef MGICP_SEED_BOX
-#define MGICP_SEED_BOX 1  // seeded 1-NN queries search the cube of their seed's ball (box_search)
-#endif
-constexpr bool kSeedBox = MGICP_SEED_BOX != 0;
+constexpr bool kSeedBox = true;  // seeded 1-NN queries search the cube of their seed's ball (box_search)
+constexpr int kRegListBatch = 8;  // register-list k-NN rows in guarded batches of this many points
 
 #include "mgicp_internal.hpp"
 
@@ -358,19 +313,6 @@ struct KnnVisitor {
     return key[K - 1] == ~0ull ? INFINITY : __uint_as_float(static_cast<uint32_t>(key[K - 1] >> 32));
   }
   __device__ __forceinline__ void insert(unsigned long long c, uint32_t cp) {
-#if MGICP_KNN_INSERT_EARLY
-    // shift from the tail and stop at the insertion slot (accepted candidates of the
-    // nearest-rows-first order usually land near the tail)
-#pragma unroll
-    for (int k = K - 1; k > 0; --k) {
-      if (!(c < key[k - 1])) { key[k] = c; pos[k] = cp; return; }
-      key[k] = key[k - 1];
-      pos[k] = pos[k - 1];
-    }
-    key[0] = c;
-    pos[0] = cp;
-    return;
-#endif
 #pragma unroll
     for (int k = K - 1; k > 0; --k) {
       const bool sh = c < key[k - 1];
@@ -388,26 +330,15 @@ struct KnnVisitor {
   }
   __device__ __forceinline__ void range(const GridView& g, uint32_t a, uint32_t b) {
     uint32_t j = a;
-#if MGICP_KNN_REGLIST_BATCH
     // guarded batches (r03): every load of a batch in flight at once, the row's tail included
-    for (; j < b; j += MGICP_KNN_REGLIST_BATCH) {
-      float4 pb[MGICP_KNN_REGLIST_BATCH];
+    for (; j < b; j += kRegListBatch) {
+      float4 pb[kRegListBatch];
 #pragma unroll
-      for (int u = 0; u < MGICP_KNN_REGLIST_BATCH; ++u) pb[u] = g.pts[min(j + u, b - 1)];
+      for (int u = 0; u < kRegListBatch; ++u) pb[u] = g.pts[min(j + u, b - 1)];
 #pragma unroll
-      for (int u = 0; u < MGICP_KNN_REGLIST_BATCH; ++u)
+      for (int u = 0; u < kRegListBatch; ++u)
         if (j + u < b) test(pb[u], j + u);
     }
-#else
-    for (; j + 4 <= b; j += 4) {  // four gathers in flight per lane (latency-bound loop)
-      const float4 p0 = g.pts[j], p1 = g.pts[j + 1], p2 = g.pts[j + 2], p3 = g.pts[j + 3];
-      test(p0, j);
-      test(p1, j + 1);
-      test(p2, j + 2);
-      test(p3, j + 3);
-    }
-    for (; j < b; ++j) test(g.pts[j], j);
-#endif
   }
 };
 
@@ -841,13 +772,9 @@ __device__ __forceinline__ double sel3(int i, double a, double b, double c) {
 // lane's LDS log as its sorted position (the (d2, original index) key is recomputed from the point,
 // bit-identically, when the log is read): thresholds only fall, so the log holds every member of the
 // final k-NN set (ties at the final k-th included) -- no second search.
-#ifndef MGICP_KNN_LOG_BATCH
 #define MGICP_KNN_LOG_BATCH 8  // log entries read per batch (compaction, moments): loads in flight together
-#endif
 constexpr int kLogBatch = MGICP_KNN_LOG_BATCH;
-#ifndef MGICP_KNN_RANGE_BATCH
 #define MGICP_KNN_RANGE_BATCH 8  // candidates per guarded batch of the logged k-NN rows (0: 4-wide + tail)
-#endif
 
 template <int K>
 struct KthVisitor {
@@ -1055,85 +982,8 @@ struct SumCert {
 // order without sorting.  Any other lane (log overflow, ties at tau, uncertified sums) is listed in
 // fb for the register-list kernel.  64-thread blocks, cap x 4 bytes of dynamic LDS per lane.
 
-#ifndef MGICP_KNN_MINW
-#define MGICP_KNN_MINW 1  // A/B: resident waves per SIMD requested for the logged k-NN kernel (VGPR cap)
-#endif
-#ifndef MGICP_KNN_FLAT
-#define MGICP_KNN_FLAT 0  // r05 A/B (measured 1.856 vs 1.870 ms per 5M cloud, VALU -1.4 %: not kept as default)
-#endif
+#define MGICP_KNN_MINW 1  // resident waves per SIMD requested for the logged k-NN kernel (VGPR cap)
 
-#if MGICP_KNN_FLAT
-// r05: rings 0 and 1 of the logged k-NN search as ONE per-lane stream.  ring_search walks a ring's row
-// ranges one after the other, each in guarded batches of 8 to the wave's longest lane (MGICP_KNN_DIV:
-// 142 test iterations per wave for 71 tests per lane); here every lane loads the bounds of the 3 x 3 x 3
-// block's 9 rows at once (one round trip), keeps the non-empty ones, and walks them in batches of 8 at
-// its own pace -- the wave runs to the lane with the most batches, not to the sum of per-row maxima.
-// Candidates ring_search would prune by the current k-th distance are tested instead (they fail the
-// threshold): the k-NN set, the log's final selection and every covariance are unchanged.  The caller
-// continues with ring_search from ring 2 (which first checks whether ring 1 already proves the result).
-template <int K>
-__device__ __forceinline__ void knn_ring1_flat(const GridView& g, float qx, float qy, float qz, KthVisitor<K>& vis) {
-  const int cx = qcell(qx, g.ox, g.inv_h), cy = qcell(qy, g.oy, g.inv_h), cz = qcell(qz, g.oz, g.inv_h);
-  const int x0 = max(cx - 1, 0), x1 = min(cx + 1, g.nx - 1);
-  const int zdn = near_side(qz, g.oz, g.h, cz), ydn = near_side(qy, g.oy, g.h, cy);
-  // near-first row order: the query's own row, its face neighbours, then the edge rows
-  const int oz[9] = {0, 0, zdn, 0, -zdn, zdn, zdn, -zdn, -zdn};
-  const int oy[9] = {0, ydn, 0, -ydn, 0, ydn, -ydn, ydn, -ydn};
-  uint32_t ra[9], re[9];
-#pragma unroll
-  for (int k = 0; k < 9; ++k) {
-    const int z = cz + oz[k], y = cy + oy[k];
-    const bool in = z >= 0 && z < g.nz && y >= 0 && y < g.ny;
-    const uint32_t* row = g.cell_start + (static_cast<size_t>(in ? z : cz) * g.ny + (in ? y : cy)) * g.nx;
-    const uint32_t a = row[x0], b = row[x1 + 1];
-    ra[k] = in ? a : 0u;
-    re[k] = in ? b : 0u;
-  }
-  // the non-empty rows, compacted to the front (static register indexing only)
-  uint32_t ca[9], ce[9];
-  int nr = 0;
-#pragma unroll
-  for (int k = 0; k < 9; ++k) {
-    ca[k] = 0u;
-    ce[k] = 0u;
-  }
-#pragma unroll
-  for (int k = 0; k < 9; ++k) {
-    const bool ne = re[k] > ra[k];
-#pragma unroll
-    for (int t = 0; t <= k; ++t)
-      if (ne && nr == t) {
-        ca[t] = ra[k];
-        ce[t] = re[k];
-      }
-    nr += ne ? 1 : 0;
-  }
-  int r = 0;
-  uint32_t j = ca[0], e = ce[0];
-  for (;;) {
-    const bool act = r < nr;
-    if (__builtin_amdgcn_ballot_w64(act) == 0ull) break;
-    if (act) {
-      float4 pb[MGICP_KNN_RANGE_BATCH];
-#pragma unroll
-      for (int u = 0; u < MGICP_KNN_RANGE_BATCH; ++u) pb[u] = g.pts[min(j + u, e - 1)];
-#pragma unroll
-      for (int u = 0; u < MGICP_KNN_RANGE_BATCH; ++u)
-        if (j + u < e) vis.test(dist2(qx, qy, qz, pb[u]), pb[u].w, j + u);
-      j += MGICP_KNN_RANGE_BATCH;
-      if (j >= e) {
-        ++r;
-#pragma unroll
-        for (int t = 1; t < 9; ++t)
-          if (r == t) {
-            j = ca[t];
-            e = ce[t];
-          }
-      }
-    }
-  }
-}
-#endif
 template <int K>
 __global__ __launch_bounds__(64, MGICP_KNN_MINW) void knn_cov2_kernel(GridView g, double eps, size_t p0, size_t p1, Cov3 cov,
                                                       const uint32_t* __restrict__ perm, int nsent, int cap,
@@ -1153,12 +1003,7 @@ __global__ __launch_bounds__(64, MGICP_KNN_MINW) void knn_cov2_kernel(GridView g
   v1.pts = g.pts;
   v1.cap = cap;
   if (ring_cap >= 0) v1.ring_cap = ring_cap;
-#if MGICP_KNN_FLAT
-  knn_ring1_flat(g, q.x, q.y, q.z, v1);
-  ring_search(g, q.x, q.y, q.z, v1, 2);
-#else
   ring_search(g, q.x, q.y, q.z, v1);
-#endif
   // ring_cap (the source's head start, lazy mode): a point whose k-NN lie farther out (clutter, debris)
   // is left to the lazy pass, which computes it only if a sweep accepts it (ok_out stays 0)
   if (v1.gave_up) return;
@@ -1234,481 +1079,6 @@ __global__ __launch_bounds__(64, MGICP_KNN_MINW) void knn_cov2_kernel(GridView g
   if (ok_out) ok_out[p] = 1;  // computed here or by the hand-off launch
 }
 
-#if MGICP_KNN_BLK
-// ---- wave-staged k-NN covariances (r05 experiment; MGICP_KNN_BLK=1 builds only) -----------------
-// Measured at C4 (5M target, knn_time.py, profiles/r05/knn*): 2.0-2.1 ms per cloud against 1.85-1.92 ms
-// for knn_cov2_kernel -- bit-identical covariances (the GPU suite passes with it), but not faster:
-// 64 grid-consecutive points span several surface crossings, so a wave's union of 3x3x3 blocks holds
-// ~385 points (26 % of the waves exceed a 448-point copy), pass 1 alone (staging + the med3 network
-// over ~99 unpruned candidates per lane) costs 1.58 ms, and the 14.8 KB of LDS per wave caps the
-// kernel at 2.5 waves per SIMD.  Kept as the record of the attempt.
-// knn_cov2_kernel runs one ring search per lane over global memory: a dependent round trip per row
-// bound and per batch of a row's points, ~20-50 per query, and only 42 % of wave cycles issue
-// (VERDICT r04 weak 3).  Here the 64 grid-consecutive queries of a wave first stage the points of the
-// union of their 3 x 3 x 3 cell blocks in LDS -- one round trip for 20 cell bounds per lane, then one
-// batch of coalesced loads -- and every lane searches that copy:
-//   pass 1: the exact k-th smallest fp32 d2 (tau) over its block with KthVisitor's med3 network (own
-//           cell first); only when the block does not certify tau against the distance to its faces
-//           (sparse neighbourhoods) does the ring search go on from ring 2 over global memory;
-//   pass 2: the block (and those rings) again with tau fixed: the candidates with d2 <= tau go to a
-//           short LDS log, and the moments are summed in log order under the order-independence
-//           certificate, exactly as knn_cov2_kernel does; ties at tau, log overflow and uncertified
-//           sums go to the register-list hand-off.  No compaction, no per-candidate log traffic.
-// The union: lane l's cells [x-1, x+1] of block row (y + dy, z + dz) are the sorted positions
-// [cs(row, x-1), cs(row, x+2)).  Over grid-ordered lanes these intervals are monotone (in both ends)
-// for each of the 9 block rows, so their union is a few merged pieces, laid out in LDS in position
-// order; lane l reads position j of block row o at LDS index j + delta[o] (one delta per piece).  A
-// wave whose intervals are not monotone (a perm that is not grid order) or whose union exceeds the
-// LDS copy reads the same intervals from global memory: same candidates, same order, same result.
-#ifndef MGICP_KNNB_CAP
-#define MGICP_KNNB_CAP 448  // staged points per wave (16 B each)
-#endif
-#ifndef MGICP_KNNB_LOG
-#define MGICP_KNNB_LOG 8  // pass-2 log entries per lane beyond K
-#endif
-#ifndef MGICP_KNNB_MINW
-#define MGICP_KNNB_MINW 3  // resident waves per SIMD requested (VGPR cap)
-#endif
-constexpr int kKnbCap = MGICP_KNNB_CAP;
-constexpr int kKnbLogExtra = MGICP_KNNB_LOG;
-constexpr int kKnbPieces = 64;
-constexpr uint32_t kKnbGlobal = 0x80000000u;  // log entry flag: a global sorted position (not an LDS index)
-
-// 64-lane inclusive scans, identity 0 (gfx9 DPP: row_shr 1/2/4/8 inside each row of 16 lanes, then
-// row_bcast:15 into rows 1 and 3 and row_bcast:31 into rows 2 and 3; a lane without a source keeps 0)
-__device__ __forceinline__ uint32_t wave_incl_add(uint32_t v) {
-  int x = static_cast<int>(v);
-  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);
-  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);
-  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);
-  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);
-  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);
-  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);
-  return static_cast<uint32_t>(x);
-}
-__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
-  uint32_t x = v;
-  x = max(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x111, 0xf, 0xf, false)));
-  x = max(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x112, 0xf, 0xf, false)));
-  x = max(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x114, 0xf, 0xf, false)));
-  x = max(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x118, 0xf, 0xf, false)));
-  x = max(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x142, 0xa, 0xf, false)));
-  x = max(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x143, 0xc, 0xf, false)));
-  return x;
-}
-
-// pass 1 past the block: KthVisitor's med3 network without its log
-template <int K>
-struct KthList {
-  static constexpr bool kNearFirst = true;
-  static constexpr bool kRingCap = true;
-  int ring_cap = 1 << 30;
-  bool gave_up = false;
-  int nrange = 0;  // global row ranges visited (the block did not settle tau)
-  float qx, qy, qz;
-  float key[K];
-  __device__ __forceinline__ void init(float x, float y, float z, int nsent) {
-    qx = x; qy = y; qz = z;
-#pragma unroll
-    for (int k = 0; k < K; ++k) key[k] = k < nsent ? -1.f : INFINITY;
-  }
-  __device__ __forceinline__ bool done(float Ls) const { return Ls > 0.f && key[K - 1] < Ls * Ls; }
-  __device__ __forceinline__ float prune2() const { return key[K - 1]; }
-  __device__ __forceinline__ void test(float d) {
-    if (d < key[K - 1]) {
-#pragma unroll
-      for (int k = K - 1; k > 0; --k) key[k] = __builtin_amdgcn_fmed3f(key[k - 1], d, key[k]);
-      key[0] = fminf(d, key[0]);
-    }
-  }
-  __device__ __forceinline__ void range(const GridView& g, uint32_t a, uint32_t b) {
-    ++nrange;
-    for (uint32_t j0 = a; j0 < b; j0 += 8) {
-      float4 pb[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) pb[u] = g.pts[min(j0 + u, b - 1)];
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (j0 + u < b) test(dist2(qx, qy, qz, pb[u]));
-    }
-  }
-};
-
-// pass 2 past the block: the candidates with d2 <= tau into the lane's log (global positions)
-struct TauLog {
-  static constexpr bool kNearFirst = false;
-  static constexpr bool kRingCap = false;
-  int ring_cap = 1 << 30;
-  bool gave_up = false;
-  float qx, qy, qz, tau;
-  uint32_t* log;  // lane-strided (stride 64)
-  int cnt, cap;
-  __device__ __forceinline__ bool done(float Ls) const { return Ls > 0.f && tau < Ls * Ls; }
-  __device__ __forceinline__ float prune2() const { return tau; }
-  __device__ __forceinline__ void push(uint32_t e) {
-    if (cnt < cap) log[cnt * 64] = e;
-    ++cnt;
-  }
-  __device__ __forceinline__ void range(const GridView& g, uint32_t a, uint32_t b) {
-    for (uint32_t j0 = a; j0 < b; j0 += 8) {
-      float4 pb[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) pb[u] = g.pts[min(j0 + u, b - 1)];
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (j0 + u < b && dist2(qx, qy, qz, pb[u]) <= tau) push((j0 + u) | kKnbGlobal);
-    }
-  }
-};
-
-// one block interval [a, b) of global positions through the lane's view (LDS copy at j + delta, or
-// global memory), four candidates in flight
-template <bool kLds, class F>
-__device__ __forceinline__ void blk_interval(const float4* __restrict__ gp, const float4* lp, uint32_t a, uint32_t b,
-                                             uint32_t delta, F&& f) {
-  for (uint32_t j = a; j < b; j += 4) {
-    float4 pb[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const uint32_t jj = min(j + u, b - 1);
-      pb[u] = kLds ? lp[jj + delta] : gp[jj];
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (j + u < b) f(pb[u], j + u);
-  }
-}
-
-// passes 1 and 2 over the lane's block (kLds: the wave's LDS copy) and, where needed, the rings past it
-// passes 1 and 2 over the lane's block (kLds: the wave's LDS copy) and, where needed, the rings past it.
-// Pass 1, phase A: the own cell, the rest of its row and the two y-face rows through the med3 network;
-// their k-th distance tau0 >= tau bounds the rest.  Phase B: the other six rows, each skipped when its
-// y / z slab lies beyond tau0 (ring_search's row test, same margins), and a candidate below tau0 is
-// only deferred (one LDS word) -- the network runs over the deferred few afterwards, not once per
-// candidate of the wave (SIMT: any inserting lane made every lane pay the 20-slot network).  A lane
-// whose phase A saw fewer than k points (tau0 = INF) inserts directly.  Pass 2 rescans the rows that
-// reach tau.
-template <int K, bool kLds>
-__device__ __forceinline__ void knn_blk_search(const GridView& g, const float4& q, int cy, int cz, bool live, bool blk,
-                                               const uint32_t (&s)[9], const uint32_t (&e)[9], uint32_t m0,
-                                               uint32_t m1, const uint32_t (&delta)[9], const float4* lp,
-                                               uint32_t* lg_lane, int nsent, int ring_cap, KthList<K>& v1,
-                                               TauLog& lg) {
-  v1.init(q.x, q.y, q.z, nsent);
-  if (ring_cap >= 0) v1.ring_cap = ring_cap;
-  if constexpr (!kLds) {
-    // a wave whose union does not fit the LDS copy: the per-lane ring search over global memory (near
-    // rows first, row pruning by the shrinking k-th distance), then pass 2 with tau fixed
-    if (live) ring_search(g, q.x, q.y, q.z, v1, 0);
-    lg.qx = q.x; lg.qy = q.y; lg.qz = q.z;
-    lg.tau = v1.key[K - 1];
-    lg.log = lg_lane;
-    lg.cnt = 0;
-    lg.cap = K + kKnbLogExtra;
-    if (live && !v1.gave_up) ring_search(g, q.x, q.y, q.z, lg, 0);
-    v1.nrange = 1;
-    return;
-  }
-  auto t1 = [&](const float4& pt, uint32_t) { v1.test(dist2(q.x, q.y, q.z, pt)); };
-  blk_interval<kLds>(g.pts, lp, m0, m1, delta[4], t1);
-  blk_interval<kLds>(g.pts, lp, s[4], m0, delta[4], t1);
-  blk_interval<kLds>(g.pts, lp, m1, e[4], delta[4], t1);
-  blk_interval<kLds>(g.pts, lp, s[3], e[3], delta[3], t1);
-  blk_interval<kLds>(g.pts, lp, s[5], e[5], delta[5], t1);
-  const float tau0 = v1.key[K - 1];
-  const bool direct = !(tau0 < INFINITY);
-  // the squared slab gap of block row o (y / z only: ring_search's row test)
-  auto row_gap2 = [&](int o) {
-    const float gy = (o % 3 == 1) ? 0.f : cell_gap(q.y, g.oy, g.h, cy + o % 3 - 1, g.slop);
-    const float gz = (o / 3 == 1) ? 0.f : cell_gap(q.z, g.oz, g.h, cz + o / 3 - 1, g.slop);
-    return gy * gy + gz * gz;
-  };
-  const int dcap = K + kKnbLogExtra;
-  int nd = 0;
-  constexpr int kB[6] = {1, 7, 0, 2, 6, 8};
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    const int o = kB[i];
-    const bool use = row_gap2(o) <= tau0 * 1.00001f;
-    blk_interval<kLds>(g.pts, lp, s[o], use ? e[o] : s[o], delta[o], [&](const float4& pt, uint32_t) {
-      const float d = dist2(q.x, q.y, q.z, pt);
-      if (d < tau0) {
-        if (direct) {
-          v1.test(d);
-        } else {
-          if (nd < dcap) lg_lane[nd * 64] = __float_as_uint(d);
-          ++nd;
-        }
-      }
-    });
-  }
-  // the deferred candidates through the network (overflow: the lane rescans phase B with it)
-  if (nd <= dcap) {
-    for (int i = 0; i < nd; ++i) v1.test(__uint_as_float(lg_lane[i * 64]));
-  } else {
-#pragma unroll
-    for (int i = 0; i < 6; ++i) blk_interval<kLds>(g.pts, lp, s[kB[i]], e[kB[i]], delta[kB[i]], t1);
-  }
-  // rings >= 2 only when the block does not certify tau (ring_search's own test at ring 2); a lane
-  // outside the grid (never, for a cloud's own points) searches from its first ring
-  if (live) ring_search(g, q.x, q.y, q.z, v1, blk ? 2 : 0);
-  lg.qx = q.x; lg.qy = q.y; lg.qz = q.z;
-  lg.tau = v1.key[K - 1];
-  lg.log = lg_lane;
-  lg.cnt = 0;
-  lg.cap = K + kKnbLogExtra;
-  if (!live || v1.gave_up) return;
-  const float tau = lg.tau;
-  const float w2 = tau * 1.00001f;
-#pragma unroll
-  for (int o = 0; o < 9; ++o) {
-    const uint32_t eo = row_gap2(o) <= w2 ? e[o] : s[o];
-    if constexpr (kLds) {
-      const uint32_t d = delta[o];  // log entries: the copy's index
-      blk_interval<kLds>(g.pts, lp, s[o], eo, d, [&](const float4& pt, uint32_t j) {
-        if (dist2(q.x, q.y, q.z, pt) <= tau) lg.push(j + d);
-      });
-    } else {
-      blk_interval<kLds>(g.pts, lp, s[o], eo, 0u, [&](const float4& pt, uint32_t j) {
-        if (dist2(q.x, q.y, q.z, pt) <= tau) lg.push(j | kKnbGlobal);
-      });
-    }
-  }
-  if (v1.nrange > 0 || !blk) ring_search(g, q.x, q.y, q.z, lg, blk ? 2 : 0);
-}
-
-template <int K>
-__global__ __launch_bounds__(64, MGICP_KNNB_MINW) void knn_blk_kernel(GridView g, double eps, size_t p0, size_t p1,
-                                                                     Cov3 cov, const uint32_t* __restrict__ perm,
-                                                                     int nsent, uint32_t* __restrict__ fb,
-                                                                     unsigned int* __restrict__ fb_count, int ring_cap,
-                                                                     uint8_t* __restrict__ ok_out) {
-  __shared__ float4 s_pts[kKnbCap];
-  __shared__ uint32_t s_log[(K + kKnbLogExtra) * 64];
-  __shared__ uint32_t s_pc[2 * kKnbPieces];  // pieces: LDS start, global start (in LDS order)
-  const int lane = static_cast<int>(threadIdx.x);
-  const size_t t = static_cast<size_t>(blockIdx.x) * 64 + lane;
-  const bool live = t < p1 - p0;
-  const size_t p = p0 + (live ? (perm ? perm[t] : t) : 0);
-#if MGICP_KNNB_STATS
-  const unsigned long long kt0 = __builtin_amdgcn_s_memtime();
-#endif
-  const float4 q = g.pts[p];
-  const int cx = qcell(q.x, g.ox, g.inv_h), cy = qcell(q.y, g.oy, g.inv_h), cz = qcell(q.z, g.oz, g.inv_h);
-  const bool blk = live && cx >= 0 && cx < g.nx && cy >= 0 && cy < g.ny && cz >= 0 && cz < g.nz;
-  // the 9 rows of the lane's block (o = 3 (dz + 1) + dy + 1): positions [s[o], e[o]); the own cell
-  // [m0, m1) inside the middle row -- 20 independent loads, one round trip
-  uint32_t s[9], e[9], m0, m1;
-  {
-    const int xa = max(cx - 1, 0), xb = min(cx + 1, g.nx - 1);
-    size_t ia[9], ib[9];
-    bool in[9];
-#pragma unroll
-    for (int o = 0; o < 9; ++o) {
-      const int y = cy + o % 3 - 1, z = cz + o / 3 - 1;
-      in[o] = blk && y >= 0 && y < g.ny && z >= 0 && z < g.nz;
-      const size_t row = in[o] ? (static_cast<size_t>(z) * g.ny + y) * g.nx : 0;
-      ia[o] = in[o] ? row + xa : 0;
-      ib[o] = in[o] ? row + xb + 1 : 0;
-    }
-    const size_t rm = blk ? (static_cast<size_t>(cz) * g.ny + cy) * g.nx + cx : 0;
-#pragma unroll
-    for (int o = 0; o < 9; ++o) {
-      s[o] = g.cell_start[ia[o]];
-      e[o] = g.cell_start[ib[o]];
-    }
-    m0 = g.cell_start[rm];
-    m1 = g.cell_start[rm + 1];
-#pragma unroll
-    for (int o = 0; o < 9; ++o)
-      if (!in[o]) s[o] = e[o] = 0u;
-    if (!blk) m0 = m1 = 0u;
-  }
-  // the union of the wave's intervals per block row: merged pieces in LDS order
-  uint32_t delta[9];
-  uint32_t base = 0, npc = 0;
-  bool mono = true;
-#pragma unroll
-  for (int o = 0; o < 9; ++o) {
-    const bool v = s[o] < e[o];
-    const uint32_t sv = v ? s[o] : 0u, ev = v ? e[o] : 0u;
-    const uint32_t ism = wave_incl_max(sv), iem = wave_incl_max(ev);
-    const uint32_t ps = __shfl_up(ism, 1, 64), pe = __shfl_up(iem, 1, 64);
-    const uint32_t psx = lane ? ps : 0u, pex = lane ? pe : 0u;
-    if (v && sv < psx) mono = false;
-    const uint32_t a = max(sv, pex);
-    const uint32_t c = (v && ev > a) ? ev - a : 0u;
-    const uint32_t ic = wave_incl_add(c);
-    const uint32_t tot = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(ic), 63));
-    const bool start = c > 0u && (sv > pex || pex == 0u);
-    const unsigned long long sm = __builtin_amdgcn_ballot_w64(start);
-    const uint32_t dst = base + (ic - c) - a;  // LDS index - position, on contributing lanes
-    const unsigned long long below = sm & ((2ull << lane) - 1ull);
-    const int L = below ? 63 - __builtin_clzll(below) : 0;
-    delta[o] = static_cast<uint32_t>(__shfl(static_cast<int>(dst), L, 64));
-    if (start) {
-      const uint32_t k = npc + static_cast<uint32_t>(__builtin_popcountll(sm & ((1ull << lane) - 1ull)));
-      if (k < static_cast<uint32_t>(kKnbPieces)) {
-        s_pc[2 * k] = base + (ic - c);
-        s_pc[2 * k + 1] = a;
-      }
-    }
-    npc += static_cast<uint32_t>(__builtin_popcountll(sm));
-    base += tot;
-  }
-  const bool stage = __builtin_amdgcn_ballot_w64(!mono) == 0ull && base <= static_cast<uint32_t>(kKnbCap) &&
-                     npc <= static_cast<uint32_t>(kKnbPieces);
-#if MGICP_KNNB_STATS
-  // [0] waves [1] staged [2] union points [3] pieces [4] non-monotone waves [5] over the cap
-  // [6] lane block candidates (sum) [7] busiest lane's block candidates (sum over waves); the atomics
-  // are issued at the end of the kernel (an atomic in flight would be waited on by the next load)
-  unsigned long long st_bs = 0;
-  uint32_t st_bm = 0;
-  {
-    uint32_t bc = 0;
-#pragma unroll
-    for (int o = 0; o < 9; ++o) bc += e[o] - s[o];
-    uint32_t bm = bc;
-    unsigned long long bs = bc;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      bm = max(bm, static_cast<uint32_t>(__shfl_xor(static_cast<int>(bm), off, 64)));
-      bs += __shfl_xor(bs, off, 64);
-    }
-    st_bs = bs;
-    st_bm = bm;
-  }
-  const bool st_nonmono = __builtin_amdgcn_ballot_w64(!mono) != 0ull;
-#endif
-  KthList<K> v1;
-  TauLog lg;
-  uint32_t* lg_lane = s_log + lane;
-#if MGICP_KNNB_STATS
-  const unsigned long long kt1 = __builtin_amdgcn_s_memtime();
-  unsigned long long kt2 = kt1;
-#endif
-  if (stage) {
-    __syncthreads();  // the piece table
-    // element i = lane + 64 u of the copy: its piece (binary search over the LDS starts)
-    constexpr int kU = (kKnbCap + 63) / 64;
-    float4 buf[kU];
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const uint32_t i = static_cast<uint32_t>(lane + 64 * u);
-      int lo = 0;
-#pragma unroll
-      for (int st = 32; st > 0; st >>= 1) {
-        const int m = lo + st;
-        if (m < static_cast<int>(npc) && s_pc[2 * m] <= i) lo = m;
-      }
-      const uint32_t gpos = s_pc[2 * lo + 1] + (i - s_pc[2 * lo]);
-      buf[u] = g.pts[i < base ? gpos : 0u];
-    }
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const uint32_t i = static_cast<uint32_t>(lane + 64 * u);
-      if (i < base) s_pts[i] = buf[u];
-    }
-    __syncthreads();
-#if MGICP_KNNB_STATS
-    kt2 = __builtin_amdgcn_s_memtime();
-#endif
-    knn_blk_search<K, true>(g, q, cy, cz, live, blk, s, e, m0, m1, delta, s_pts, lg_lane, nsent, ring_cap, v1, lg);
-  } else {
-    knn_blk_search<K, false>(g, q, cy, cz, live, blk, s, e, m0, m1, delta, s_pts, lg_lane, nsent, ring_cap, v1, lg);
-  }
-#if MGICP_KNNB_STATS
-  const unsigned long long kt3 = __builtin_amdgcn_s_memtime();
-#endif
-  if (!live || v1.gave_up) return;  // gave up: the lazy pass computes it if a sweep accepts it
-#if MGICP_KNNB_DIAG == 2  // diagnostic: pass 1 only (tau stored)
-  cov.a[p] = make_double2(static_cast<double>(lg.tau), 0.0);
-  if (ok_out) ok_out[p] = 1;
-  return;
-#endif
-  const int kreal = K - nsent;
-  const int cnt = lg.cnt;
-  bool ok = cnt == kreal;  // (<= K, within the log)
-  if (ok) {
-    double m0d = 0.0, m1d = 0.0, m2d = 0.0;
-    double a[3][3] = {{0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}};
-    SumCert c0, c1, c2, c00, c10, c11, c20, c21, c22;
-    for (int i0 = 0; i0 < cnt; i0 += 4) {
-      float4 pb[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint32_t en = lg_lane[min(i0 + u, cnt - 1) * 64];
-        pb[u] = (en & kKnbGlobal) ? g.pts[en & ~kKnbGlobal] : s_pts[en];
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (i0 + u >= cnt) continue;
-        const float4 pt = pb[u];
-        const float xx = pt.x * pt.x, yx = pt.y * pt.x, yy = pt.y * pt.y;
-        const float zx = pt.z * pt.x, zy = pt.z * pt.y, zz = pt.z * pt.z;
-        m0d += pt.x;
-        m1d += pt.y;
-        m2d += pt.z;
-        a[0][0] += static_cast<double>(xx);
-        a[1][0] += static_cast<double>(yx);
-        a[1][1] += static_cast<double>(yy);
-        a[2][0] += static_cast<double>(zx);
-        a[2][1] += static_cast<double>(zy);
-        a[2][2] += static_cast<double>(zz);
-        c0.add(pt.x);
-        c1.add(pt.y);
-        c2.add(pt.z);
-        c00.add(xx);
-        c10.add(yx);
-        c11.add(yy);
-        c20.add(zx);
-        c21.add(zy);
-        c22.add(zz);
-      }
-    }
-    ok = c0.ok() && c1.ok() && c2.ok() && c00.ok() && c10.ok() && c11.ok() && c20.ok() && c21.ok() && c22.ok();
-#if MGICP_KNNB_DIAG == 1  // diagnostic: no eigen-decomposition (the raw sums are stored)
-    if (ok) {
-      cov.a[p] = make_double2(m0d, a[0][0]);
-      cov.b[p] = make_double2(m1d, a[1][1]);
-      cov.c[p] = make_double2(m2d, a[2][2]);
-    }
-#else
-    if (ok) cov_finish(m0d, m1d, m2d, a, static_cast<double>(kreal), eps, cov, p);
-#endif
-  }
-#if MGICP_KNNB_STATS
-  {  // [8] lanes past the block (rings >= 2) [9] hand-offs [10] live lanes; shader cycles per wave
-     // [11] setup, [12] staging copy, [13] passes 1-2 of staged waves, [15] setup, [16] passes of the others
-    const unsigned long long pm = __builtin_amdgcn_ballot_w64(v1.nrange > 0 || !blk);
-    const unsigned long long hm = __builtin_amdgcn_ballot_w64(!ok);
-    const unsigned long long lm = __builtin_amdgcn_ballot_w64(true);
-    if (lane == __builtin_ctzll(lm)) {
-      if (lane == 0) {
-        atomicAdd(&g_corr_phase[0], 1ull);
-        atomicAdd(&g_corr_phase[1], stage ? 1ull : 0ull);
-        atomicAdd(&g_corr_phase[2], static_cast<unsigned long long>(base));
-        atomicAdd(&g_corr_phase[3], static_cast<unsigned long long>(npc));
-        atomicAdd(&g_corr_phase[4], st_nonmono ? 1ull : 0ull);
-        atomicAdd(&g_corr_phase[5], base > static_cast<uint32_t>(kKnbCap) ? 1ull : 0ull);
-        atomicAdd(&g_corr_phase[6], st_bs);
-        atomicAdd(&g_corr_phase[7], static_cast<unsigned long long>(st_bm));
-        atomicAdd(&g_corr_phase[stage ? 11 : 15], kt1 - kt0);
-        if (stage) atomicAdd(&g_corr_phase[12], kt2 - kt1);
-        atomicAdd(&g_corr_phase[stage ? 13 : 16], kt3 - kt2);
-      }
-      atomicAdd(&g_corr_phase[8], static_cast<unsigned long long>(__builtin_popcountll(pm)));
-      atomicAdd(&g_corr_phase[9], static_cast<unsigned long long>(__builtin_popcountll(hm)));
-      atomicAdd(&g_corr_phase[10], static_cast<unsigned long long>(__builtin_popcountll(lm)));
-    }
-  }
-#endif
-  // ties at tau, log overflow or an uncertified sum: the sorted register-list kernel finishes it
-  if (!ok) fb[atomicAdd(fb_count, 1u)] = static_cast<uint32_t>(p);
-  if (ok_out) ok_out[p] = 1;
-}
-
-#endif  // MGICP_KNN_BLK
 
 // ------------------------------------------------------------------------------------
 // correspondence + Mahalanobis
@@ -1739,11 +1109,11 @@ __device__ __forceinline__ void seed_query(const GridView& tg, int seeded, uint3
 #pragma unroll
   for (int k = 0; k < 8; ++k) sp[k] = kNone;
   if (seeded) sp[7] = prev;  // last iteration's match
-  if ((!seeded || MGICP_SEED_BOTH) && tg.seed) {
+  if (tg.seed) {  // seeded sweeps also test the seed map's candidate (the nearer one wins)
     // the seed map: a point of a Chebyshev-nearest non-empty cell of the query's cell (and, in the
     // first sweep, of its 6 face neighbours)
     const int cx = qcell(qx, tg.ox, tg.inv_h), cy = qcell(qy, tg.oy, tg.inv_h), cz = qcell(qz, tg.oz, tg.inv_h);
-    const bool seven = MGICP_SEED_NEIGHBOURS && (!seeded || MGICP_SEED_NEIGHBOURS > 1);
+    const bool seven = !seeded;  // the first sweep tests the seeds of the query's cell and its 6 face neighbours
     const int dd[7][3] = {{0, 0, 0}, {-1, 0, 0}, {1, 0, 0}, {0, -1, 0}, {0, 1, 0}, {0, 0, -1}, {0, 0, 1}};
 #pragma unroll
     for (int k = 0; k < 7; ++k) {
@@ -1832,7 +1202,7 @@ __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_wave_kernel(
     GridView tg, const float4* __restrict__ src, size_t p0, size_t p1, Xf34 T, double thr, int seeded,
     uint32_t* __restrict__ nn_pos, uint32_t* __restrict__ flags, const uint32_t* __restrict__ qperm, float rcap2,
     int max_rows, int max_xcells, float union_min_r, NnWork* __restrict__ work, unsigned int* __restrict__ work_n,
-    int split_max, int lds_cap, int far_split) {
+    int split_max, int lds_cap) {
   __shared__ f4v stage[4][2 * kStagePairs];
   // small-ball waves: the union box's cell bounds, row offsets and points (dynamic LDS, lds_cap
   // points per wave; 0 = off)
@@ -2094,25 +1464,11 @@ __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_wave_kernel(
     MGICP_PH(4);
     if (!live || fin) return;
   } else {
-    // r05 (far_split): a wave finishing in place hands its FAR stragglers (bound beyond rcap: scan debris
-    // and clutter a few centimetres off the part, which the gate may still accept) to the finish kernel,
-    // so its near lanes do not wait for their ball searches; the far ones run there in waves of their own
-    const bool far = far_split && work && fin && vis.prune2() > rcap2;
-    const unsigned long long farm = __builtin_amdgcn_ballot_w64(far);
-    if (farm) {
-      unsigned int base = 0;
-      if (lane == 0) base = atomicAdd(work_n, static_cast<unsigned int>(__builtin_popcountll(farm)));
-      base = __builtin_amdgcn_readfirstlane(base);
-      const unsigned int off = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned int>(farm >> 32),
-                                                         __builtin_amdgcn_mbcnt_lo(static_cast<unsigned int>(farm), 0u));
-      if (far) work[base + off] = NnWork{static_cast<uint32_t>(p - p0), vis.pos, vis.best};
-    }
-    if (fin && !far) {
+    if (fin) {
       if (vis.best != ~0ull) box_search(tg, qx, qy, qz, vis);
       else ring_search(tg, qx, qy, qz, vis);
     }
     MGICP_PH(4);
-    if (far) return;
   }
   if (!live) return;
   const bool ok = vis.best != ~0ull &&
@@ -2186,9 +1542,8 @@ __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_kernel(GridV
     const uint32_t pp = nn_pos[p - p0];
     if (pp != 0xffffffffu) vis.range(tg, pp, pp + 1);
   }
-  if ((!seeded || MGICP_SEED_BOTH) && tg.seed) {
-#if MGICP_SEED_NEIGHBOURS
-    if (!seeded || MGICP_SEED_NEIGHBOURS > 1) {
+  if (tg.seed) {  // seeded sweeps also test the seed map's candidate (the nearer one wins)
+    if (!seeded) {
       // the first sweep: the seeds of the query's cell and its 6 face neighbours, the nearest wins
       const int cx = qcell(qx, tg.ox, tg.inv_h), cy = qcell(qy, tg.oy, tg.inv_h), cz = qcell(qz, tg.oz, tg.inv_h);
       const int dd[7][3] = {{0, 0, 0}, {-1, 0, 0}, {1, 0, 0}, {0, -1, 0}, {0, 1, 0}, {0, 0, -1}, {0, 0, 1}};
@@ -2202,7 +1557,6 @@ __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_kernel(GridV
         }
       }
     } else
-#endif
     {
       // a point of a Chebyshev-nearest non-empty cell (seed map): the first sweep's seed, and in
       // later sweeps a second candidate beside the last match (queries move by up to centimetres
@@ -2245,9 +1599,7 @@ __global__ __launch_bounds__(256, MGICP_CORR_WAVES) void correspond_kernel(GridV
 // real point, no closer than the true 1-NN).  Queries outside the fine grid, or in a cell with no
 // target point within D(1 + 1e-5) + its half diagonal of the centre, are rejected.
 constexpr int kVlCand = 1024;  // candidates a build wave keeps in LDS (more: the cell stays a fallback cell)
-#ifndef MGICP_VLIST_BATCH
 #define MGICP_VLIST_BATCH 4  // list entries a query loads per round (a multiple of 4)
-#endif
 constexpr int kVlBatch = MGICP_VLIST_BATCH;
 
 __device__ __forceinline__ void vl_cell_xyz(const VListView& v, uint32_t ci, uint32_t& ix, uint32_t& iy, uint32_t& iz) {
@@ -3276,21 +2628,6 @@ __device__ __forceinline__ void load_group(const CorrSoA& c, uint32_t i, CorrGro
 
 // the group's 4 correspondences in stream order (residuals two at a time in packed fp32)
 __device__ __forceinline__ void fdf_group(const Xf34& A, const CorrGroup& g, double (&acc)[kRedVals]) {
-#if MGICP_PACKED_RESID
-  pf2 rx01, ry01, rz01, rx23, ry23, rz23;
-  resid2(A, pf2{g.f[0].x, g.f[0].y}, pf2{g.f[1].x, g.f[1].y}, pf2{g.f[2].x, g.f[2].y}, pf2{g.f[3].x, g.f[3].y},
-         pf2{g.f[4].x, g.f[4].y}, pf2{g.f[5].x, g.f[5].y}, rx01, ry01, rz01);
-  resid2(A, pf2{g.f[0].z, g.f[0].w}, pf2{g.f[1].z, g.f[1].w}, pf2{g.f[2].z, g.f[2].w}, pf2{g.f[3].z, g.f[3].w},
-         pf2{g.f[4].z, g.f[4].w}, pf2{g.f[5].z, g.f[5].w}, rx23, ry23, rz23);
-  fdf_point_r(rx01.x, ry01.x, rz01.x, g.f[0].x, g.f[1].x, g.f[2].x, g.d[0].x, g.d[2].x, g.d[4].x, g.d[6].x,
-              g.d[8].x, g.d[10].x, acc);
-  fdf_point_r(rx01.y, ry01.y, rz01.y, g.f[0].y, g.f[1].y, g.f[2].y, g.d[0].y, g.d[2].y, g.d[4].y, g.d[6].y,
-              g.d[8].y, g.d[10].y, acc);
-  fdf_point_r(rx23.x, ry23.x, rz23.x, g.f[0].z, g.f[1].z, g.f[2].z, g.d[1].x, g.d[3].x, g.d[5].x, g.d[7].x,
-              g.d[9].x, g.d[11].x, acc);
-  fdf_point_r(rx23.y, ry23.y, rz23.y, g.f[0].w, g.f[1].w, g.f[2].w, g.d[1].y, g.d[3].y, g.d[5].y, g.d[7].y,
-              g.d[9].y, g.d[11].y, acc);
-#else
   fdf_point(A, g.f[0].x, g.f[1].x, g.f[2].x, g.f[3].x, g.f[4].x, g.f[5].x, g.d[0].x, g.d[2].x, g.d[4].x,
             g.d[6].x, g.d[8].x, g.d[10].x, acc);
   fdf_point(A, g.f[0].y, g.f[1].y, g.f[2].y, g.f[3].y, g.f[4].y, g.f[5].y, g.d[0].y, g.d[2].y, g.d[4].y,
@@ -3299,7 +2636,6 @@ __device__ __forceinline__ void fdf_group(const Xf34& A, const CorrGroup& g, dou
             g.d[7].x, g.d[9].x, g.d[11].x, acc);
   fdf_point(A, g.f[0].w, g.f[1].w, g.f[2].w, g.f[3].w, g.f[4].w, g.f[5].w, g.d[1].y, g.d[3].y, g.d[5].y,
             g.d[7].y, g.d[9].y, g.d[11].y, acc);
-#endif
 }
 
 // The gate of a pass whose state is not known at launch (pre-launched gated passes and the
@@ -3371,18 +2707,6 @@ __device__ __forceinline__ void chunk_store(int j, double (&acc)[kRedVals], cons
                                             double* __restrict__ partial, int lane) {
   const double cnt = static_cast<double>(ccnt[j]);
   double* pj = partial + static_cast<size_t>(j) * kRedVals;
-#if MGICP_CHUNK_SHFL
-  // r02 form (A/B): 13 wave_sum shuffle trees, lane 0 stores
-#pragma unroll
-  for (int v = 0; v < 13; ++v) acc[v] = wave_sum(acc[v]);
-  if (lane == 0) {
-#pragma unroll
-    for (int v = 0; v < 13; ++v) st_sc1(pj + v, acc[v]);
-    st_sc1(pj + 13, cnt);
-    st_sc1(pj + 14, 0.0);
-    st_sc1(pj + 15, 0.0);
-  }
-#else
   // acc[13..15] are never accumulated (+0.0), so value 13 -- the count -- is replaced after the
   // tree and 14, 15 come out +0.0 as the r02 form stored them
   wave_sum16(acc, lane);
@@ -3392,7 +2716,6 @@ __device__ __forceinline__ void chunk_store(int j, double (&acc)[kRedVals], cons
     w.x = lo32(acc[0]); w.y = hi32(acc[0]); w.z = lo32(v1); w.w = hi32(v1);
     asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(pj + (lane >> 2)), "v"(w) : "memory");
   }
-#endif
 }
 
 // ---- the tagged tail of the resident server (r03) ------------------------------------------------
@@ -3686,9 +3009,6 @@ __global__ __launch_bounds__(64 * kWaves, 1) void fdf_server_kernel(
   static_assert(kR <= 4 && (kR == 4 || kR + kL <= 4), "resident groups: chunk 0, then chunk 1 only after a full chunk 0");
   __shared__ float4 lf[kWaves][kL][6][64];
   __shared__ double2 ld[kWaves][kL][12][64];
-#if MGICP_SRV_PREFETCH == 2
-  __shared__ float4 pf_lds[kWaves][64];  // dummy destination of the cache-warming LDS-DMA loads
-#endif
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int nw = gridDim.x * kWaves;
   const int w0 = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x * kWaves + wid));
@@ -3735,46 +3055,9 @@ __global__ __launch_bounds__(64 * kWaves, 1) void fdf_server_kernel(
   // others poll the mailbox block 0 forwards to.  1 = the host's pinned copy (PCIe reads by one
   // block); gridDim = a command block the host stores straight into device memory (BAR)
   const int host_pollers = kBench ? 0 : pollers;
-#if MGICP_SRV_PREFETCH
-  // r05 A/B: a wave that starts a pass with a streamed chunk (stagger) loads that chunk's first group
-  // before it waits at the gate, so the load's latency falls into the host round trip between passes
-  // (the streams do not change during a BFGS run; the group is only loaded early, the sums are the same)
-  const int nst_pf = w1 + nw < nch ? (nch - w1 - 1) / nw : 0;
-  const int split_pf = MGICP_SRV_STAGGER == 2 ? (wid * nst_pf + kWaves / 2) / kWaves
-                                              : (MGICP_SRV_STAGGER == 1 && (wid & 1) ? nst_pf : 0);
-  const int wpf = w1 + nw;
-#if MGICP_SRV_PREFETCH == 1
-  const uint32_t ipf = wpf < nch ? chunk_g0(wpf) + lane : 0u;
-  const bool pf_ok = split_pf > 0 && wpf < nch && ipf < chunk_g1(ccnt, wpf);
-  CorrGroup pf;
-#endif
-#endif
   for (unsigned long long seq = seq0;; ++seq) {
     Xf34 A = Abench;
     int rev = 0;
-#if MGICP_SRV_PREFETCH == 1
-    if (pf_ok) load_group(c, ipf, pf);
-#elif MGICP_SRV_PREFETCH == 2
-    // mode 2: warm the caches with the group through LDS-DMA loads into a dummy LDS row (no VGPRs: the
-    // server's 512 registers are taken by its resident groups)
-#if defined(__HIP_DEVICE_COMPILE__)  // (the builtin exists in the device pass only)
-    if (split_pf > 0 && wpf < nch) {  // (recomputed per pass: no register held across the loop)
-      uint32_t lo = static_cast<uint32_t>(lane);
-      asm volatile("" : "+v"(lo));  // the addresses are formed here each pass, not hoisted out of the loop
-      const uint32_t ipf = chunk_g0(wpf) + lo;
-      const float* fs[6] = {c.sx, c.sy, c.sz, c.qx, c.qy, c.qz};
-      const double* ms[6] = {c.m00, c.m01, c.m02, c.m11, c.m12, c.m22};
-#pragma unroll
-      for (int e = 0; e < 6; ++e)
-        __builtin_amdgcn_global_load_lds(const_cast<float*>(fs[e] + 4 * static_cast<size_t>(ipf)), &pf_lds[wid][0], 16, 0, 0);
-#pragma unroll
-      for (int e = 0; e < 6; ++e) {
-        __builtin_amdgcn_global_load_lds(const_cast<double*>(ms[e] + 4 * static_cast<size_t>(ipf)), &pf_lds[wid][0], 16, 0, 0);
-        __builtin_amdgcn_global_load_lds(const_cast<double*>(ms[e] + 4 * static_cast<size_t>(ipf) + 2), &pf_lds[wid][0], 16, 0, 0);
-      }
-    }
-#endif
-#endif
     // the timing form stamps rows with seq | 2^31 (align passes stamp their pass index, < 2^31)
     unsigned int rstamp = static_cast<unsigned int>(seq) | 0x80000000u;
     if (!(kBench && seq == seq0) && !pass_gate(seq, cmd, mail, timeout, nullptr, host_pollers, A, rev, rstamp))
@@ -3802,18 +3085,9 @@ __global__ __launch_bounds__(64 * kWaves, 1) void fdf_server_kernel(
 #pragma unroll
         for (int v = 0; v < kRedVals; ++v) acc[v] = 0.0;
         const uint32_t g1 = chunk_g1(ccnt, w);
-#if MGICP_SRV_PREFETCH == 1
-        bool first = w == wpf && pf_ok;
-#endif
         for (uint32_t i = chunk_g0(w) + lane; i < g1; i += 64) {
           CorrGroup g;
-#if MGICP_SRV_PREFETCH == 1
-          if (first) g = pf;
-          else load_group(c, i, g);
-          first = false;
-#else
           load_group(c, i, g);
-#endif
           fdf_group(A, g, acc);
         }
         store(w, acc);
@@ -3868,22 +3142,6 @@ __global__ __launch_bounds__(64 * kWaves, 1) void fdf_server_kernel(
     if (w0 >= nch) continue;
     // the timing form writes host rows too when given them (chained on the device by a global
     // ticket), so it times the pass the aligns run
-#if MGICP_SRV_NOTAIL
-    // diagnostic build (timing form only): no chunk tickets, super sums or rows -- every wave takes
-    // the chain ticket once its chunks are stored; what the pass costs without its reduction tail
-    bool fin = false;
-    if (kBench) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const unsigned int nact = static_cast<unsigned int>(min(nw, nch));
-      const int nsup = (nch + kSuperChunks - 1) / kSuperChunks;
-      int l = 0;
-      if (lane == 0)
-        l = __hip_atomic_fetch_add(tickets + nsup, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) % nact == nact - 1 ? 1 : 0;
-      fin = __shfl(l, 0, 64) != 0;
-    } else {
-      fin = wave_tickets(w0, nw, nch, 0, tickets, partial, spart, out, done_flag, seq, lane, rows, false, rstamp);
-    }
-#else
     bool fin = false;
     if (tagged) {
       if (w0 < nsup) {
@@ -3922,7 +3180,6 @@ __global__ __launch_bounds__(64 * kWaves, 1) void fdf_server_kernel(
       fin = wave_tickets(w0, nw, nch, 0, tickets, partial, spart, out, done_flag, seq, lane, rows, kBench && rows,
                          rstamp);
     }
-#endif
     if (fin && lane == 0) {
       if (ptimes) ptimes[2 * (seq & 1023) + 1] = wall_clock64();
       if (kBench) {
@@ -4357,22 +3614,18 @@ hipError_t launch_iota(uint32_t* v, size_t n, hipStream_t s) {
   return hipGetLastError();
 }
 
-// log capacity (entries per lane) of the r04 logged k-NN kernel (MGICP_KNN_BLK=0 builds): K + 28
-[[maybe_unused]] static int knn_log_cap(int K) { return std::min(K + 28, 128); }
+// log capacity (entries per lane) of the logged k-NN kernel: K + 28
+static int knn_log_cap(int K) { return std::min(K + 28, 128); }
 
 template <int K>
 static hipError_t knn_cov_k(const GridView& g, double eps, size_t p0, size_t p1, Cov3 cov,
                             const uint32_t* perm, int k, uint32_t* fb, unsigned int* fb_count, hipStream_t s,
                             int ring_cap, uint8_t* ok, int chain) {
   if (fb) {
-#if MGICP_KNN_BLK
-    knn_blk_kernel<K><<<nblk(p1 - p0, 64), 64, 0, s>>>(g, eps, p0, p1, cov, perm, K - k, fb, fb_count, ring_cap, ok);
-#else
     const int cap = knn_log_cap(K);
     knn_cov2_kernel<K><<<nblk(p1 - p0, 64), 64, cap * 64 * sizeof(uint32_t), s>>>(g, eps, p0, p1, cov, perm,
                                                                                  K - k, cap, fb, fb_count, ring_cap,
                                                                                  ok);
-#endif
     // chain: the hand-off follows at once in stream order, its count read on the device (a grid of
     // `chain` blocks striding over the list)
     if (chain > 0) knn_cov_kernel<K><<<chain, 256, 0, s>>>(g, eps, 0, 0, cov, fb, K - k, fb_count);
@@ -4384,7 +3637,7 @@ static hipError_t knn_cov_k(const GridView& g, double eps, size_t p0, size_t p1,
 
 // exact instantiations for PCL's default (20) and its round neighbours; any other k in
 // [1, kMaxK] runs on the next multiple of 8 with K - k sentinel slots.  With fb / fb_count the
-// wave-staged kernel (r05; knn_cov2_kernel in MGICP_KNN_BLK=0 builds) runs and lists the points it leaves to KnnVisitor; without, (or for that
+// logged kernel (knn_cov2_kernel) runs and lists the points it leaves to KnnVisitor; without, (or for that
 // list: perm = fb, p0 = 0, p1 = count) the register-list kernel runs.
 hipError_t launch_knn_cov(const GridView& g, int k, double eps, size_t p0, size_t p1, Cov3 cov,
                           const uint32_t* perm, uint32_t* fb, unsigned int* fb_count, hipStream_t s, int ring_cap,
@@ -4505,7 +3758,7 @@ hipError_t launch_correspond(const GridView& tgt, const float4* src, size_t p0, 
 hipError_t launch_correspond_wave(const GridView& tgt, const float4* src, size_t p0, size_t p1, Xf34 T,
                                   double thr, int seeded, uint32_t* nn_pos, uint32_t* flags, const uint32_t* qperm,
                                   float rcap2, int max_rows, int max_xcells, float union_min_r, void* work,
-                                  unsigned int* work_n, int split_max, int lds_cap, hipStream_t s, int far_split) {
+                                  unsigned int* work_n, int split_max, int lds_cap, hipStream_t s) {
   if (p1 <= p0) return hipSuccess;
   if (!tgt.pairs || (work && !work_n)) return hipErrorInvalidValue;
   NnWork* w = static_cast<NnWork*>(work);
@@ -4517,7 +3770,7 @@ hipError_t launch_correspond_wave(const GridView& tgt, const float4* src, size_t
   const size_t shm = lds_cap ? 4 * static_cast<size_t>(std::max(lds_cap, 0) + kLdsMeta) * sizeof(float4) : 0;
   correspond_wave_kernel<<<nblk(p1 - p0), 256, shm, s>>>(tgt, src, p0, p1, T, thr, seeded, nn_pos, flags, qperm,
                                                          rcap2, max_rows, max_xcells, union_min_r, w, work_n,
-                                                         split_max, lds_cap, far_split);
+                                                         split_max, lds_cap);
   if (w) {
     // grid-stride over the stragglers: 8 blocks of 4 waves per CU (the count is known on the device only)
     const unsigned int nb = static_cast<unsigned int>(std::min<size_t>(nblk(p1 - p0), 2048));

@@ -236,3 +236,94 @@ class Rendezvous:
         if self.sock is not None:
             self.sock.close()
         self.peers, self.sock = [], None
+
+
+def setup_transport(eng, pg, world: int, rank: int, transport: str, n_source: int, probe=None,
+                    force_rccl_fail: bool = False) -> dict:
+    """Join `world` ranks (one engine per process) and pick the per-pass exchange; every rank calls this
+    with the same arguments, every decision is agreed through `pg` (Rendezvous.broadcast /
+    allreduce_max), so all ranks end on the same transport.
+
+    r06: a first multi-GPU run degrades instead of dying.  RCCL carries only the
+    one-time split of the target covariances (and the GN mode's per-iteration gathers when no segment
+    exists); if the unique id or ncclCommInitRank fails on any rank, every rank becomes an RCCL-free
+    shard (mgicp_comm_init(ctx, N, r, NULL)): the target's covariances are then computed whole on every
+    rank (per-point values, the same bits as the split + all-gather) and the per-pass rows go through the
+    node-wide shared segment (or over xGMI).  force_rccl_fail: take that path without trying RCCL (test).
+
+    probe: optional (source, target) clouds for one align through the xGMI exchange; a failure there
+    falls back to the host segment.  Returns {"transport": str, "rccl": bool, "notes": [...]}.
+    """
+    notes = []
+    cerr = None
+    if force_rccl_fail:
+        cerr = "forced (force_rccl_fail)"
+    else:
+        uid = b""
+        if rank == 0:
+            try:
+                uid = type(eng).unique_id()
+            except Exception as exc:  # noqa: BLE001 -- rank 0's id failed: nobody tries RCCL
+                cerr = f"unique id: {exc}"
+        uid = pg.broadcast(uid if rank == 0 else None)
+        if not uid:
+            cerr = cerr or "unique id unavailable on rank 0"
+        else:
+            try:
+                eng.comm_init(world, rank, uid)
+            except Exception as exc:  # noqa: BLE001 -- reported
+                cerr = f"ncclCommInitRank: {exc}"
+    rccl = pg.allreduce_max(1.0 if cerr else 0.0) == 0
+    if not rccl:
+        notes.append(f"RCCL unavailable ({cerr or 'on another rank'}): RCCL-free shards, target covariances "
+                     "computed whole on every rank")
+        eng.comm_init(world, rank, None)
+        if transport == "rccl":
+            transport = "shm"
+    if transport == "rccl":
+        return {"transport": "rccl", "rccl": True, "notes": notes}
+    import secrets
+
+    name = pg.broadcast(f"/mgicp_{os.getpid()}_{secrets.token_hex(6)}".encode() if rank == 0 else None)
+    err = None
+    try:
+        eng.attach_shm(name.decode(), n_source)
+    except Exception as exc:  # noqa: BLE001 -- reported
+        err = str(exc)
+    if pg.allreduce_max(1.0 if err else 0.0) > 0:
+        if not err:
+            eng.detach_shm()
+        if not rccl:
+            raise RuntimeError(f"no exchange for {world} ranks: RCCL ({cerr}) and the shared segment "
+                               f"({err or 'on another rank'}) both failed")
+        return {"transport": f"rccl (shared segment unavailable: {err or 'on another rank'})", "rccl": True,
+                "notes": notes}
+    tail = "rccl (target covariances)" if rccl else "no RCCL (target covariances computed on every rank)"
+    out = {"transport": f"shm rows + {tail}", "rccl": rccl, "notes": notes}
+    if transport != "xgmi":
+        return out
+    xerr = None
+    try:
+        eng.attach_xgmi()
+    except Exception as exc:  # noqa: BLE001 -- reported
+        xerr = str(exc)
+    if pg.allreduce_max(1.0 if xerr else 0.0) > 0:
+        if not xerr:
+            eng.attach_xgmi(False)
+        out["transport"] = f"shm rows (xGMI exchange unavailable: {xerr or 'on another rank'}) + {tail}"
+        return out
+    out["transport"] = f"xGMI row exchange + device totals; shm rendezvous/gathers; {tail}"
+    if probe is not None:
+        # one align on a sample through the exchange: if rows written into peer GPUs' memory never show up
+        # there, every rank falls back to the host segment (the same sums) instead of failing the run
+        perr = None
+        try:
+            eng.set_source_xyz(probe[0])
+            eng.set_target_xyz(probe[1])
+            eng.align()
+        except Exception as exc:  # noqa: BLE001 -- reported
+            perr = str(exc)
+        if pg.allreduce_max(1.0 if perr else 0.0) > 0:
+            eng.attach_xgmi(False)
+            out["transport"] = f"shm rows (xGMI probe align failed: {perr or 'on another rank'}) + {tail}"
+    return out

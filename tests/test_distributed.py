@@ -817,3 +817,132 @@ def test_single_rank_comm_matches_plain(part_small, solver):
     np.testing.assert_array_equal(coll.align(), T_plain)  # iterate(): cached grids, same result
     coll.close()
     plain.close()
+
+
+class _FakeEngine:
+    """Records the transport calls setup_transport makes (CPU test of its decisions)."""
+
+    fail_comm_on = ()
+
+    def __init__(self, rank):
+        self.rank = rank
+        self.calls = []
+
+    @staticmethod
+    def unique_id():
+        return bytes(range(128))
+
+    def comm_init(self, world, rank, uid):
+        self.calls.append(("comm_init", uid is not None))
+        if uid is not None and rank in self.fail_comm_on:
+            raise RuntimeError("ncclCommInitRank: unhandled system error (simulated)")
+
+    def attach_shm(self, name, n):
+        self.calls.append(("attach_shm", name.startswith("/mgicp_")))
+
+    def detach_shm(self):
+        self.calls.append(("detach_shm",))
+
+    def attach_xgmi(self, on=True):
+        self.calls.append(("attach_xgmi", on))
+
+
+def _transport_worker(rank, world, port, fail_on, transport, q):
+    from leica_point_cloud_processing_amd.parallel import Rendezvous, setup_transport
+
+    pg = Rendezvous(rank, world, addr="127.0.0.1", port=port, timeout=60)
+    _FakeEngine.fail_comm_on = fail_on
+    eng = _FakeEngine(rank)
+    try:
+        tr = setup_transport(eng, pg, world, rank, transport, 1000)
+        q.put((rank, tr["transport"], tr["rccl"], eng.calls))
+    except Exception as exc:  # noqa: BLE001
+        q.put((rank, repr(exc), None, eng.calls))
+    pg.close()
+
+
+@pytest.mark.parametrize("fail_on,transport", [((), "xgmi"), ((1,), "xgmi"), ((0, 1), "rccl"), ((1,), "shm")])
+def test_setup_transport_degrades_when_rccl_fails(fail_on, transport):
+    """if ncclCommInitRank fails on ANY rank, EVERY rank becomes an RCCL-free shard
+    (comm_init(N, r, NULL)) and the rows go through the segment (an 'rccl' request too) / xGMI; all ranks
+    agree on the same transport."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_transport_worker, args=(r, world, port, fail_on, transport, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=60) for _ in procs), key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    names = {t for _, t, _, _ in res}
+    assert len(names) == 1, res
+    for rank, tname, rccl, calls in res:
+        assert rccl == (not fail_on), res
+        if fail_on:
+            assert ("comm_init", False) in calls, calls  # the RCCL-free shard
+            assert ("attach_shm", True) in calls, calls
+            assert "no RCCL" in tname
+        want_x = transport == "xgmi"
+        assert (("attach_xgmi", True) in calls) == want_x, calls
+        assert tname.startswith("xGMI" if want_x else "shm rows"), tname
+
+
+def _fallback_rank(world, rank, port, n, transport, q):
+    try:
+        from leica_point_cloud_processing_amd import synth
+        from leica_point_cloud_processing_amd.engine import GICPEngine
+        from leica_point_cloud_processing_amd.parallel import Rendezvous, setup_transport
+
+        os.environ["MGICP_REMOTE_DEADLINE_S"] = "20"
+        pg = Rendezvous(rank, world, addr="127.0.0.1", port=port, timeout=120)
+        scan, cad, _ = synth.scan_vs_cad(n, n)
+        e = GICPEngine(device=0, options={"srv_cus": 80})
+        tr = setup_transport(e, pg, world, rank, transport, n, force_rccl_fail=True)
+        e.set_source_xyz(scan)
+        e.set_target_xyz(cad)
+        T = e.align()
+        res = (e.last_result["iterations"], e.last_result["n_evals"], e.last_result["n_corr"])
+        st = e.pass_stats()
+        e.close()
+        pg.close()
+        q.put((rank, T, res, st, tr["transport"]))
+    except Exception as exc:  # noqa: BLE001
+        q.put((rank, repr(exc), None, None, None))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("transport", ["shm", "xgmi"])
+def test_rccl_free_fallback_bitwise_single(transport):
+    """a 2-process run whose RCCL init 'failed' (setup_transport(force_rccl_fail)) runs
+    as RCCL-free shards -- the target's covariances computed whole on each rank, rows through the segment
+    or the xGMI exchange -- and gives T, iterations, passes and n_corr bitwise equal to one context."""
+    from leica_point_cloud_processing_amd import synth
+    from leica_point_cloud_processing_amd.engine import GICPEngine
+
+    n, world = 300_000, 2
+    scan, cad, _ = synth.scan_vs_cad(n, n)
+    ref = GICPEngine()
+    ref.set_source_xyz(scan)
+    ref.set_target_xyz(cad)
+    T_ref = ref.align()
+    res_ref = (ref.last_result["iterations"], ref.last_result["n_evals"], ref.last_result["n_corr"])
+    ref.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fallback_rank, args=(world, r, port, n, transport, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = sorted((q.get(timeout=240) for _ in procs), key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, T, res, st, tname in got:
+        assert not isinstance(T, str), T
+        np.testing.assert_array_equal(T, T_ref)
+        assert res == res_ref
+        assert st["transport"] == (4 if transport == "xgmi" else 2), st
+        assert "no RCCL" in tname, tname

@@ -148,6 +148,65 @@ def test_c4f_steady_state_cell_lists_vs_oracle():
     e0.close()
 
 
+def test_reused_context_equals_fresh_context_c4f():
+    """an align is a function of its inputs, not of the context's history.  The
+    reference's setters on a reused GICPAlignment (setSourceCloud / setTargetCloud, then run();
+    include/GICPAlignment.h, src/GICPAlignment.cpp:89-96) must give what a fresh object gives:
+      (a) one context aligns C4, then gets C4F's clouds through set_source / set_target;
+      (b) one context aligns C4F's scan against a different target (every other CAD point), then gets
+          only C4F's target (the source kept: its grid was sized against the other target and must be
+          rebuilt against this one);
+    each final align equals a fresh context BITWISE (T, iterations, passes, n_corr) and the full-size
+    oracle (iterations, n_corr, T <= 1e-4; unpinned against PCL binaries).  C4F is the knife-edge
+    config: r05 saw 4 iterations against the oracle's 3 from a source grid sized differently."""
+    from leica_point_cloud_processing_amd import synth
+    from leica_point_cloud_processing_amd.engine import GICPEngine
+
+    c = CONFIGS["C4F"]
+    scan, cad, _, T_ref, info = _clouds_and_oracle("C4F")
+
+    def result(e):
+        r = e.last_result
+        return (r["iterations"], r["n_evals"], r["n_corr"])
+
+    fresh = GICPEngine(max_iter=c["max_iter"])
+    fresh.set_source_xyz(scan)
+    fresh.set_target_xyz(cad)
+    T_f = fresh.align()
+    res_f = result(fresh)
+    fresh.close()
+    assert res_f[0] == info["iterations"] and res_f[2] == info["n_corr_last"], (res_f, info["iterations"])
+    assert frob(T_f, T_ref) <= FROB_TOL
+
+    c4 = CONFIGS["C4"]
+    s4, t4, _ = synth.scan_vs_cad(c4["n"], c4["nt"])
+    a = GICPEngine(max_iter=c["max_iter"])
+    a.set_source_xyz(s4)
+    a.set_target_xyz(t4)
+    a.align()
+    a.align()
+    a.set_source_xyz(scan)
+    a.set_target_xyz(cad)
+    T_a = a.align()
+    res_a = result(a)
+    a.close()
+    del s4, t4
+
+    b = GICPEngine(max_iter=c["max_iter"])
+    b.set_source_xyz(scan)
+    b.set_target_xyz(np.ascontiguousarray(cad[::2]))
+    b.align()
+    b.set_target_xyz(cad)  # the source is kept
+    T_b = b.align()
+    res_b = result(b)
+    b.close()
+    print(f"C4F fresh {res_f} | reused after C4 {res_a} frob {frob(T_a, T_f):.3e} | new target only {res_b} "
+          f"frob {frob(T_b, T_f):.3e} | oracle its {info['iterations']} n_corr {info['n_corr_last']}")
+    np.testing.assert_array_equal(T_a, T_f)
+    np.testing.assert_array_equal(T_b, T_f)
+    assert res_a == res_f and res_b == res_f
+
+
 def test_state_machine_identical_clouds_known_answer():
     """test_state_machine.cpp:31-47,51-80: cubePointCloud(cloud, 1, 10000) with glibc rand() from its
     default seed, source_cloud == target_cloud, GICPState at defaults (gicp_with_covariances false,
