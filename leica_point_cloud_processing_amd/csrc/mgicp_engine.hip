@@ -860,7 +860,10 @@ int cov_prep_async(mgicp_ctx* ctx, bool tgt) {
   // cap -- scan clutter, debris -- is left to the lazy pass, which computes it only if a sweep accepts
   // it; r04 C4F: the uncapped head start spent ~40 ms on them); its points are marked in cov_ok
   const bool capped = !tgt && ctx->lazy_src_cov && ctx->knn_logged && ctx->async_ring_cap >= 0;
-  ctx->src_async_lazy = capped;
+  // r06 fix: the flag belongs to the SOURCE's launch -- the target's head start (set_target after
+  // set_source on a context whose old target let the source start first) must not clear it, or the
+  // source's join would mark the points its capped launch gave up on as computed (stale covariances)
+  if (!tgt) ctx->src_async_lazy = capped;
   if (capped) {
     HIPCK(ctx->cov_ok.reserve(c.n));
     HIPCK(ctx->cov_need.reserve(c.n));

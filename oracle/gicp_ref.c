@@ -358,6 +358,11 @@ struct ref_gicp {
     double mom[MOM_VALS];
     float T0[4][4];
     double ctr[3];
+    /* summation-order ledger (r06, ref_set_sum_order): 0 the order above, 1 the engine's fixed tree over
+     * sum_perm, 2 reversed sequential, 3 sequential over sum_perm */
+    int sum_mode;
+    uint32_t* sum_perm; /* ns entries: stream position -> source index */
+    int* sum_tj;        /* per source index: its correspondence slot, -1 = rejected (scratch) */
 };
 
 void ref_default_params(ref_params* p) {
@@ -388,6 +393,11 @@ int ref_set_params(ref_gicp* g, const ref_params* p) {
     return REF_OK;
 }
 
+static void free_sum_order(ref_gicp* g) {
+    free(g->sum_perm); free(g->sum_tj);
+    g->sum_perm = NULL; g->sum_tj = NULL; g->sum_mode = 0;
+}
+
 static void free_scratch(ref_gicp* g) {
     free(g->out); free(g->mahal); free(g->corr_src); free(g->corr_tgt);
     g->out = NULL; g->mahal = NULL; g->corr_src = g->corr_tgt = NULL; g->m = 0;
@@ -398,6 +408,7 @@ void ref_destroy(ref_gicp* g) {
     kd_free(&g->tree_src); kd_free(&g->tree_tgt);
     free(g->src); free(g->tgt); free(g->cov_src); free(g->cov_tgt);
     free_scratch(g);
+    free_sum_order(g);
     free(g);
 }
 
@@ -414,6 +425,7 @@ static float* copy_xyz(const float* xyz, size_t n, size_t stride, int* bad) {
 }
 
 int ref_set_source(ref_gicp* g, const float* xyz, size_t n, size_t stride) {
+    free_sum_order(g);  /* a stream order belongs to one source cloud */
     if (!g || (!xyz && n) || stride < 12) return REF_E_INVALID;
     int bad;
     free(g->src);
@@ -879,6 +891,76 @@ static int estimate_gn(ref_gicp* g, float T[4][4]) {
     return 0;
 }
 
+/* ---- summation-order ledger (r06) ------------------------------------------
+ * The engine sums a pass over a FIXED tree keyed to its source stream order (mgicp_kernels.hip
+ * fdf_soa_body / chunk_store / wave_tickets / wave_total): chunks of 1024 stream positions; in a chunk
+ * the accepted correspondences are compacted in stream order into groups of 4, lane l of the wave takes
+ * groups l, l + 64, ... and accumulates their terms in order; the 64 lane sums meet in the shuffle tree
+ * (pairs l, l + d for d = 32 ... 1); a super = 32 consecutive chunks, summed in chunk order from the
+ * first; the total: lane l sums supers l, l + 64, ... from 0.0, then the same shuffle tree.  Restated
+ * here over any stream order (sum_perm), so the oracle can run the BFGS on the engine's sums, on
+ * another order's, or on a reversed sequential sum -- the spread of iterations and T over orders. */
+static void acc_add(fdf_acc* a, const fdf_acc* b) {
+    a->f = a->f + b->f;
+    for (int k = 0; k < 3; ++k) a->gt[k] = a->gt[k] + b->gt[k];
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) a->R[r][c] = a->R[r][c] + b->R[r][c];
+}
+static void lane_tree(fdf_acc* lanes) { /* lanes[0] = the 64-lane shuffle tree */
+    for (int off = 32; off > 0; off >>= 1)
+        for (int i = 0; i < off; ++i) acc_add(&lanes[i], &lanes[i + off]);
+}
+static void fdf_tree(ref_gicp* g, const float A[4][4], fdf_acc* tot) {
+    const int ns = g->ns, nch = (ns + 1023) / 1024, nsup = (nch + 31) / 32;
+    fdf_acc* chunk = (fdf_acc*)calloc((size_t)nch, sizeof(fdf_acc));
+    fdf_acc lanes[64], one;
+    int* list = (int*)malloc(1024 * sizeof(int));
+    for (int j = 0; j < nch; ++j) {
+        int cnt = 0;
+        for (int p = 1024 * j; p < ns && p < 1024 * (j + 1); ++p) {
+            const int slot = g->sum_tj[g->sum_perm[p]];
+            if (slot >= 0) list[cnt++] = slot;
+        }
+        memset(lanes, 0, sizeof(lanes));
+        for (int k = 0; k < cnt; ++k) {
+            const int lane = (k / 4) % 64;
+            fdf_range(g, A, list[k], list[k] + 1, &one);
+            acc_add(&lanes[lane], &one);
+        }
+        lane_tree(lanes);
+        chunk[j] = lanes[0];
+    }
+    memset(lanes, 0, sizeof(lanes));
+    for (int sj = 0; sj < nsup; ++sj) {
+        fdf_acc a = chunk[32 * sj];
+        for (int q = 1; q < 32 && 32 * sj + q < nch; ++q) acc_add(&a, &chunk[32 * sj + q]);
+        acc_add(&lanes[sj % 64], &a);
+    }
+    lane_tree(lanes);
+    *tot = lanes[0];
+    free(list);
+    free(chunk);
+}
+
+int ref_set_sum_order(ref_gicp* g, int mode, const uint32_t* perm, size_t n) {
+    if (!g || mode < 0 || mode > 3) return REF_E_INVALID;
+    free_sum_order(g);
+    if (mode == 1 || mode == 3) {
+        if (!perm || n != (size_t)g->ns) return REF_E_INVALID;
+        g->sum_perm = (uint32_t*)malloc(n * sizeof(uint32_t));
+        g->sum_tj = (int*)malloc(n * sizeof(int));
+        char* seen = (char*)calloc(n, 1);
+        for (size_t p = 0; p < n; ++p) {
+            if (perm[p] >= n || seen[perm[p]]) { free(seen); free_sum_order(g); return REF_E_INVALID; }
+            seen[perm[p]] = 1;
+            g->sum_perm[p] = perm[p];
+        }
+        free(seen);
+    }
+    g->sum_mode = mode;
+    return REF_OK;
+}
+
 static void functor_eval(ref_gicp* g, const double x[6], double* f, double grad[6]) {
     if (g->prm.objective == 1) {
         moments_eval(g, x, f, grad);
@@ -889,7 +971,26 @@ static void functor_eval(ref_gicp* g, const double x[6], double* f, double grad[
     int m = g->m;
     int nt = g->prm.threads > 1 ? g->prm.threads : 1;
     fdf_acc tot;
-    if (nt == 1) {
+    if (g->sum_mode) {
+        if (g->sum_mode == 2) {  /* reversed sequential */
+            fdf_acc one;
+            memset(&tot, 0, sizeof(tot));
+            for (int c = m - 1; c >= 0; --c) { fdf_range(g, A, c, c + 1, &one); acc_add(&tot, &one); }
+        } else {
+            for (int i = 0; i < g->ns; ++i) g->sum_tj[i] = -1;
+            for (int c = 0; c < m; ++c) g->sum_tj[g->corr_src[c]] = c;
+            if (g->sum_mode == 1) {
+                fdf_tree(g, A, &tot);
+            } else {  /* sequential over sum_perm */
+                fdf_acc one;
+                memset(&tot, 0, sizeof(tot));
+                for (int p = 0; p < g->ns; ++p) {
+                    const int c = g->sum_tj[g->sum_perm[p]];
+                    if (c >= 0) { fdf_range(g, A, c, c + 1, &one); acc_add(&tot, &one); }
+                }
+            }
+        }
+    } else if (nt == 1) {
         fdf_range(g, A, 0, m, &tot);
     } else {
         fdf_acc* parts = (fdf_acc*)calloc((size_t)nt, sizeof(fdf_acc));

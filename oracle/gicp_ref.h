@@ -105,6 +105,10 @@ int ref_fdf(ref_gicp* g, const double x[6], double* f, double g6[6]);
 /* raw sums of the functor over correspondences [c0, c1): f, g_t[3], Rsum[9] row-major, count
  * (the per-shard partials of the multi-GPU decomposition) */
 int ref_fdf_sums(ref_gicp* g, const double x[6], int c0, int c1, double out14[14]);
+/* r06 summation-order ledger: every later objective pass sums in mode 0 (the default: sequential in
+ * correspondence order, or the OpenMP parts), 1 (the engine's fixed chunk -> super -> total tree over
+ * the stream order perm[0..n), n = source points), 2 (reversed sequential) or 3 (sequential over perm) */
+int ref_set_sum_order(ref_gicp* g, int mode, const uint32_t* perm, size_t n);
 /* applyState(I, x): column-major float 4x4. */
 void ref_apply_state(const double x[6], float out_cm[16]);
 

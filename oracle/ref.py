@@ -77,6 +77,7 @@ def load():
         "ref_moments": (ctypes.c_int, [P, FP, DP]),
         "ref_moments_range": (ctypes.c_int, [P, FP, ctypes.c_int, ctypes.c_int, DP]),
         "ref_fdf_sums": (ctypes.c_int, [P, DP, ctypes.c_int, ctypes.c_int, DP]),
+        "ref_set_sum_order": (ctypes.c_int, [P, ctypes.c_int, P, sz]),
         "ref_apply_state": (None, [DP, FP]),
         "ref_segment_differences": (ctypes.c_int, [P, sz, sz, P, sz, sz, ctypes.c_double, P, ctypes.POINTER(sz)]),
         "ref_voxel_grid": (ctypes.c_int, [P, sz, sz, ctypes.c_int, FP, ctypes.c_int, FP, P, ctypes.POINTER(sz),
@@ -181,6 +182,15 @@ class RefGICP:
         g = cm(np.eye(4) if guess is None else guess)
         m = self.lib.ref_correspondences(self.h, _fp(cm(T)), _fp(g), _ip(tgt), _fp(d2), _dp(M))
         return m, tgt, d2, M
+
+    def set_sum_order(self, mode: int, perm=None):
+        """r06 summation-order ledger (gicp_ref.h ref_set_sum_order): 0 default, 1 the engine's fixed tree
+        over the stream order `perm` (source indices), 2 reversed sequential, 3 sequential over `perm`."""
+        buf = None if perm is None else np.ascontiguousarray(perm, np.uint32)
+        rc = self.lib.ref_set_sum_order(self.h, int(mode), None if buf is None else buf.ctypes.data,
+                                        0 if buf is None else len(buf))
+        assert rc == 0, rc
+        self._sum_perm = buf
 
     def fdf_sums(self, x, c0, c1):
         x = np.asarray(x, np.float64)

@@ -1,8 +1,8 @@
-# r06 check: GPU suite, smoke, default C4 and C4F bench lines -> gpurun_out/r05/<name>
+# r06 check: GPU suite, smoke, default C4 and C4F bench lines -> gpurun_out/r06/<name>
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/r06/${1:-check}; mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests -x -v --timeout 300 --timeout-method thread -m gpu -rP > $O/pytest_gpu.log 2>&1 || { echo "pytest failed"; grep -E "FAILED|Error" $O/pytest_gpu.log | head; exit 1; }
+timeout -k 10 800 python -u -m pytest tests -x -v --timeout 300 --timeout-method thread -m gpu -rP > $O/pytest_gpu.log 2>&1 || { echo "pytest failed"; grep -E "FAILED|Error" $O/pytest_gpu.log | head; exit 1; }
 tail -1 $O/pytest_gpu.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke failed"; tail -20 $O/smoke.log; exit 1; }
 cat $O/smoke.log

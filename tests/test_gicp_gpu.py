@@ -719,3 +719,38 @@ def test_growing_clouds_reuse_buffers_bitwise(engine_mod):
         assert e.last_result["iterations"] == f.last_result["iterations"]
         f.close()
     e.close()
+
+
+def test_reused_context_source_first_lazy_covariances(engine_mod):
+    """r06 bug fix: on a context that already holds a target, set_source starts the source's ring-capped
+    head start at once (lazy mode) and set_target's head start then ran -- and cleared the flag that
+    leaves the capped-out points (clutter, debris) to the lazy pass, so the source's join marked them
+    computed with the previous cloud's covariances (20 594 wrong rows at 1M, max error 1.0; the C4F
+    align then took 4 iterations instead of 3).  The reference's order (setSourceCloud, then
+    setTargetCloud, GICPAlignment.cpp:89-90) on a reused context must equal a fresh context: every
+    source covariance, a sweep's matrices and the align."""
+    from leica_point_cloud_processing_amd import synth
+
+    n = 600_000
+    scan, cad, _ = synth.scan_vs_cad(n, n, clutter=0.04, debris=n // 125)
+    s0, t0, _ = synth.scan_vs_cad(n, n)
+    got = []
+    for reuse in (False, True):
+        for what in ("align", "cov"):
+            e = engine_mod()
+            if reuse:
+                e.set_source_xyz(s0)
+                e.set_target_xyz(t0)
+                e.align()
+            e.set_source_xyz(scan)
+            e.set_target_xyz(cad)
+            if what == "align":
+                T = e.align()
+                res = (e.last_result["iterations"], e.last_result["n_evals"], e.last_result["n_corr"])
+            else:
+                cs = e.debug_covariances("source", len(scan))
+            e.close()
+        got.append((T, res, cs))
+    np.testing.assert_array_equal(got[1][0], got[0][0])
+    assert got[1][1] == got[0][1]
+    np.testing.assert_array_equal(got[1][2], got[0][2])
