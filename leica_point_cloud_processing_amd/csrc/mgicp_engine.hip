@@ -556,10 +556,6 @@ struct mgicp_ctx {
   DevBuf<uint32_t> knn_fb2;         // the source's hand-off list
   bool knn_logged = true;           // wave-staged k-NN kernel + hand-off (debug option "knn_logged" 0: register-list only)
   DevBuf<uint32_t> knn_fb;          // points the logged k-NN kernel leaves to the register-list one
-  // r06: the logged k-NN kernel's certified moment sums (10 doubles per point of the cloud), finished by
-  // knn_finish_kernel -- one buffer per stream (debug option "knn_split" 0: the finish inside the search)
-  bool knn_split = true;
-  DevBuf<double> knn_mom, aux_mom;
   unsigned int knn_fallbacks = 0;   // their count in the last covariance launch
   DevBuf<float> fpartial;
   // the target's 1-NN cell lists (r04, DESIGN.md "1-NN cell lists"; debug option "vlist" 0: the r03 sweeps)
@@ -893,16 +889,11 @@ int cov_prep_async(mgicp_ctx* ctx, bool tgt) {
       ctx->qperm_aux = true;
     }
   }
-  double* mom = nullptr;
-  if (ctx->knn_logged && ctx->knn_split) {  // shared by both clouds' launches: they run in aux-stream order
-    HIPCK(ctx->aux_mom.reserve(kMomDoubles * c.n));
-    mom = ctx->aux_mom.p;
-  }
   HIPCK(launch_knn_cov(c.view, ctx->prm.k, ctx->prm.gicp_eps, 0, c.n, c.cov3(), nullptr,
                        ctx->knn_logged ? (tgt ? ctx->knn_fb.p : ctx->knn_fb2.p) : nullptr,
                        ctx->knn_logged ? ctx->aux_cnt.p + (tgt ? 0 : 1) : nullptr, ctx->aux_stream,
                        capped ? ctx->async_ring_cap : -1, capped ? ctx->cov_ok.p : nullptr,
-                       ctx->knn_logged ? 2 * std::max(ctx->cus, 1) : 0, mom));
+                       ctx->knn_logged ? 2 * std::max(ctx->cus, 1) : 0));
   HIPCK(hipEventRecord(ctx->aux_ev[tgt ? 0 : 1], ctx->aux_stream));
   MGICP_TRACE_AT(tgt ? "head start: target k-NN queued" : "head start: source k-NN queued");
   (tgt ? ctx->tgt_cov_pending : ctx->src_cov_pending) = true;
@@ -1432,14 +1423,8 @@ int compute_cov(mgicp_ctx* ctx, Cloud& cl, size_t p0, size_t p1, size_t stride =
   unsigned int* fb_count = reinterpret_cast<unsigned int*>(ctx->u64.p);
   {
     ProfScope ps(ctx, kFamCov);
-    double* mom = nullptr;
-    if (logged && ctx->knn_split) {
-      HIPCK(ctx->knn_mom.reserve(kMomDoubles * cl.n));
-      mom = ctx->knn_mom.p;
-    }
     HIPCK(launch_knn_cov(cl.view, ctx->prm.k, ctx->prm.gicp_eps, p0, p1, cl.cov3(), perm,
-                         logged ? ctx->knn_fb.p : nullptr, logged ? fb_count : nullptr, ctx->stream, -1, nullptr, 0,
-                         mom));
+                         logged ? ctx->knn_fb.p : nullptr, logged ? fb_count : nullptr, ctx->stream));
   }
   if (logged) {
     // the points the logged kernel left to the register-list kernel (log overflow, ties at tau)
@@ -1567,14 +1552,8 @@ int cov_lazy(mgicp_ctx* ctx) {
   if (logged) HIPCK(ctx->knn_fb.reserve(need));
   {
     ProfScope ps(ctx, kFamCov);
-    double* mom = nullptr;
-    if (logged && ctx->knn_split) {
-      HIPCK(ctx->knn_mom.reserve(kMomDoubles * ctx->src.n));
-      mom = ctx->knn_mom.p;
-    }
     HIPCK(launch_knn_cov(ctx->src.view, ctx->prm.k, ctx->prm.gicp_eps, 0, need, ctx->src.cov3(), ctx->cov_need.p,
-                         logged ? ctx->knn_fb.p : nullptr, logged ? cnt + 1 : nullptr, ctx->stream, -1, nullptr, 0,
-                         mom));
+                         logged ? ctx->knn_fb.p : nullptr, logged ? cnt + 1 : nullptr, ctx->stream));
   }
   if (logged) {
     HIPCK(hipMemcpyAsync(ctx->h_small, cnt + 1, sizeof(unsigned int), hipMemcpyDeviceToHost, ctx->stream));
@@ -3819,9 +3798,6 @@ int mgicp_debug_option(mgicp_ctx* ctx, const char* name, double value) {
     ctx->lazy_src_cov = on;
     ctx->src.have_cov = false;
     ctx->src_lazy_ready = false;
-  } else if (n == "knn_split") {                        // k-NN: the fp64 finish in its own kernel (1) or in the search (0)
-    if (int rj = cov_join_all(ctx)) return rj;
-    ctx->knn_split = on;
   } else if (n == "knn_logged") {                       // k-NN: the logged kernel + hand-off (1) or the register-list kernel only (0)
     ctx->knn_logged = on;
     ctx->src.have_cov = ctx->tgt.have_cov = false;

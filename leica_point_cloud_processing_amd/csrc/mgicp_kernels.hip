@@ -973,26 +973,6 @@ struct SumCert {
   }
 };
 
-constexpr size_t kMomStride = kMomDoubles;  // doubles per point of the certified moment sums (9 + the marker)
-
-// r06: the fp64 finish of the logged k-NN kernel's certified points -- mean, centred moments, Jacobi,
-// PCL's {1, 1, eps} regularisation (cov_finish, unchanged arithmetic) -- one thread per point at full
-// occupancy.  A point without the marker (ring-capped, uncertified: the register-list hand-off writes it)
-// is skipped.  perm: the same query list as the search launch.
-__global__ __launch_bounds__(256) void knn_finish_kernel(const double* __restrict__ mom, size_t p0, size_t p1,
-                                                         const uint32_t* __restrict__ perm, double kd, double eps,
-                                                         Cov3 cov) {
-  const size_t t = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (t >= p1 - p0) return;
-  const size_t p = p0 + (perm ? perm[t] : t);
-  const double2* m = reinterpret_cast<const double2*>(mom + kMomStride * p);
-  const double2 v4 = m[4];
-  if (v4.y != 1.0) return;
-  const double2 v0 = m[0], v1 = m[1], v2 = m[2], v3 = m[3];
-  double a[3][3] = {{v1.y, 0.0, 0.0}, {v2.x, v2.y, 0.0}, {v3.x, v3.y, v4.x}};
-  cov_finish(v0.x, v0.y, v1.x, a, kd, eps, cov, p);
-}
-
 // Logged-threshold k-NN covariance (default): ONE near-first ring search finds the exact k-th float
 // d2 (tau) with KthVisitor's med3 network while logging every candidate that was within the
 // threshold of its time into the lane's LDS log (compacted to the entries within the current
@@ -1008,8 +988,7 @@ template <int K>
 __global__ __launch_bounds__(64, MGICP_KNN_MINW) void knn_cov2_kernel(GridView g, double eps, size_t p0, size_t p1, Cov3 cov,
                                                       const uint32_t* __restrict__ perm, int nsent, int cap,
                                                       uint32_t* __restrict__ fb, unsigned int* __restrict__ fb_count,
-                                                      int ring_cap, uint8_t* __restrict__ ok_out,
-                                                      double* __restrict__ mom) {
+                                                      int ring_cap, uint8_t* __restrict__ ok_out) {
   extern __shared__ uint32_t s_pos[];
   const size_t t = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (t >= p1 - p0) return;
@@ -1027,10 +1006,7 @@ __global__ __launch_bounds__(64, MGICP_KNN_MINW) void knn_cov2_kernel(GridView g
   ring_search(g, q.x, q.y, q.z, v1);
   // ring_cap (the source's head start, lazy mode): a point whose k-NN lie farther out (clutter, debris)
   // is left to the lazy pass, which computes it only if a sweep accepts it (ok_out stays 0)
-  if (v1.gave_up) {
-    if (mom) mom[kMomStride * p + 9] = 0.0;  // no moments: the finish skips this point
-    return;
-  }
+  if (v1.gave_up) return;
 #if MGICP_KNN_DIV
   {  // [18] wave iterations of test() [19] max over lanes of the lane's tests [20] lane tests [21] waves
     // [22] search cycles [23] moments + finish cycles (shader clock, summed over waves)
@@ -1092,21 +1068,8 @@ __global__ __launch_bounds__(64, MGICP_KNN_MINW) void knn_cov2_kernel(GridView g
     }
     ok = m == kreal && c0.ok() && c1.ok() && c2.ok() && c00.ok() && c10.ok() && c11.ok() && c20.ok() &&
          c21.ok() && c22.ok();
-    if (ok && mom) {
-      // r06: the nine certified sums leave the search kernel (80 B per point) and
-      // knn_finish_kernel runs PCL's mean / Jacobi / regularisation at full occupancy -- the fp64 finish
-      // no longer holds this wave's LDS log and registers
-      double2* o = reinterpret_cast<double2*>(mom + kMomStride * p);
-      o[0] = make_double2(m0, m1);
-      o[1] = make_double2(m2, a[0][0]);
-      o[2] = make_double2(a[1][0], a[1][1]);
-      o[3] = make_double2(a[2][0], a[2][1]);
-      o[4] = make_double2(a[2][2], 1.0);
-    } else if (ok) {
-      cov_finish(m0, m1, m2, a, static_cast<double>(kreal), eps, cov, p);
-    }
+    if (ok) cov_finish(m0, m1, m2, a, static_cast<double>(kreal), eps, cov, p);
   }
-  if (!ok && mom) mom[kMomStride * p + 9] = 0.0;
 #if MGICP_KNN_DIV
   if (threadIdx.x == 0) atomicAdd(&g_corr_phase[23], __builtin_amdgcn_s_memtime() - kt0);
 #endif
@@ -3657,13 +3620,12 @@ static int knn_log_cap(int K) { return std::min(K + 28, 128); }
 template <int K>
 static hipError_t knn_cov_k(const GridView& g, double eps, size_t p0, size_t p1, Cov3 cov,
                             const uint32_t* perm, int k, uint32_t* fb, unsigned int* fb_count, hipStream_t s,
-                            int ring_cap, uint8_t* ok, int chain, double* mom) {
+                            int ring_cap, uint8_t* ok, int chain) {
   if (fb) {
     const int cap = knn_log_cap(K);
     knn_cov2_kernel<K><<<nblk(p1 - p0, 64), 64, cap * 64 * sizeof(uint32_t), s>>>(g, eps, p0, p1, cov, perm,
                                                                                  K - k, cap, fb, fb_count, ring_cap,
-                                                                                 ok, mom);
-    if (mom) knn_finish_kernel<<<nblk(p1 - p0), 256, 0, s>>>(mom, p0, p1, perm, static_cast<double>(k), eps, cov);
+                                                                                 ok);
     // chain: the hand-off follows at once in stream order, its count read on the device (a grid of
     // `chain` blocks striding over the list)
     if (chain > 0) knn_cov_kernel<K><<<chain, 256, 0, s>>>(g, eps, 0, 0, cov, fb, K - k, fb_count);
@@ -3679,22 +3641,22 @@ static hipError_t knn_cov_k(const GridView& g, double eps, size_t p0, size_t p1,
 // list: perm = fb, p0 = 0, p1 = count) the register-list kernel runs.
 hipError_t launch_knn_cov(const GridView& g, int k, double eps, size_t p0, size_t p1, Cov3 cov,
                           const uint32_t* perm, uint32_t* fb, unsigned int* fb_count, hipStream_t s, int ring_cap,
-                          uint8_t* ok, int chain, double* mom) {
+                          uint8_t* ok, int chain) {
   if (p1 <= p0) return hipSuccess;
   switch (k) {
-    case 5: return knn_cov_k<5>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain, mom);
-    case 10: return knn_cov_k<10>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain, mom);
-    case 15: return knn_cov_k<15>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain, mom);
-    case 20: return knn_cov_k<20>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain, mom);
-    case 25: return knn_cov_k<25>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain, mom);
-    case 30: return knn_cov_k<30>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain, mom);
+    case 5: return knn_cov_k<5>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain);
+    case 10: return knn_cov_k<10>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain);
+    case 15: return knn_cov_k<15>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain);
+    case 20: return knn_cov_k<20>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain);
+    case 25: return knn_cov_k<25>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain);
+    case 30: return knn_cov_k<30>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain);
     default: break;
   }
   if (k < 1 || k > kMaxK) return hipErrorInvalidValue;
-  if (k <= 8) return knn_cov_k<8>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain, mom);
-  if (k <= 16) return knn_cov_k<16>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain, mom);
-  if (k <= 24) return knn_cov_k<24>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain, mom);
-  return knn_cov_k<32>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain, mom);
+  if (k <= 8) return knn_cov_k<8>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain);
+  if (k <= 16) return knn_cov_k<16>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain);
+  if (k <= 24) return knn_cov_k<24>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain);
+  return knn_cov_k<32>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain);
 }
 
 

@@ -363,7 +363,7 @@ def test_seeded_correspondences_lattice_ties(engine_mod):
 @pytest.mark.gpu
 @pytest.mark.parametrize("k", [20, 7, 32])
 def test_logged_knn_matches_register_list(engine_mod, part_small, monkeypatch, capfd, k):
-    """The k-NN kernel (logged; debug option "knn_logged", default 1) sums the moments in log order when exactly k
+    """The k-NN kernel (wave-staged since r05; debug option "knn_logged", default 1) sums the moments in log order when exactly k
     entries fall within tau and the nine sums are certified order-independent; every other point
     goes to the register-list kernel.  Both paths must give the register-list kernel's covariances
     bit for bit -- on clouds built to hit the hand-off: a part centred on the origin (neighbours
@@ -382,17 +382,14 @@ def test_logged_knn_matches_register_list(engine_mod, part_small, monkeypatch, c
     handed = {}
     for name, pts in clouds.items():
         res = {}
-        # "1n": the logged kernel with its fp64 finish inside the search (r06 debug option "knn_split" 0);
-        # "1": the default since r06 -- the certified sums finished by knn_finish_kernel
-        for knn2 in ("0", "1n", "1"):
+        for knn2 in ("0", "1"):
             monkeypatch.setenv("MGICP_KNN_STATS", "1")
-            e = engine_mod(k=k, options={"knn_logged": int(knn2[0]), "knn_split": int(knn2 != "1n")})
+            e = engine_mod(k=k, options={"knn_logged": int(knn2)})
             e.set_source_xyz(pts)
             e.set_target_xyz(pts[: len(pts) // 2])
             res[knn2] = e.debug_covariances("source", len(pts))
             del e
         np.testing.assert_array_equal(res["1"], res["0"], err_msg=name)
-        np.testing.assert_array_equal(res["1n"], res["0"], err_msg=name)
         err = capfd.readouterr().err
         left = [int(l.split()[3]) for l in err.splitlines() if l.startswith("[knn]") and f"] {len(pts)} points" in l]
         handed[name] = left[-1] if left else None
