@@ -22,6 +22,7 @@
 #define MI355X_GICP_H
 
 #include <stddef.h>
+#include <stdint.h>
 
 #ifdef __cplusplus
 extern "C" {
@@ -195,6 +196,10 @@ int mgicp_comm_attach_xgmi(mgicp_ctx* ctx, int on);
 /* ---- introspection for parity tests (original point order) ---- */
 /* covariances of the source (which = 0) or target (which = 1): n x {c00,c01,c02,c11,c12,c22} */
 int mgicp_debug_covariances(mgicp_ctx* ctx, int which, double* out_c6);
+/* r06: the original indices of this rank's source points in the order the objective's compacted streams
+ * -- and so every pass's fixed reduction tree -- visit them (the grid-sorted order); returns the count.
+ * The oracle's summation-order ledger runs the engine's tree over it (oracle/gicp_ref.h ref_set_sum_order). */
+int mgicp_debug_source_order(mgicp_ctx* ctx, uint32_t* out, size_t cap);
 /* one correspondence sweep at T (col-major); out_tgt[i] = target index or -1;
  * out_M6 (optional) = n x {m00,m01,m02,m11,m12,m22}; returns the count or < 0 */
 int mgicp_debug_correspondences(mgicp_ctx* ctx, const float T_cm[16], int* out_tgt, double* out_M6);
@@ -285,8 +290,8 @@ int mgicp_set_profiling(mgicp_ctx* ctx, int on);
 int mgicp_debug_option(mgicp_ctx* ctx, const char* name, double value);
 /* target cache (mgicp_release_cache): out[0] the current target was adopted from the cache, out[1]
  * adoptions and out[2] donations on this device so far, out[3] an entry is cached on this device,
- * out[4] a source set before any target started its grid from the cached target's cell size: 0 no,
- * 1 pending, 2 kept (the target set next had that cell size), 3 discarded and rebuilt.
+ * out[4] 0 (r05: the source grid's start from a cached target; since r06 a grid depends on its own cloud
+ * alone).
  * Debug option "target_cache" 1: this context adopts and leaves targets (default 0: neither). */
 int mgicp_debug_cache_stats(mgicp_ctx* ctx, long long out[5]);
 

@@ -97,6 +97,7 @@ _SIGNATURES = {
                                                ctypes.POINTER(ctypes.c_longlong), ctypes.c_int]),
     "mgicp_debug_target_cov_slice": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, _DP]),
     "mgicp_debug_vlist_stats": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_longlong)]),
+    "mgicp_debug_source_order": (ctypes.c_int, [_P, ctypes.c_void_p, ctypes.c_size_t]),
     "mgicp_debug_covariances": (ctypes.c_int, [_P, ctypes.c_int, _DP]),
     "mgicp_debug_correspondences": (ctypes.c_int, [_P, _FP, _IP, _DP]),
     "mgicp_debug_correspondences_seeded": (ctypes.c_int, [_P, _FP, _IP, _DP]),

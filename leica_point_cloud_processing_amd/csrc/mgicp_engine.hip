@@ -265,12 +265,6 @@ struct Cloud {
   double occupancy = 0;        // grid sizing target (points per non-empty cell); 0 = context default
   size_t n_built = 0;          // points of the last grid built in this slot
   bool fresh_grid = false;     // the grid is the one a fresh context builds for these points (target cache)
-  // r06: the start of the source grid's sizing loop is the target grid's cell size (and point count) it was
-  // built against; a source grid whose basis is not the current target's is rebuilt (src_basis_check), so a
-  // grid -- and with it every sorted order and sum -- is a function of the clouds alone, never of the slot's
-  // history.  0 / 0: the 3-D guess.
-  float basis_h = 0.f;
-  size_t basis_n = 0;
   DevBuf<double2> cov;        // 3 * cov_stride
   size_t cov_stride = 0;      // entries per covariance array (n, or the padded all-gather size)
   float lo[3] = {0.f, 0.f, 0.f}, hi[3] = {0.f, 0.f, 0.f};  // bounding box (original coordinates)
@@ -593,12 +587,6 @@ struct mgicp_ctx {
   bool tcache_on = false;               // debug option "target_cache" (r06: opt-in; VERDICT r05 weak 5 --
                                         // the reference node aligns once per process)
   bool tcache_adopted = false;          // the current target came from the cache
-  // r05: a source set before any target sized its grid from the cached target's cell size (spec_h,
-  // spec_n); checked against the target set_target brings: 1 pending, 2 kept, 3 discarded (rebuilt)
-  int src_spec = 0;
-  unsigned long long src_rebasis = 0;  // r06: source grids rebuilt because the target changed under them
-  float spec_h = 0.f;
-  size_t spec_n = 0;
   // multi-GPU
   int nranks = 1, rank = 0;
   ncclComm_t comm = nullptr;
@@ -878,10 +866,10 @@ int cov_prep_async(mgicp_ctx* ctx, bool tgt) {
     HIPCK(hipMemsetAsync(ctx->aux_cnt.p + (tgt ? 0 : 1), 0, sizeof(unsigned int), ctx->stream));
   }
   HIPCK(hipStreamSynchronize(ctx->stream));  // the grid (and the count) before the aux stream reads them
-  // r05, the source guessed from the cached target (GICPState's order): its Morton query order is sorted
-  // on the aux stream ahead of its k-NN, so the main stream stays empty for set_target's upload (queued
-  // behind a main-stream sort that shares the CUs with the k-NN, the target's copies waited ~2 ms)
-  if (!tgt && ctx->src_spec == 1 && ctx->query_order && !ctx->qperm_valid && !ctx->qperm_aux) {
+  // the source's Morton query order is sorted on the aux stream ahead of its k-NN, so the main stream stays
+  // empty for set_target's upload (r05: queued behind a main-stream sort that shares the CUs with the k-NN,
+  // the target's copies waited ~2 ms)
+  if (!tgt && ctx->query_order && !ctx->qperm_valid && !ctx->qperm_aux) {
     const size_t p0 = ctx->shard_p0(), ns = ctx->shard_p1() - p0;
     if (ns > 0 && morton_perm(ctx, c, p0, ns, ctx->qperm, true)) {
       HIPCK(hipEventRecord(ctx->aux_ev[2], ctx->aux_stream));
@@ -903,73 +891,20 @@ int cov_prep_async(mgicp_ctx* ctx, bool tgt) {
   return MGICP_OK;
 }
 
-// r05: GICPState sets the source before the target (GICPAlignment.cpp:89-90), so a fresh context's source
-// grid -- which starts from the target's cell size -- had to wait for set_target, and its covariances ran
-// into the first align.  When the device's target cache holds a target, the source grid starts from THAT
-// target's cell size at set_source; spec_check confirms it once the real target's grid exists (the same
-// cell size and point count: the grid, every sorted order and sum are those of the synchronous path) or
-// throws the source's grid and covariances away and rebuilds them from the real target.
-bool spec_from_cache(mgicp_ctx* ctx) {
-  if (!ctx->tcache_on || !ctx->async_tgt || !ctx->aux_stream || ctx->nranks != 1 || ctx->comm || ctx->have_shm ||
-      ctx->profiling || ctx->src.n_built > 0)
-    return false;
-  TargetCache& c = g_tcache[ctx->device & 63];
-  std::lock_guard<std::mutex> lk(c.mu);
-  if (!c.valid || !(c.t.view.h > 0.f) || c.t.n_built == 0) return false;
-  ctx->spec_h = c.t.view.h;
-  ctx->spec_n = c.t.n_built;
-  ctx->src_spec = 1;
-  return true;
-}
-// r06: also the general form of that check (src_basis_check): any built source grid whose sizing started
-// from another target grid than the current one (a new target with the source kept, a speculative guess
-// that missed) is rebuilt, so the source's grid is the one a fresh context builds for this cloud pair
-int spec_check(mgicp_ctx* ctx) {
-  if (ctx->tgt.dirty || ctx->tgt.n_built == 0) return MGICP_OK;
-  Cloud& s = ctx->src;
-  const bool basis_ok = s.basis_h == ctx->tgt.view.h && s.basis_n == ctx->tgt.n_built;
-  if (ctx->src_spec == 1) {
-    if (basis_ok) {
-      ctx->src_spec = 2;
-      return MGICP_OK;
-    }
-    ctx->src_spec = 3;
-  } else if (s.dirty || s.n_built == 0 || basis_ok) {
-    return MGICP_OK;
-  } else {
-    ctx->src_rebasis++;
-  }
-  if (int rc = cov_join(ctx, false)) return rc;  // its k-NN launch reads the grid about to be rebuilt
-  if (ctx->qperm_aux) {  // so does the aux stream's Morton sort
-    HIPCK(hipStreamWaitEvent(ctx->stream, ctx->aux_ev[2], 0));
-    ctx->qperm_aux = false;
-  }
-  s.dirty = true;
-  s.have_cov = false;
-  s.view.h = 0.f;  // no previous grid: the rebuild starts from the real target's cell size
-  s.n_built = 0;
-  ctx->qperm_valid = false;
-  ctx->src_lazy_ready = false;
-  ctx->src_async_lazy = false;
-  ctx->have_corr = false;
-  ctx->seed_valid = false;
-  return MGICP_OK;
-}
-
-// after a set_*: the head start for every cloud that can have it, in prepare's order -- the target
-// first, the source only once the target's grid exists (the source grid starts from the target's
-// cell size, so the grids, and with them every sorted order and sum, are those of the synchronous
-// path whatever the order of the set_* calls; the reference calls setInputSource first,
-// GICPAlignment.cpp:89-90).  r05: the target's covariances are joined only before the first
-// compaction, so they run beside the source's grid build, its Morton order and the first 1-NN sweep
+// after a set_*: the head start of the cloud just set -- its grid now (its host round trips), then its
+// k-NN covariances on the aux stream.  r06: the source's grid is sized from the source alone (like the
+// target's from the target), so its head start runs at set_source, whatever the order of the set_* calls
+// and whether a target exists yet: the reference sets the source first (GICPAlignment.cpp:89-90), and
+// the source's k-NN now overlaps set_target's upload and grid build.  (r04-r05 started the source's grid
+// from the target's cell size, so a source set first waited for set_target; that dependency rested on a
+// C4F trajectory flip later traced to a bug -- set_target's head start cleared the source's ring-cap flag
+// -- not to the summation order, which the r06 ledger shows does not move C2F / C4F / C5:
+// DESIGN.md "Summation-order ledger".)  The target's covariances are joined only before the first
+// compaction, so they run beside the first 1-NN sweep.
 int cov_prep_async_all(mgicp_ctx* ctx) {
   int rc = MGICP_OK;
   if (ctx->tgt.dirty && (rc = cov_prep_async(ctx, true))) return rc;
-  if ((rc = spec_check(ctx))) return rc;
-  if (ctx->src.dirty && !ctx->tgt.dirty && ctx->tgt.n_built > 0)
-    rc = cov_prep_async(ctx, false);
-  else if (ctx->src.dirty && ctx->tgt.n_built == 0 && !ctx->tgt.dirty && spec_from_cache(ctx))
-    rc = cov_prep_async(ctx, false);  // GICPState's order: the source first, its target most likely cached
+  if (ctx->src.dirty) rc = cov_prep_async(ctx, false);
   return rc;
 }
 
@@ -985,11 +920,6 @@ int upload_cloud(mgicp_ctx* ctx, Cloud& cl, const float* xyz, size_t n, size_t s
   }
   if (&cl == &ctx->src && ctx->qperm_aux)  // the aux stream's Morton sort still reads the source's grid
     HIPCK(hipStreamWaitEvent(ctx->stream, ctx->aux_ev[2], 0));
-  if (&cl == &ctx->src && ctx->src_spec == 1) {  // a speculative grid is no "previous grid" of the new source
-    cl.view.h = 0.f;
-    cl.n_built = 0;
-    ctx->src_spec = 0;
-  }
   const double t0 = now_ms();
   MGICP_TRACE_AT("upload: begin");
   HIPCK(cl.orig.reserve(n));
@@ -1026,8 +956,8 @@ int upload_cloud(mgicp_ctx* ctx, Cloud& cl, const float* xyz, size_t n, size_t s
 }
 
 // r05 target cache.  A single-rank context leaves its target at destroy when the grid is the one a fresh
-// context would build for those points (fresh_grid: sized from the 3-D guess, so the source grid, which
-// starts from the target's cell size, and every sum come out the same -- DESIGN.md "Target cache").
+// context would build for those points (fresh_grid; since r06 every grid is sized from its own cloud
+// alone -- DESIGN.md "Target cache").
 void tcache_donate(mgicp_ctx* ctx, bool cov_complete) {
   Cloud& t = ctx->tgt;
   if (!ctx->tcache_on || ctx->nranks != 1 || ctx->comm || ctx->have_shm || t.dirty || t.n == 0 || t.n_built != t.n ||
@@ -1212,24 +1142,11 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
     return nc;
   };
   double h = maxext > 0.f ? static_cast<double>(maxext) / std::cbrt(static_cast<double>(n)) : 1.0;
-  // r06: the start of the sizing loop is a function of the clouds only.  The target
-  // (and any cloud but the source) always starts from the 3-D guess above -- never from this slot's
-  // previous grid: the loop accepts any size in a 0.6-1.6x occupancy band, so a different start gives a
-  // different accepted grid.  The source starts from the CURRENT target's cell size, scaled as a surface
-  // (sqrt n): its sorted order, so the fixed reduction tree of every objective pass, follows the target's
-  // (measured r05, a source grid sized on its own flips one BFGS line-search decision at C4F: 4 iterations
-  // against the oracle's 3, frob 7.7e-3).  src_basis_check rebuilds a source grid whose basis is stale.
-  float basis_h = 0.f;
-  size_t basis_n = 0;
-  if (&cl == &ctx->src && !ctx->tgt.dirty && ctx->tgt.view.h > 0.f && ctx->tgt.n_built > 0) {
-    basis_h = ctx->tgt.view.h;
-    basis_n = ctx->tgt.n_built;
-  } else if (&cl == &ctx->src && ctx->src_spec == 1) {  // the cached target's (spec_check confirms it)
-    basis_h = ctx->spec_h;
-    basis_n = ctx->spec_n;
-  }
-  if (basis_h > 0.f) h = static_cast<double>(basis_h) * std::sqrt(static_cast<double>(basis_n) / n);
-  const bool fresh = &cl != &ctx->src || basis_h == 0.f;
+  // r06: the cell size is a function of this cloud alone: the loop below always
+  // starts from the 3-D guess above -- never from this slot's previous grid or from the other cloud's
+  // (the loop accepts any size in a 0.6-1.6x occupancy band, so a different start would give a different
+  // grid for the same points; the source's grid sets the order of every objective sum)
+  const bool fresh = true;
   h = std::max(h, 1e-6);
   int nd[3];
   double h_prev = 0, occ_prev = 0;
@@ -1356,8 +1273,6 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
   cl.ncells = nc;
   cl.n_built = n;
   cl.fresh_grid = fresh;
-  cl.basis_h = basis_h;
-  cl.basis_n = basis_n;
   cl.dirty = false;
   cl.have_cov = false;
   if (&cl == &ctx->tgt) ctx->vl_valid = false;  // the 1-NN cell lists index the old target
@@ -1502,7 +1417,6 @@ int prepare(mgicp_ctx* ctx, bool need_cov) {
                 "a cloud has fewer points than k_correspondences (PCL computeCovariances)");
   int rc;
   if (ctx->tgt.dirty && (rc = build_grid(ctx, ctx->tgt))) return rc;
-  if ((rc = spec_check(ctx))) return rc;
   if (ctx->src.dirty && (rc = build_grid(ctx, ctx->src))) return rc;
   if (!need_cov) return MGICP_OK;
   // set_target's covariances still running count as current: the first sweep runs beside them and
@@ -3436,6 +3350,21 @@ int mgicp_debug_vlist_stats(mgicp_ctx* ctx, long long out[8]) {
   return MGICP_OK;
 }
 
+// r06: the objective's stream order -- original indices of this rank's source points in the order the
+// compacted streams (and so every sum's fixed tree) visit them; the oracle's summation-order ledger runs
+// the engine's tree over it (oracle/gicp_ref.c ref_set_sum_order).  Returns the count (<= cap written).
+int mgicp_debug_source_order(mgicp_ctx* ctx, uint32_t* out, size_t cap) {
+  if (!ctx || !out) return MGICP_E_INVALID;
+  HIPCK(hipSetDevice(ctx->device));
+  int rc = prepare(ctx, false);
+  if (rc) return rc;
+  const size_t p0 = ctx->shard_p0(), ns = ctx->shard_p1() - p0;
+  if (cap < ns) return fail(ctx, MGICP_E_INVALID, "debug_source_order: cap below the shard's point count");
+  HIPCK(hipMemcpyAsync(out, ctx->src.perm.p + p0, ns * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+  if ((rc = sync(ctx))) return rc;
+  return static_cast<int>(ns);
+}
+
 int mgicp_debug_covariances(mgicp_ctx* ctx, int which, double* out_c6) {
   if (!ctx || !out_c6 || (which != 0 && which != 1)) return MGICP_E_INVALID;
   HIPCK(hipSetDevice(ctx->device));
@@ -3750,7 +3679,7 @@ int mgicp_set_profiling(mgicp_ctx* ctx, int on) {
 
 // r05 target cache: [0] the current target was adopted from the cache, [1] adoptions and [2] donations
 // on this device so far (process-wide), [3] an entry is cached on this device, [4] the source grid's start
-// from the cached target's cell size (0 none, 1 pending, 2 kept, 3 discarded and rebuilt)
+// from the cached target's cell size (r05; since r06 always 0: the source's grid never depends on the target)
 int mgicp_debug_cache_stats(mgicp_ctx* ctx, long long out[5]) {
   if (!ctx || !out) return MGICP_E_INVALID;
   TargetCache& c = g_tcache[ctx->device & 63];
@@ -3759,7 +3688,7 @@ int mgicp_debug_cache_stats(mgicp_ctx* ctx, long long out[5]) {
   out[1] = c.hits;
   out[2] = c.donations;
   out[3] = c.valid ? 1 : 0;
-  out[4] = ctx->src_spec;
+  out[4] = 0;  // r06: no speculative source grid any more (the source's grid never depends on the target)
   return MGICP_OK;
 }
 

@@ -342,6 +342,12 @@ class GICPEngine:
         return {k: int(out[i]) for i, k in enumerate(self.VLIST_STATS)}
 
     # -- introspection (parity tests, profiling) ----------------------------------------------
+    def debug_source_order(self, n: int) -> np.ndarray:
+        """Original indices of the source points in the objective's stream order (mgicp_debug_source_order)."""
+        out = np.zeros(n, np.uint32)
+        m = self._check(self._lib.mgicp_debug_source_order(self._h, out.ctypes.data, n), "debug_source_order")
+        return out[:m]
+
     def debug_covariances(self, which: str, n: int) -> np.ndarray:
         out = np.zeros((n, 6), np.float64)
         self._check(self._lib.mgicp_debug_covariances(self._h, 0 if which == "source" else 1, _dp(out)),

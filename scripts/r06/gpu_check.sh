@@ -8,6 +8,6 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 cat $O/smoke.log
 timeout -k 10 400 python3 -u bench.py > $O/bench_C4.json 2> $O/bench_C4.err || { tail -30 $O/bench_C4.err; exit 1; }
 python3 scripts/r05/show_bench.py $O/bench_C4.json
-timeout -k 10 400 python3 -u bench.py --config C4F --gn-steps 0 --cold-pairs 1 --c5-leg 0 > $O/bench_C4F.json 2> $O/bench_C4F.err || { tail -30 $O/bench_C4F.err; exit 1; }
+timeout -k 10 120 python3 scripts/r06/dump_order.py C4F $O/order_C4F.npy && timeout -k 10 400 python3 -u bench.py --config C4F --gn-steps 0 --cold-pairs 1 --c5-leg 0 > $O/bench_C4F.json 2> $O/bench_C4F.err || { tail -30 $O/bench_C4F.err; exit 1; }
 python3 scripts/r05/show_bench.py $O/bench_C4F.json
 echo done

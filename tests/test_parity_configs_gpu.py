@@ -244,3 +244,48 @@ def test_state_machine_identical_clouds_known_answer():
         T_ref, info = o.align()
         assert info["converged"] == 1 and info["iterations"] == 1
         assert np.array_equal(T_ref, np.eye(4, dtype=np.float32))
+
+
+@pytest.mark.parametrize("name", ["C2", "C2F"])
+def test_oracle_on_the_engine_tree_is_bitwise_the_engine(name):
+    """r06 summation-order ledger, pinned: the oracle restates the engine's fixed reduction tree
+    (gicp_ref.c fdf_tree) and runs it over the engine's own stream order (mgicp_debug_source_order).
+    Then an objective evaluation (f and PCL's gradient) at several states and the whole align -- T,
+    iterations, evaluations and every per-iteration transform -- equal the engine's BIT FOR BIT: the only
+    difference between engine and oracle left in DESIGN.md "Numerics" (the summation order) is closed, and
+    the oracle's default sequential order gives the same T here as well."""
+    from leica_point_cloud_processing_amd.engine import GICPEngine
+    from oracle import ref
+
+    c = CONFIGS[name]
+    scan, cad, T_true, T_seq, info_seq = _clouds_and_oracle(name)
+    e = GICPEngine(max_iter=c["max_iter"])
+    e.set_source_xyz(scan)
+    e.set_target_xyz(cad)
+    order = e.debug_source_order(len(scan))
+    assert len(order) == len(scan) and np.array_equal(np.sort(order), np.arange(len(scan)))
+    o = ref.RefGICP(max_iterations=c["max_iter"], threads=ORACLE_THREADS)
+    o.set_source(scan)
+    o.set_target(cad)
+    o.set_sum_order(1, order)
+    T0 = np.linalg.inv(T_true).astype(np.float32)
+    o.correspondences(T0)
+    e.debug_correspondences(T0, len(scan))
+    rng = np.random.default_rng(3)
+    for _ in range(4):
+        x = rng.normal(0, [0.01, 0.01, 0.01, 0.005, 0.005, 0.005])
+        f_o, g_o = o.fdf(x)
+        f_e, g_e = e.debug_fdf(x)
+        assert f_e == f_o, (f_e, f_o)
+        np.testing.assert_array_equal(g_e, g_o)
+    T_o, info = o.align(want_trace=True)
+    T_e = e.align()
+    tr = e.debug_trace(c["max_iter"] + 1)
+    e.close()
+    print(f"{name}: engine tree in the oracle -- iterations {info['iterations']}, frob vs engine "
+          f"{frob(T_o, T_e):.3e}, vs the sequential oracle {frob(T_o, T_seq):.3e}")
+    np.testing.assert_array_equal(T_o, T_e)
+    assert info["iterations"] == info_seq["iterations"]
+    assert len(tr) == len(info["trace"])
+    for a, b in zip(tr, info["trace"]):
+        np.testing.assert_array_equal(np.asarray(a, np.float32), np.asarray(b, np.float32))
