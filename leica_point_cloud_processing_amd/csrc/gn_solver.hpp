@@ -161,8 +161,10 @@ inline void so3_exp(const double w[3], double Rx[3][3]) {
     a = 1.0 - th2 / 6.0;
     b = 0.5 - th2 / 24.0;
   } else {
-    a = std::sin(th) / th;
-    b = (1.0 - std::cos(th)) / th2;
+    double sth, cth;
+    ::sincos(th, &sth, &cth);  // glibc sincos, as the gcc-built oracle restatement calls it (r06)
+    a = sth / th;
+    b = (1.0 - cth) / th2;
   }
   const double W[3][3] = {{0, -w[2], w[1]}, {w[2], 0, -w[0]}, {-w[1], w[0], 0}};
   for (int i = 0; i < 3; ++i)

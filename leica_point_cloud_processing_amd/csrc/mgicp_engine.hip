@@ -104,10 +104,16 @@ struct Mat4 {  // row-major float 4x4
 // GICP::applyState(t = I, x): R = AngleAxisf(x5,Z) * AngleAxisf(x4,Y) * AngleAxisf(x3,X)
 // evaluated through Eigen's quaternion products, then t.col(3) += (x0, x1, x2, 0).
 struct Quat { float w, x, y, z; };
+// r06: glibc's sincosf / sincos, not sinf + cosf / sin + cos.  PCL is built by gcc, whose sincos pass
+// turns Eigen's cos(ha) / sin(ha) (and computeRDerivative's cos / sin of each angle) into ONE sincos call;
+// glibc's sincos differs from separate sin / cos calls by an ulp on rare arguments (7 in 1e5 random
+// gradients differed, tests/test_parity_configs_gpu.py::test_oracle_on_the_engine_tree_is_bitwise_the_engine
+// caught one), and clang never forms it -- so the engine names it.
 Quat quat_axis(float angle, int axis) {
   const float ha = 0.5f * angle;
-  const float s = std::sin(ha);
-  Quat q{std::cos(ha), 0.f, 0.f, 0.f};
+  float s, c;
+  ::sincosf(ha, &s, &c);
+  Quat q{c, 0.f, 0.f, 0.f};
   if (axis == 0) q.x = s;
   if (axis == 1) q.y = s;
   if (axis == 2) q.z = s;
@@ -148,9 +154,10 @@ Mat4 apply_state(const Vec6& x) {
 // GICP::computeRDerivative + matricesInnerProd (tr(dR * Rsum))
 void r_derivative(const Vec6& x, const double R[3][3], Vec6& g) {
   const double phi = x[3], theta = x[4], psi = x[5];
-  const double cphi = std::cos(phi), sphi = std::sin(phi);
-  const double ctheta = std::cos(theta), stheta = std::sin(theta);
-  const double cpsi = std::cos(psi), spsi = std::sin(psi);
+  double cphi, sphi, ctheta, stheta, cpsi, spsi;  // glibc's sincos, as gcc-built PCL calls it (quat_axis)
+  ::sincos(phi, &sphi, &cphi);
+  ::sincos(theta, &stheta, &ctheta);
+  ::sincos(psi, &spsi, &cpsi);
   double d[3][3][3];
   // d/dphi
   d[0][0][0] = 0.; d[0][1][0] = 0.; d[0][2][0] = 0.;

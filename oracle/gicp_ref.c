@@ -26,6 +26,7 @@
  *     C = u1u1' + u2u2' + eps*u3u3' up to fp64 rounding).
  */
 #define _POSIX_C_SOURCE 200809L
+#define _GNU_SOURCE 1 /* sincos / sincosf (glibc) */
 #include "gicp_ref.h"
 
 #include <float.h>
@@ -481,8 +482,11 @@ typedef struct { float w, x, y, z; } quatf;
 static quatf quat_axis(float angle, int axis) {
     quatf q;
     float ha = 0.5f * angle;
-    float s = sinf(ha);
-    q.w = cosf(ha);
+    /* glibc sincosf: gcc-built PCL / Eigen get cos(ha), sin(ha) from one sincosf call (gcc's sincos pass);
+     * named explicitly so the oracle does not depend on its own compiler forming it */
+    float s, cw;
+    sincosf(ha, &s, &cw);
+    q.w = cw;
     q.x = axis == 0 ? s : 0.f;
     q.y = axis == 1 ? s : 0.f;
     q.z = axis == 2 ? s : 0.f;
@@ -539,9 +543,10 @@ static double inner_prod(const double a[3][3], const double b[3][3]) {
 
 static void r_derivative(const double x[6], const double R[3][3], double g[6]) {
     double phi = x[3], theta = x[4], psi = x[5];
-    double cphi = cos(phi), sphi = sin(phi);
-    double ctheta = cos(theta), stheta = sin(theta);
-    double cpsi = cos(psi), spsi = sin(psi);
+    double cphi, sphi, ctheta, stheta, cpsi, spsi; /* glibc sincos, as gcc-built PCL calls it */
+    sincos(phi, &sphi, &cphi);
+    sincos(theta, &stheta, &ctheta);
+    sincos(psi, &spsi, &cpsi);
     double dphi[3][3], dtheta[3][3], dpsi[3][3];
     dphi[0][0] = 0.; dphi[1][0] = 0.; dphi[2][0] = 0.;
     dphi[0][1] = sphi * spsi + cphi * cpsi * stheta;
@@ -834,8 +839,10 @@ static void gn_exp(const double w[3], double Rx[3][3]) {
         a = 1.0 - th2 / 6.0;
         b = 0.5 - th2 / 24.0;
     } else {
-        a = sin(th) / th;
-        b = (1.0 - cos(th)) / th2;
+        double sth, cth;
+        sincos(th, &sth, &cth);
+        a = sth / th;
+        b = (1.0 - cth) / th2;
     }
     double W[3][3] = {{0, -w[2], w[1]}, {w[2], 0, -w[0]}, {-w[1], w[0], 0}};
     for (int i = 0; i < 3; ++i)
