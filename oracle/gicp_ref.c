@@ -968,6 +968,10 @@ int ref_set_sum_order(ref_gicp* g, int mode, const uint32_t* perm, size_t n) {
     return REF_OK;
 }
 
+/* the raw 13 sums of one pass in the current summation mode (ledger checks against the engine's
+ * mgicp_debug_fdf_sums): f, grad_t[3], Rsum[3][3] row-major, then the count */
+int ref_fdf_mode_sums(ref_gicp* g, const double x[6], double out14[14]);
+
 static void functor_eval(ref_gicp* g, const double x[6], double* f, double grad[6]) {
     if (g->prm.objective == 1) {
         moments_eval(g, x, f, grad);
@@ -1025,6 +1029,29 @@ static void functor_eval(ref_gicp* g, const double x[6], double* f, double grad[
             for (int b = 0; b < 3; ++b) tot.R[a][b] *= s;
         r_derivative(x, tot.R, grad);
     }
+}
+
+int ref_fdf_mode_sums(ref_gicp* g, const double x[6], double out14[14]) {
+    if (!g || !out14 || g->m <= 0) return REF_E_INVALID;
+    float A[4][4];
+    apply_state(x, A);
+    fdf_acc tot;
+    if (g->sum_mode == 1 || g->sum_mode == 3) {
+        for (int i = 0; i < g->ns; ++i) g->sum_tj[i] = -1;
+        for (int c = 0; c < g->m; ++c) g->sum_tj[g->corr_src[c]] = c;
+    }
+    if (g->sum_mode == 1) {
+        fdf_tree(g, A, &tot);
+    } else {
+        fdf_range(g, A, 0, g->m, &tot);
+    }
+    out14[0] = tot.f;
+    for (int a = 0; a < 3; ++a) {
+        out14[1 + a] = tot.gt[a];
+        for (int b = 0; b < 3; ++b) out14[4 + 3 * a + b] = tot.R[a][b];
+    }
+    out14[13] = (double)g->m;
+    return REF_OK;
 }
 
 int ref_fdf_sums(ref_gicp* g, const double x[6], int c0, int c1, double out14[14]) {

@@ -109,6 +109,8 @@ int ref_fdf_sums(ref_gicp* g, const double x[6], int c0, int c1, double out14[14
  * correspondence order, or the OpenMP parts), 1 (the engine's fixed chunk -> super -> total tree over
  * the stream order perm[0..n), n = source points), 2 (reversed sequential) or 3 (sequential over perm) */
 int ref_set_sum_order(ref_gicp* g, int mode, const uint32_t* perm, size_t n);
+/* the raw sums of one pass at x in the current mode (0: sequential, 1: the engine tree) */
+int ref_fdf_mode_sums(ref_gicp* g, const double x[6], double out14[14]);
 /* applyState(I, x): column-major float 4x4. */
 void ref_apply_state(const double x[6], float out_cm[16]);
 

@@ -78,6 +78,7 @@ def load():
         "ref_moments_range": (ctypes.c_int, [P, FP, ctypes.c_int, ctypes.c_int, DP]),
         "ref_fdf_sums": (ctypes.c_int, [P, DP, ctypes.c_int, ctypes.c_int, DP]),
         "ref_set_sum_order": (ctypes.c_int, [P, ctypes.c_int, P, sz]),
+        "ref_fdf_mode_sums": (ctypes.c_int, [P, DP, DP]),
         "ref_apply_state": (None, [DP, FP]),
         "ref_segment_differences": (ctypes.c_int, [P, sz, sz, P, sz, sz, ctypes.c_double, P, ctypes.POINTER(sz)]),
         "ref_voxel_grid": (ctypes.c_int, [P, sz, sz, ctypes.c_int, FP, ctypes.c_int, FP, P, ctypes.POINTER(sz),
@@ -191,6 +192,13 @@ class RefGICP:
                                         0 if buf is None else len(buf))
         assert rc == 0, rc
         self._sum_perm = buf
+
+    def fdf_mode_sums(self, x):
+        """raw 14 sums of one pass at x in the current summation mode (set_sum_order)"""
+        x = np.asarray(x, np.float64)
+        out = np.zeros(14, np.float64)
+        assert self.lib.ref_fdf_mode_sums(self.h, _dp(x), _dp(out)) == 0
+        return out
 
     def fdf_sums(self, x, c0, c1):
         x = np.asarray(x, np.float64)

@@ -274,6 +274,8 @@ def test_oracle_on_the_engine_tree_is_bitwise_the_engine(name):
     rng = np.random.default_rng(3)
     for _ in range(4):
         x = rng.normal(0, [0.01, 0.01, 0.01, 0.005, 0.005, 0.005])
+        s_o, s_e = o.fdf_mode_sums(x), e.debug_fdf_sums(x)
+        np.testing.assert_array_equal(s_e[:14], s_o, err_msg="raw sums (f, grad_t, Rsum, count)")
         f_o, g_o = o.fdf(x)
         f_e, g_e = e.debug_fdf(x)
         assert f_e == f_o, (f_e, f_o)
