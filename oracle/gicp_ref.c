@@ -362,6 +362,7 @@ struct ref_gicp {
     /* summation-order ledger (r06, ref_set_sum_order): 0 the order above, 1 the engine's fixed tree over
      * sum_perm, 2 reversed sequential, 3 sequential over sum_perm */
     int sum_mode;
+    int mahal_upper;    /* 1: the Mahalanobis matrix's upper triangle mirrored (the engine's 6-entry storage) */
     uint32_t* sum_perm; /* ns entries: stream position -> source index */
     int* sum_tj;        /* per source index: its correspondence slot, -1 = rejected (scratch) */
 };
@@ -949,6 +950,12 @@ static void fdf_tree(ref_gicp* g, const float A[4][4], fdf_acc* tot) {
     free(chunk);
 }
 
+int ref_set_mahalanobis_upper(ref_gicp* g, int on) {
+    if (!g) return REF_E_INVALID;
+    g->mahal_upper = on != 0;
+    return REF_OK;
+}
+
 int ref_set_sum_order(ref_gicp* g, int mode, const uint32_t* perm, size_t n) {
     if (!g || mode < 0 || mode > 3) return REF_E_INVALID;
     free_sum_order(g);
@@ -1488,7 +1495,9 @@ static int correspondence_sweep(ref_gicp* g, const float T[4][4], const float G[
         if (nn_tgt) nn_tgt[i] = ((double)d2 < thr) ? j : -1;
         if (nn_d2) nn_d2[i] = d2;
         if ((double)d2 < thr) {
-            mahalanobis(R, g->cov_src + 6 * (size_t)i, g->cov_tgt + 6 * (size_t)j, g->mahal + 9 * (size_t)i);
+            double* M9 = g->mahal + 9 * (size_t)i;
+            mahalanobis(R, g->cov_src + 6 * (size_t)i, g->cov_tgt + 6 * (size_t)j, M9);
+            if (g->mahal_upper) { M9[3] = M9[1]; M9[6] = M9[2]; M9[7] = M9[5]; }
             tj[i] = j;
         } else {
             tj[i] = -1;

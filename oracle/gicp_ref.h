@@ -111,6 +111,10 @@ int ref_fdf_sums(ref_gicp* g, const double x[6], int c0, int c1, double out14[14
 int ref_set_sum_order(ref_gicp* g, int mode, const uint32_t* perm, size_t n);
 /* the raw sums of one pass at x in the current mode (0: sequential, 1: the engine tree) */
 int ref_fdf_mode_sums(ref_gicp* g, const double x[6], double out14[14]);
+/* r06: 1 = use the Mahalanobis matrix's upper triangle mirrored, as the engine stores it (6 fp64 per
+ * correspondence); 0 (default) = PCL's full Eigen inverse of (R C1 R' + C2), whose off-diagonal pairs
+ * differ by an ulp when R != I (R C1 R' is not exactly symmetric in fp64).  Applies from the next sweep. */
+int ref_set_mahalanobis_upper(ref_gicp* g, int on);
 /* applyState(I, x): column-major float 4x4. */
 void ref_apply_state(const double x[6], float out_cm[16]);
 

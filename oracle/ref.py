@@ -79,6 +79,7 @@ def load():
         "ref_fdf_sums": (ctypes.c_int, [P, DP, ctypes.c_int, ctypes.c_int, DP]),
         "ref_set_sum_order": (ctypes.c_int, [P, ctypes.c_int, P, sz]),
         "ref_fdf_mode_sums": (ctypes.c_int, [P, DP, DP]),
+        "ref_set_mahalanobis_upper": (ctypes.c_int, [P, ctypes.c_int]),
         "ref_apply_state": (None, [DP, FP]),
         "ref_segment_differences": (ctypes.c_int, [P, sz, sz, P, sz, sz, ctypes.c_double, P, ctypes.POINTER(sz)]),
         "ref_voxel_grid": (ctypes.c_int, [P, sz, sz, ctypes.c_int, FP, ctypes.c_int, FP, P, ctypes.POINTER(sz),
@@ -192,6 +193,10 @@ class RefGICP:
                                         0 if buf is None else len(buf))
         assert rc == 0, rc
         self._sum_perm = buf
+
+    def set_mahalanobis_upper(self, on: bool):
+        """gicp_ref.h ref_set_mahalanobis_upper: mirror M's upper triangle (the engine's storage)"""
+        assert self.lib.ref_set_mahalanobis_upper(self.h, int(bool(on))) == 0
 
     def fdf_mode_sums(self, x):
         """raw 14 sums of one pass at x in the current summation mode (set_sum_order)"""

@@ -6,8 +6,10 @@ Orders: seq (input order, 1 thread: PCL's own order), omp<N> (N OpenMP parts, wh
 tests' oracle runs), rev (reversed sequential), tree:<order> (the engine's fixed chunk -> super ->
 total tree, gicp_ref.c fdf_tree, over a stream order), seq:<order> (sequential over that order);
 stream orders: input (source input order), morton (30-bit Morton codes over the source's own bbox,
-stable in the input index -- the canonical order proposed for the engine), engine (a stream order saved
-by the engine, --engine-order file.npy: position -> original index).
+stable in the input index), engine (the stream order the engine's grid gives, saved on the GPU box by
+scripts/r06/dump_order.py, --engine-order file.npy: position -> original index).  A "+upper" suffix runs
+the order with the Mahalanobis matrix's upper triangle mirrored (the engine's 6-entry storage) instead of
+PCL's full Eigen inverse.
 usage: python3 scripts/r06/order_ledger.py C4F [--orders seq,rev,tree:morton,...] [--out file.json]"""
 import argparse
 import json
@@ -70,6 +72,12 @@ def main():
     rows = []
     base = None
     for name in a.orders.split(","):
+        # "+upper": the Mahalanobis matrix's upper triangle mirrored (the engine's 6-entry storage)
+        upper = name.endswith("+upper")
+        o.set_mahalanobis_upper(upper)
+        base_name = name[: -len("+upper")] if upper else name
+        name_full = name
+        name = base_name
         if name.startswith("omp"):
             o.set_params(threads=int(name[3:]))
             o.set_sum_order(0)
@@ -89,7 +97,7 @@ def main():
         T = T.astype(np.float64)
         if base is None:
             base = T
-        row = {"order": name, "iterations": int(info["iterations"]), "n_evals": int(info["n_evals"]),
+        row = {"order": name_full, "iterations": int(info["iterations"]), "n_evals": int(info["n_evals"]),
                "n_corr_last": int(info["n_corr_last"]), "frob_vs_first": float(np.linalg.norm(T - base)),
                "err_vs_truth": float(np.abs(T @ T_true - np.eye(4)).max()), "s": round(dt, 1)}
         rows.append(row)

@@ -249,11 +249,12 @@ def test_state_machine_identical_clouds_known_answer():
 @pytest.mark.parametrize("name", ["C2", "C2F"])
 def test_oracle_on_the_engine_tree_is_bitwise_the_engine(name):
     """r06 summation-order ledger, pinned: the oracle restates the engine's fixed reduction tree
-    (gicp_ref.c fdf_tree) and runs it over the engine's own stream order (mgicp_debug_source_order).
-    Then an objective evaluation (f and PCL's gradient) at several states and the whole align -- T,
-    iterations, evaluations and every per-iteration transform -- equal the engine's BIT FOR BIT: the only
-    difference between engine and oracle left in DESIGN.md "Numerics" (the summation order) is closed, and
-    the oracle's default sequential order gives the same T here as well."""
+    (gicp_ref.c fdf_tree) over the engine's own stream order (mgicp_debug_source_order), with the
+    Mahalanobis matrix's upper triangle mirrored as the engine stores it (ref_set_mahalanobis_upper).
+    Then the raw pass sums, f and PCL's gradient at several states, and the whole align -- T, iterations
+    and every per-iteration transform -- equal the engine's BIT FOR BIT.  Those are the only two
+    differences between engine and oracle (DESIGN.md "Numerics"); the default oracle (sequential or
+    OpenMP sums, PCL's full M) gives the same T at every config (test_config_final_transform_vs_oracle)."""
     from leica_point_cloud_processing_amd.engine import GICPEngine
     from oracle import ref
 
@@ -268,6 +269,7 @@ def test_oracle_on_the_engine_tree_is_bitwise_the_engine(name):
     o.set_source(scan)
     o.set_target(cad)
     o.set_sum_order(1, order)
+    o.set_mahalanobis_upper(True)  # the engine's 6-entry M (PCL's full inverse differs by an ulp off-diagonal)
     T0 = np.linalg.inv(T_true).astype(np.float32)
     o.correspondences(T0)
     e.debug_correspondences(T0, len(scan))
