@@ -548,7 +548,8 @@ struct mgicp_ctx {
   // one stream for both clouds' launches: with a stream each the process exceeds its hardware queues
   // (GPU_MAX_HW_QUEUES, 4) and the main stream ends up sharing one with them (profiles/r04/prep7)
   hipStream_t aux_stream = nullptr;
-  hipEvent_t aux_ev[3] = {nullptr, nullptr, nullptr};  // completion of the target's [0] / source's [1] launch,
+  hipEvent_t aux_ev[4] = {nullptr, nullptr, nullptr, nullptr};  // [3]: main stream -> aux (a grid built) (r06)
+  // completion of the target's [0] / source's [1] launch,
                                                        // [2] the source's Morton order sorted on the aux stream
   bool qperm_aux = false;                    // qperm is being sorted on the aux stream (aux_ev[2])
   DevBuf<uint32_t> aq_keys, aq_keys_sorted, aq_vals;  // its sort buffers (the main stream's may be busy)
@@ -805,7 +806,8 @@ int reset_stamps(mgicp_ctx* ctx) {
 }
 
 // Upload strided host records (or copy device records) and pack to float4 (original order).
-int build_grid(mgicp_ctx* ctx, Cloud& cl);
+int build_grid(mgicp_ctx* ctx, Cloud& cl, bool defer_extras = false);
+int build_grid_extras(mgicp_ctx* ctx, Cloud& cl);
 const uint32_t* query_perm(mgicp_ctx* ctx);
 bool morton_perm(mgicp_ctx* ctx, const Cloud& c, size_t p0, size_t n, DevBuf<uint32_t>& out, bool aux);
 
@@ -848,7 +850,9 @@ int cov_prep_async(mgicp_ctx* ctx, bool tgt) {
   if (!ctx->async_tgt || !ctx->aux_stream || ctx->nranks != 1 || ctx->comm || ctx->have_shm || ctx->profiling ||
       static_cast<size_t>(ctx->prm.k) > c.n)
     return MGICP_OK;
-  if (build_grid(ctx, c) != MGICP_OK || c.n < static_cast<size_t>(ctx->prm.k)) return MGICP_OK;
+  // r06: the grid's core (sorted points, cell starts) only; the 1-NN extras are queued after the k-NN
+  if (build_grid(ctx, c, true) != MGICP_OK) return MGICP_OK;
+  if (c.n < static_cast<size_t>(ctx->prm.k)) return build_grid_extras(ctx, c);
   HIPCK(c.cov.reserve(3 * c.n));
   c.cov_stride = c.n;
   // the source in the lazy mode: a ring-capped launch (a point whose 20 neighbours lie beyond the
@@ -872,7 +876,10 @@ int cov_prep_async(mgicp_ctx* ctx, bool tgt) {
     HIPCK(ctx->aux_cnt.reserve(2));
     HIPCK(hipMemsetAsync(ctx->aux_cnt.p + (tgt ? 0 : 1), 0, sizeof(unsigned int), ctx->stream));
   }
-  HIPCK(hipStreamSynchronize(ctx->stream));  // the grid (and the count) before the aux stream reads them
+  // the grid (and the count) before the aux stream reads them: a device-side dependency (r06; r04-r05
+  // waited on the host)
+  HIPCK(hipEventRecord(ctx->aux_ev[3], ctx->stream));
+  HIPCK(hipStreamWaitEvent(ctx->aux_stream, ctx->aux_ev[3], 0));
   // the source's Morton query order is sorted on the aux stream ahead of its k-NN, so the main stream stays
   // empty for set_target's upload (r05: queued behind a main-stream sort that shares the CUs with the k-NN,
   // the target's copies waited ~2 ms)
@@ -892,6 +899,7 @@ int cov_prep_async(mgicp_ctx* ctx, bool tgt) {
   HIPCK(hipEventRecord(ctx->aux_ev[tgt ? 0 : 1], ctx->aux_stream));
   MGICP_TRACE_AT(tgt ? "head start: target k-NN queued" : "head start: source k-NN queued");
   (tgt ? ctx->tgt_cov_pending : ctx->src_cov_pending) = true;
+  if (int rc = build_grid_extras(ctx, c)) return rc;  // the target's empty / seed map, boxes, pairs
   // r05: the source's 1-NN query order (a Morton sort of the shard) now, on the main stream beside the
   // covariances -- not inside the first align's loop
   if (!tgt && !ctx->qperm_aux) (void)query_perm(ctx);
@@ -1083,7 +1091,7 @@ int tcache_adopt(mgicp_ctx* ctx) {
 }
 
 // Build the row-sorted uniform grid of a cloud (one-time per set_*).
-int build_grid(mgicp_ctx* ctx, Cloud& cl) {
+int build_grid(mgicp_ctx* ctx, Cloud& cl, bool defer_extras) {
   const size_t n = cl.n;
   hipStream_t s = ctx->stream;
   // 1. bounding box + finiteness
@@ -1123,7 +1131,7 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
       cl.dirty = false;
       return MGICP_OK;  // empty cloud: callers check cl.n
     }
-    return build_grid(ctx, cl);
+    return build_grid(ctx, cl, defer_extras);
   }
   if (bad > 0) return fail(ctx, MGICP_E_NONFINITE, "cloud contains NaN/Inf coordinates");
   for (int d = 0; d < 3; ++d) {
@@ -1230,9 +1238,11 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
                           cl.perm.p, n, bits, s));
   HIPCK(launch_gather_sorted(cl.orig.p, cl.perm.p, n, cl.pts.p, s));
   MGICP_TRACE_AT("grid: sort queued");
-  rc = sync(ctx);
-  if (rc) return rc;
-  MGICP_TRACE_AT("grid: sorted");
+  if (!defer_extras) {
+    rc = sync(ctx);
+    if (rc) return rc;
+    MGICP_TRACE_AT("grid: sorted");
+  }
   // the build scratch stays allocated for the next build (hipFree + hipMalloc of these
   // tens-of-MB buffers cost milliseconds of host time between the two clouds' builds)
   GridView& g = cl.view;
@@ -1250,33 +1260,8 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
   g.pts = cl.pts.p;
   g.empty_dist = nullptr;
   g.seed = nullptr;
-  if (cl.want_empty_map) {
-    HIPCK(cl.empty_dist.reserve(nc));
-    HIPCK(ctx->scratch.reserve(nc));
-    if (cl.want_seed_map) {
-      HIPCK(cl.seed.reserve(nc));
-      HIPCK(cl.seed_scratch.reserve(nc));
-    }
-    HIPCK(launch_empty_map(cl.cell_start.p, nd[0], nd[1], nd[2], cl.empty_dist.p, ctx->scratch.p, s,
-                           cl.want_seed_map ? cl.seed.p : nullptr, cl.want_seed_map ? cl.seed_scratch.p : nullptr,
-                           &g));
-    if ((rc = sync(ctx))) return rc;
-    MGICP_TRACE_AT("grid: empty map done");
-    g.empty_dist = cl.empty_dist.p;
-    if (cl.want_seed_map) g.seed = cl.seed.p;
-  }
   g.boxes = nullptr;
-  if (cl.want_boxes && nc <= kMaxBoxCells) {
-    HIPCK(cl.boxes.reserve(2 * nc));
-    HIPCK(launch_cell_boxes(cl.pts.p, cl.cell_start.p, nc, cl.boxes.p, s));
-    g.boxes = cl.boxes.p;
-  }
   g.pairs = nullptr;
-  if (cl.want_pairs) {
-    HIPCK(cl.pairs.reserve(2 * pair_count(n)));
-    HIPCK(launch_pairs(cl.pts.p, n, cl.pairs.p, s));
-    g.pairs = cl.pairs.p;
-  }
   cl.ncells = nc;
   cl.n_built = n;
   cl.fresh_grid = fresh;
@@ -1287,6 +1272,41 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl) {
   if (&cl == &ctx->src || &cl == &ctx->tgt) {  // sorted positions changed
     ctx->have_corr = false;
     ctx->seed_valid = false;
+  }
+  return defer_extras ? MGICP_OK : build_grid_extras(ctx, cl);
+}
+
+// The 1-NN sweeps' extras of a built grid (target): empty-space + seed map, per-cell boxes, the
+// pair-interleaved copy -- queued on the main stream, no host wait.  r06: set_target's head start queues
+// the target's k-NN (which needs none of them) BEFORE these, so the 0.7-0.8 ms of the empty map at C4 run
+// beside the k-NN instead of in front of it (the target's k-NN is the cold first align's long pole).
+int build_grid_extras(mgicp_ctx* ctx, Cloud& cl) {
+  GridView& g = cl.view;
+  hipStream_t s = ctx->stream;
+  const size_t nc = cl.ncells, n = cl.n;
+  if (cl.want_empty_map) {
+    HIPCK(cl.empty_dist.reserve(nc));
+    HIPCK(ctx->scratch.reserve(nc));
+    if (cl.want_seed_map) {
+      HIPCK(cl.seed.reserve(nc));
+      HIPCK(cl.seed_scratch.reserve(nc));
+    }
+    HIPCK(launch_empty_map(cl.cell_start.p, g.nx, g.ny, g.nz, cl.empty_dist.p, ctx->scratch.p, s,
+                           cl.want_seed_map ? cl.seed.p : nullptr, cl.want_seed_map ? cl.seed_scratch.p : nullptr,
+                           &g));
+    MGICP_TRACE_AT("grid: empty map queued");
+    g.empty_dist = cl.empty_dist.p;
+    if (cl.want_seed_map) g.seed = cl.seed.p;
+  }
+  if (cl.want_boxes && nc <= kMaxBoxCells) {
+    HIPCK(cl.boxes.reserve(2 * nc));
+    HIPCK(launch_cell_boxes(cl.pts.p, cl.cell_start.p, nc, cl.boxes.p, s));
+    g.boxes = cl.boxes.p;
+  }
+  if (cl.want_pairs) {
+    HIPCK(cl.pairs.reserve(2 * pair_count(n)));
+    HIPCK(launch_pairs(cl.pts.p, n, cl.pairs.p, s));
+    g.pairs = cl.pairs.p;
   }
   return MGICP_OK;
 }
@@ -2576,7 +2596,8 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
   if (ctx->async_tgt && (se != hipSuccess ||
                          hipEventCreateWithFlags(&ctx->aux_ev[0], hipEventDisableTiming) != hipSuccess ||
                          hipEventCreateWithFlags(&ctx->aux_ev[1], hipEventDisableTiming) != hipSuccess ||
-                         hipEventCreateWithFlags(&ctx->aux_ev[2], hipEventDisableTiming) != hipSuccess)) {
+                         hipEventCreateWithFlags(&ctx->aux_ev[2], hipEventDisableTiming) != hipSuccess ||
+                         hipEventCreateWithFlags(&ctx->aux_ev[3], hipEventDisableTiming) != hipSuccess)) {
     if (ctx->aux_stream) (void)hipStreamDestroy(ctx->aux_stream);
     for (hipEvent_t& ev : ctx->aux_ev)
       if (ev) (void)hipEventDestroy(ev), ev = nullptr;
