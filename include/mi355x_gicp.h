@@ -282,7 +282,7 @@ int mgicp_debug_vlist_stats(mgicp_ctx* ctx, long long out[8]);
 int mgicp_set_profiling(mgicp_ctx* ctx, int on);
 /* test / diagnostic forms of the engine, set explicitly on one context (never through the
  * environment): "resident", "host_rows", "srv_cus", "fused_finish", "gated", "bar_cmd" (the
- * objective-pass path), "async_cov", "lazy_src_cov", "knn_logged" (covariances), "vlist",
+ * objective-pass path), "async_cov", "lazy_src_cov", "knn_logged", "knn_wave" (covariances), "vlist",
  * "vlist_cold", "vlist_eager", "vlist_stats", "fuse_compact" (1-NN cell lists),
  * "target_cache", "grid_occ" (grid
  * sizing of the next set_*).  Every form gives the default path's results bit for bit (the GPU tests

@@ -556,6 +556,7 @@ struct mgicp_ctx {
   DevBuf<unsigned char> aq_scratch;
   DevBuf<unsigned int> aux_cnt;     // their hand-off counts: [0] target, [1] source
   DevBuf<uint32_t> knn_fb2;         // the source's hand-off list
+  bool knn_wave = true;             // r06: lazy pass + hand-offs by the wave-per-query kernel (debug option "knn_wave")
   bool knn_logged = true;           // wave-staged k-NN kernel + hand-off (debug option "knn_logged" 0: register-list only)
   DevBuf<uint32_t> knn_fb;          // points the logged k-NN kernel leaves to the register-list one
   unsigned int knn_fallbacks = 0;   // their count in the last covariance launch
@@ -895,7 +896,7 @@ int cov_prep_async(mgicp_ctx* ctx, bool tgt) {
                        ctx->knn_logged ? (tgt ? ctx->knn_fb.p : ctx->knn_fb2.p) : nullptr,
                        ctx->knn_logged ? ctx->aux_cnt.p + (tgt ? 0 : 1) : nullptr, ctx->aux_stream,
                        capped ? ctx->async_ring_cap : -1, capped ? ctx->cov_ok.p : nullptr,
-                       ctx->knn_logged ? 2 * std::max(ctx->cus, 1) : 0));
+                       ctx->knn_logged ? 2 * std::max(ctx->cus, 1) : 0, ctx->knn_wave));
   HIPCK(hipEventRecord(ctx->aux_ev[tgt ? 0 : 1], ctx->aux_stream));
   MGICP_TRACE_AT(tgt ? "head start: target k-NN queued" : "head start: source k-NN queued");
   (tgt ? ctx->tgt_cov_pending : ctx->src_cov_pending) = true;
@@ -1380,8 +1381,11 @@ int compute_cov(mgicp_ctx* ctx, Cloud& cl, size_t p0, size_t p1, size_t stride =
     if (stats) std::fprintf(stderr, "[knn] %zu points, %u left to the register-list kernel\n", p1 - p0, nfb);
     if (nfb) {
       ProfScope ps(ctx, kFamCov);
-      HIPCK(launch_knn_cov(cl.view, ctx->prm.k, ctx->prm.gicp_eps, 0, nfb, cl.cov3(), ctx->knn_fb.p, nullptr,
-                           nullptr, ctx->stream));
+      if (ctx->knn_wave)
+        HIPCK(launch_knn_wave(cl.view, ctx->prm.k, ctx->prm.gicp_eps, ctx->knn_fb.p, nullptr, nfb, cl.cov3(), ctx->stream));
+      else
+        HIPCK(launch_knn_cov(cl.view, ctx->prm.k, ctx->prm.gicp_eps, 0, nfb, cl.cov3(), ctx->knn_fb.p, nullptr,
+                             nullptr, ctx->stream));
     }
   }
   int rc = sync(ctx);
@@ -1482,6 +1486,15 @@ int cov_lazy(mgicp_ctx* ctx) {
   unsigned int* cnt = reinterpret_cast<unsigned int*>(ctx->u64.p);  // [0] points to compute, [1] hand-offs
   HIPCK(hipMemsetAsync(cnt, 0, 2 * sizeof(unsigned int), ctx->stream));
   HIPCK(launch_cov_need(ctx->flags.p, ctx->cov_ok.p, p0, ns, ctx->cov_need.p, cnt, ctx->stream));
+  if (ctx->knn_wave && !knn_stats_on()) {
+    // r06: one wave per listed point, the count read on the device (no host round trip): the points a sweep
+    // accepts without a covariance are mostly the isolated ones the head start's ring cap left (C4F: debris
+    // and clutter near the part), whose long ring searches the per-lane kernel ran one lane each
+    ProfScope ps(ctx, kFamCov);
+    HIPCK(launch_knn_wave(ctx->src.view, ctx->prm.k, ctx->prm.gicp_eps, ctx->cov_need.p, cnt, ns, ctx->src.cov3(),
+                          ctx->stream, 8 * std::max(ctx->cus, 1)));
+    return MGICP_OK;
+  }
   HIPCK(hipMemcpyAsync(ctx->h_small, cnt, sizeof(unsigned int), hipMemcpyDeviceToHost, ctx->stream));
   int rc = sync(ctx);
   if (rc) return rc;
@@ -1489,6 +1502,12 @@ int cov_lazy(mgicp_ctx* ctx) {
   std::memcpy(&need, ctx->h_small, sizeof(need));
   if (knn_stats_on()) std::fprintf(stderr, "[knn-lazy] source covariances to compute for this sweep: %u\n", need);
   if (!need) return MGICP_OK;
+  if (ctx->knn_wave) {
+    ProfScope ps(ctx, kFamCov);
+    HIPCK(launch_knn_wave(ctx->src.view, ctx->prm.k, ctx->prm.gicp_eps, ctx->cov_need.p, nullptr, need, ctx->src.cov3(),
+                          ctx->stream));
+    return MGICP_OK;
+  }
   const bool logged = ctx->knn_logged;
   if (logged) HIPCK(ctx->knn_fb.reserve(need));
   {
@@ -3755,6 +3774,8 @@ int mgicp_debug_option(mgicp_ctx* ctx, const char* name, double value) {
     ctx->lazy_src_cov = on;
     ctx->src.have_cov = false;
     ctx->src_lazy_ready = false;
+  } else if (n == "knn_wave") {                         // k-NN: lazy pass + hand-offs one wave per point (1) or per lane (0)
+    ctx->knn_wave = on;
   } else if (n == "knn_logged") {                       // k-NN: the logged kernel + hand-off (1) or the register-list kernel only (0)
     ctx->knn_logged = on;
     ctx->src.have_cov = ctx->tgt.have_cov = false;

@@ -124,10 +124,15 @@ hipError_t launch_xform_points(const float4* in, size_t n, Xf34 T, float4* out,
 // kernel; run that list with perm = fb, p0 = 0, p1 = count, fb = nullptr.
 // ring_cap >= 0 (logged kernel only): a query whose search passes that ring gives up -- no
 // covariance, not listed in fb, ok[p] stays 0; every other query sets ok[p] = 1 (ok nullable)
+// r06: exact k-NN covariances with one wave per query (the lazy pass, the hand-off), queries list[i] for
+// i < *count (count non-null, device-side) or n; blocks <= 0: one wave per query
+hipError_t launch_knn_wave(const GridView& g, int k, double eps, const uint32_t* list, const unsigned int* count,
+                           size_t n, Cov3 cov, hipStream_t s, int blocks = 0);
 hipError_t launch_knn_cov(const GridView& g, int k, double eps, size_t p0, size_t p1,
                           Cov3 cov, const uint32_t* perm /*nullable: query order*/, uint32_t* fb,
                           unsigned int* fb_count, hipStream_t s, int ring_cap = -1, uint8_t* ok = nullptr,
-                          int chain = 0 /*> 0: the hand-off launch follows on s, that many blocks, device count*/);
+                          int chain = 0 /*> 0: the hand-off launch follows on s, that many blocks, device count*/,
+                          bool wave_handoff = true /*r06: the chained hand-off by knn_wave_kernel*/);
 // nn_pos: per source point (shard-relative) the matched target sorted position, UINT32_MAX when
 // rejected; with `seeded` its previous contents seed the exact 1-NN search.  flags: 1 if accepted.
 hipError_t launch_correspond(const GridView& tgt, const float4* src, size_t p0, size_t p1, Xf34 T,

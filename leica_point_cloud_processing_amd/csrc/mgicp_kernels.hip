@@ -954,6 +954,170 @@ __device__ __forceinline__ void cov_from_sorted(const GridView& g, double eps, c
   cov_finish(m0, m1, m2, a, static_cast<double>(K - nsent), eps, cov, p);
 }
 
+// ---- r06: one WAVE per query (the lazy pass and the hand-off) ----------------------------------
+// The per-lane ring search (KnnVisitor / KthVisitor) walks a query's rings row by row on one lane; a
+// point whose k neighbours lie many rings out -- scan clutter and debris the gate accepts (C4F: 21k of them
+// in the first sweep, their 20-NN 2-3 cm away, 6-8 rings of 3.6 mm cells) -- then chains hundreds of
+// dependent row loads, and the few waves of the lazy pass ran ~5 ms at C4F for that tail.  Here the 64
+// lanes of a wave share ONE query: ring by ring, lane l takes rows l, l + 64, ... of the shell, keeping its
+// own K smallest (d2 bits, original index) keys; a row is skipped when it lies beyond min(the lane's own
+// K-th, the wave's smallest K-th at the ring start) -- each is an upper bound of the true K-th distance,
+// the subset argument, with ring_search's 1e-5 margin and slop.  After ring r - 1 the search stops when
+// k keys of the whole wave lie strictly inside L, the distance to the unvisited cells (ring_search's
+// bound and margins).  A k-round wave merge (64-bit min, the winning lane pops its front) yields the k
+// keys in ascending (d2, index) order; the moments are summed in that order and finished by cov_finish --
+// cov_from_sorted's sums of KnnVisitor's set, bit for bit.
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned int lo = __shfl_xor(static_cast<unsigned int>(v), o, 64);
+    const unsigned int hi = __shfl_xor(static_cast<unsigned int>(v >> 32), o, 64);
+    const unsigned long long w = (static_cast<unsigned long long>(hi) << 32) | lo;
+    v = w < v ? w : v;
+  }
+  return v;
+}
+
+template <int K>
+struct WaveKnnLane {
+  unsigned long long key[K];
+  uint32_t pos[K];
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int i = 0; i < K; ++i) { key[i] = ~0ull; pos[i] = 0u; }
+  }
+  __device__ __forceinline__ float kth2() const {
+    return key[K - 1] == ~0ull ? INFINITY : __uint_as_float(static_cast<uint32_t>(key[K - 1] >> 32));
+  }
+  __device__ __forceinline__ void insert(unsigned long long c, uint32_t cp) {
+#pragma unroll
+    for (int i = K - 1; i > 0; --i) {
+      const bool sh = c < key[i - 1];
+      const bool here = !sh && c < key[i];
+      key[i] = sh ? key[i - 1] : (here ? c : key[i]);
+      pos[i] = sh ? pos[i - 1] : (here ? cp : pos[i]);
+    }
+    if (c < key[0]) { key[0] = c; pos[0] = cp; }
+  }
+  __device__ __forceinline__ void range(const GridView& g, float qx, float qy, float qz, uint32_t a, uint32_t b) {
+    for (uint32_t j0 = a; j0 < b; j0 += 4) {
+      float4 pb[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) pb[u] = g.pts[min(j0 + u, b - 1)];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (j0 + u >= b) continue;
+        const unsigned long long c = mkkey(dist2(qx, qy, qz, pb[u]), pb[u].w);
+        if (c < key[K - 1]) insert(c, j0 + u);
+      }
+    }
+  }
+  // entries with d2 strictly below Ls^2 (the list is ascending)
+  __device__ __forceinline__ int below(float Ls2) const {
+    int n = 0;
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+      n += (key[i] != ~0ull && __uint_as_float(static_cast<uint32_t>(key[i] >> 32)) < Ls2) ? 1 : 0;
+    return n;
+  }
+};
+
+// queries: list[i] (sorted positions of the cloud) for i < *count (device count) or n; one wave each,
+// grid-striding.  k <= K neighbours (K: the instantiation).
+template <int K>
+__global__ __launch_bounds__(256) void knn_wave_kernel(GridView g, double eps, const uint32_t* __restrict__ list,
+                                                       const unsigned int* __restrict__ count, size_t n, int k,
+                                                       Cov3 cov) {
+  const int lane = threadIdx.x & 63;
+  const size_t nq = count ? static_cast<size_t>(*count) : n;
+  const size_t nw = static_cast<size_t>(gridDim.x) * (blockDim.x >> 6);
+  for (size_t wq = static_cast<size_t>(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6); wq < nq; wq += nw) {
+    const size_t p = list ? list[wq] : wq;
+    const float4 q = g.pts[p];
+    const float qx = q.x, qy = q.y, qz = q.z;
+    WaveKnnLane<K> L;
+    L.init();
+    const int cx = qcell(qx, g.ox, g.inv_h), cy = qcell(qy, g.oy, g.inv_h), cz = qcell(qz, g.oz, g.inv_h);
+    int rmin = max(max(dist_out(cx, g.nx), dist_out(cy, g.ny)), dist_out(cz, g.nz));
+    if (rmin == 0 && g.empty_dist)
+      rmin = g.empty_dist[static_cast<size_t>(cx) +
+                          static_cast<size_t>(g.nx) * (static_cast<size_t>(cy) + static_cast<size_t>(g.ny) * cz)];
+    for (int r = rmin; r < (1 << 22); ++r) {
+      if (r > 0) {
+        const float Lb = fminf(fminf(axis_bound(qx, g.ox, g.h, cx, r - 1, g.nx), axis_bound(qy, g.oy, g.h, cy, r - 1, g.ny)),
+                               axis_bound(qz, g.oz, g.h, cz, r - 1, g.nz));
+        if (Lb == INFINITY) break;  // every cell visited
+        const float Ls = Lb * 0.99999f - g.slop;
+        int nb = Ls > 0.f ? L.below(Ls * Ls) : 0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) nb += __shfl_xor(nb, o, 64);
+        if (nb >= k) break;
+      }
+      // the wave's tightest upper bound of the k-th distance at the ring start
+      float wb = L.kth2();
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) wb = fminf(wb, __shfl_xor(wb, o, 64));
+      const int x0 = cx - r, x1 = cx + r, y0 = cy - r, y1 = cy + r, z0 = cz - r, z1 = cz + r;
+      const int xlo = max(x0, 0), xhi = min(x1, g.nx - 1);
+      const int ylo = max(y0, 0), yhi = min(y1, g.ny - 1);
+      const int zlo = max(z0, 0), zhi = min(z1, g.nz - 1);
+      if (xlo > xhi || ylo > yhi || zlo > zhi) continue;
+      const int ny_r = yhi - ylo + 1;
+      const int nrows = (zhi - zlo + 1) * ny_r;
+      for (int t = lane; t < nrows; t += 64) {
+        const int z = zlo + t / ny_r, y = ylo + t % ny_r;
+        const bool zf = (z == z0) || (z == z1);
+        const float gz = cell_gap(qz, g.oz, g.h, z, g.slop);
+        const float gy = cell_gap(qy, g.oy, g.h, y, g.slop);
+        const float gyz = gy * gy + gz * gz;
+        const float w = fminf(L.kth2(), wb) * 1.00001f;
+        if (gyz > w) continue;
+        const uint32_t* row = g.cell_start + (static_cast<size_t>(z) * g.ny + y) * g.nx;
+        if (zf || y == y0 || y == y1) {
+          const float rx = sqrtf(w - gyz) + g.slop;
+          const int xa = max(xlo, qcell(qx - rx, g.ox, g.inv_h));
+          const int xb = min(xhi, qcell(qx + rx, g.ox, g.inv_h));
+          if (xa <= xb) L.range(g, qx, qy, qz, row[xa], row[xb + 1]);
+        } else {
+          if (x0 >= 0) {
+            const float gx = cell_gap(qx, g.ox, g.h, x0, g.slop);
+            if (gx * gx + gyz <= w) L.range(g, qx, qy, qz, row[x0], row[x0 + 1]);
+          }
+          if (x1 < g.nx) {
+            const float gx = cell_gap(qx, g.ox, g.h, x1, g.slop);
+            if (gx * gx + gyz <= fminf(L.kth2(), wb) * 1.00001f) L.range(g, qx, qy, qz, row[x1], row[x1 + 1]);
+          }
+        }
+      }
+    }
+    // k-round merge in ascending key order; the moments in that order (cov_from_sorted's)
+    double m0 = 0.0, m1 = 0.0, m2 = 0.0;
+    double a[3][3] = {{0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}};
+    for (int i = 0; i < k; ++i) {
+      const unsigned long long m = wave_min_u64(L.key[0]);
+      const unsigned long long win = __builtin_amdgcn_ballot_w64(L.key[0] == m);
+      const int wl = win ? static_cast<int>(__builtin_ctzll(win)) : 0;
+      const uint32_t wp = __builtin_amdgcn_readlane(L.pos[0], wl);
+      if (lane == wl) {
+#pragma unroll
+        for (int j = 0; j < K - 1; ++j) { L.key[j] = L.key[j + 1]; L.pos[j] = L.pos[j + 1]; }
+        L.key[K - 1] = ~0ull;
+      }
+      const float4 pt = g.pts[wp];
+      m0 += pt.x;
+      m1 += pt.y;
+      m2 += pt.z;
+      a[0][0] += static_cast<double>(pt.x * pt.x);
+      a[1][0] += static_cast<double>(pt.y * pt.x);
+      a[1][1] += static_cast<double>(pt.y * pt.y);
+      a[2][0] += static_cast<double>(pt.z * pt.x);
+      a[2][1] += static_cast<double>(pt.z * pt.y);
+      a[2][2] += static_cast<double>(pt.z * pt.z);
+    }
+    if (lane == 0) cov_finish(m0, m1, m2, a, static_cast<double>(k), eps, cov, p);
+  }
+}
+
 // Order-independence certificate for a double sum of n <= 32 floats: if every nonzero term is a
 // normal float with |f| in [2^Emin, 2^(Emax+1)) and Emax - Emin <= 24, every term is a multiple of
 // 2^(Emin-23) and every partial sum, in ANY order, is bounded by 32 * 2^(Emax+1) <= 2^(Emin-23+53):
@@ -1819,15 +1983,6 @@ __global__ __launch_bounds__(256) void vl_centre_kernel(GridView tg, VListView v
                     static_cast<double>(__uint_as_float(static_cast<uint32_t>(vis.best >> 32))) < thr_c;
     v.bcentre[i] = ok ? vis.pos : 0xffffffffu;
   }
-}
-
-__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long x) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const unsigned long long y = __shfl_xor(x, o, 64);
-    x = y < x ? y : x;
-  }
-  return x;
 }
 
 // affine dominance over the grown box (closed form of the minimum over its corners): does a (box-centred
@@ -3620,7 +3775,7 @@ static int knn_log_cap(int K) { return std::min(K + 28, 128); }
 template <int K>
 static hipError_t knn_cov_k(const GridView& g, double eps, size_t p0, size_t p1, Cov3 cov,
                             const uint32_t* perm, int k, uint32_t* fb, unsigned int* fb_count, hipStream_t s,
-                            int ring_cap, uint8_t* ok, int chain) {
+                            int ring_cap, uint8_t* ok, int chain, bool wave_handoff) {
   if (fb) {
     const int cap = knn_log_cap(K);
     knn_cov2_kernel<K><<<nblk(p1 - p0, 64), 64, cap * 64 * sizeof(uint32_t), s>>>(g, eps, p0, p1, cov, perm,
@@ -3628,11 +3783,32 @@ static hipError_t knn_cov_k(const GridView& g, double eps, size_t p0, size_t p1,
                                                                                  ok);
     // chain: the hand-off follows at once in stream order, its count read on the device (a grid of
     // `chain` blocks striding over the list)
-    if (chain > 0) knn_cov_kernel<K><<<chain, 256, 0, s>>>(g, eps, 0, 0, cov, fb, K - k, fb_count);
+    if (chain > 0 && wave_handoff) knn_wave_kernel<K><<<chain, 256, 0, s>>>(g, eps, fb, fb_count, 0, k, cov);
+    else if (chain > 0) knn_cov_kernel<K><<<chain, 256, 0, s>>>(g, eps, 0, 0, cov, fb, K - k, fb_count);
   } else {
     knn_cov_kernel<K><<<nblk(p1 - p0), 256, 0, s>>>(g, eps, p0, p1, cov, perm, K - k, nullptr);
   }
   return hipGetLastError();
+}
+
+// r06: the wave-per-query k-NN over a list (device count, or n), k <= K
+template <int K>
+static hipError_t knn_wave_k(const GridView& g, double eps, const uint32_t* list, const unsigned int* count, size_t n,
+                             int k, Cov3 cov, hipStream_t s, int blocks) {
+  if (blocks <= 0) blocks = static_cast<int>(std::min<size_t>((n + 3) / 4, 65535));
+  if (blocks <= 0) return hipSuccess;
+  knn_wave_kernel<K><<<blocks, 256, 0, s>>>(g, eps, list, count, n, k, cov);
+  return hipGetLastError();
+}
+
+hipError_t launch_knn_wave(const GridView& g, int k, double eps, const uint32_t* list, const unsigned int* count,
+                           size_t n, Cov3 cov, hipStream_t s, int blocks) {
+  if (!count && n == 0) return hipSuccess;
+  if (k <= 8) return knn_wave_k<8>(g, eps, list, count, n, k, cov, s, blocks);
+  if (k <= 16) return knn_wave_k<16>(g, eps, list, count, n, k, cov, s, blocks);
+  if (k <= 20) return knn_wave_k<20>(g, eps, list, count, n, k, cov, s, blocks);
+  if (k <= 24) return knn_wave_k<24>(g, eps, list, count, n, k, cov, s, blocks);
+  return knn_wave_k<32>(g, eps, list, count, n, k, cov, s, blocks);
 }
 
 // exact instantiations for PCL's default (20) and its round neighbours; any other k in
@@ -3641,22 +3817,22 @@ static hipError_t knn_cov_k(const GridView& g, double eps, size_t p0, size_t p1,
 // list: perm = fb, p0 = 0, p1 = count) the register-list kernel runs.
 hipError_t launch_knn_cov(const GridView& g, int k, double eps, size_t p0, size_t p1, Cov3 cov,
                           const uint32_t* perm, uint32_t* fb, unsigned int* fb_count, hipStream_t s, int ring_cap,
-                          uint8_t* ok, int chain) {
+                          uint8_t* ok, int chain, bool wave_handoff) {
   if (p1 <= p0) return hipSuccess;
   switch (k) {
-    case 5: return knn_cov_k<5>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain);
-    case 10: return knn_cov_k<10>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain);
-    case 15: return knn_cov_k<15>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain);
-    case 20: return knn_cov_k<20>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain);
-    case 25: return knn_cov_k<25>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain);
-    case 30: return knn_cov_k<30>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain);
+    case 5: return knn_cov_k<5>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain, wave_handoff);
+    case 10: return knn_cov_k<10>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain, wave_handoff);
+    case 15: return knn_cov_k<15>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain, wave_handoff);
+    case 20: return knn_cov_k<20>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain, wave_handoff);
+    case 25: return knn_cov_k<25>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain, wave_handoff);
+    case 30: return knn_cov_k<30>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain, wave_handoff);
     default: break;
   }
   if (k < 1 || k > kMaxK) return hipErrorInvalidValue;
-  if (k <= 8) return knn_cov_k<8>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain);
-  if (k <= 16) return knn_cov_k<16>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain);
-  if (k <= 24) return knn_cov_k<24>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain);
-  return knn_cov_k<32>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain);
+  if (k <= 8) return knn_cov_k<8>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain, wave_handoff);
+  if (k <= 16) return knn_cov_k<16>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain, wave_handoff);
+  if (k <= 24) return knn_cov_k<24>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain, wave_handoff);
+  return knn_cov_k<32>(g, eps, p0, p1, cov, perm, k, fb, fb_count, s, ring_cap, ok, chain, wave_handoff);
 }
 
 

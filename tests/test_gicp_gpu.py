@@ -658,9 +658,10 @@ def test_lazy_source_covariances_match_eager(engine_mod, monkeypatch):
 
     scan, cad, _ = synth.scan_vs_cad(60_000, 60_000, clutter=0.04, debris=600)
     res = {}
-    for lazy in (1, 0):
-        # without set_*'s covariance head start, which would cover every point
-        e = engine_mod(options={"async_cov": 0, "lazy_src_cov": lazy})
+    for lazy in (1, "1p", 0):
+        # without set_*'s covariance head start, which would cover every point; "1p": the lazy pass on the
+        # per-lane kernels (r06 debug option "knn_wave" 0) instead of one wave per point
+        e = engine_mod(options={"async_cov": 0, "lazy_src_cov": int(lazy != 0), "knn_wave": int(lazy != "1p")})
         e.set_source_xyz(scan)
         e.set_target_xyz(cad)
         T = e.align()
@@ -669,13 +670,42 @@ def test_lazy_source_covariances_match_eager(engine_mod, monkeypatch):
         m, tj, M = e.debug_correspondences(T, len(scan))
         res[lazy] = (T, T2, r["iterations"], r["n_evals"], r["n_corr"], m, tj, M)
         e.close()
-    a, b = res[1], res[0]
-    np.testing.assert_array_equal(a[0], b[0])
-    np.testing.assert_array_equal(a[1], b[1])
-    assert a[2:6] == b[2:6]
-    assert a[4] < len(scan)  # the clutter is rejected
-    np.testing.assert_array_equal(a[6], b[6])
-    np.testing.assert_array_equal(a[7], b[7])
+    for a in (res[1], res["1p"]):
+        b = res[0]
+        np.testing.assert_array_equal(a[0], b[0])
+        np.testing.assert_array_equal(a[1], b[1])
+        assert a[2:6] == b[2:6]
+        assert a[4] < len(scan)  # the clutter is rejected
+        np.testing.assert_array_equal(a[6], b[6])
+        np.testing.assert_array_equal(a[7], b[7])
+
+
+def test_wave_knn_matches_register_list(engine_mod, part_small):
+    """r06 knn_wave_kernel (one wave per query: the lazy pass and the hand-off) against the per-lane
+    register-list kernel (debug option "knn_logged" 0, every point): covariances bit for bit on clouds that
+    stress it -- isolated clutter (many rings), a lattice (ties at the k-th distance: the logged kernel hands
+    those points to the wave kernel), duplicates, a plane -- and several k (the rounded-up instantiations
+    included).  The lazy pass (wave kernel) is pinned by test_lazy_source_covariances_match_eager."""
+    from leica_point_cloud_processing_amd import synth
+
+    scan, cad, _ = synth.scan_vs_cad(80_000, 80_000, clutter=0.1, debris=2000)
+    g = np.arange(0.0, 1.0, 0.05, dtype=np.float32)
+    X, Y, Z = np.meshgrid(g, g, g[:6], indexing="ij")
+    lattice = np.stack([X.ravel(), Y.ravel(), Z.ravel()], 1).astype(np.float32)
+    dup = np.concatenate([part_small[0][:4000], part_small[0][:4000]])
+    plane = part_small[0][:20000].copy()
+    plane[:, 2] = 0.0
+    for name, pts in {"clutter": scan, "lattice": lattice, "dup": dup, "plane": plane}.items():
+        for k in (20, 7, 12):
+            res = {}
+            for form in ("wave", "lane"):
+                opts = {"knn_logged": 1, "knn_wave": 1} if form == "wave" else {"knn_logged": 0, "knn_wave": 0}
+                e = engine_mod(k=k, options=opts)
+                e.set_source_xyz(pts)
+                e.set_target_xyz(pts[: max(k + 1, len(pts) // 2)])
+                res[form] = e.debug_covariances("source", len(pts))
+                e.close()
+            np.testing.assert_array_equal(res["wave"], res["lane"], err_msg=f"{name} k={k}")
 
 
 def test_list_policy_align_iterate_pair_builds_nothing(engine_mod, part_small):
