@@ -327,9 +327,25 @@ def main():
         # a rank whose exchange never delivers fails the align within 30 s (library default 120 s), so the
         # xGMI probe below can fall back to the host segment within the run
         os.environ.setdefault("MGICP_REMOTE_DEADLINE_S", "30")
+    # ms_create and its parts: dlopen of libmgicp.so (the HIP runtime and RCCL libraries
+    # it links), the HIP runtime's device init (first HIP call), then mgicp_create (streams, events, the pinned
+    # pass words and the BAR command block)
+    import ctypes as _ct
+
+    from leica_point_cloud_processing_amd import _lib as _mlib
+
     t_c = time.perf_counter()
+    _lib_h = _mlib.load()
+    t_dl = time.perf_counter()
+    _ndev = _ct.c_int(0)
+    _lib_h.mgicp_device_count(_ct.byref(_ndev))
+    t_rt = time.perf_counter()
     eng = GICPEngine(device=local, max_iter=args.max_iter, fixed_iterations=int(args.fixed))
-    ms_create = 1e3 * (time.perf_counter() - t_c)
+    t_ctx = time.perf_counter()
+    ms_create = 1e3 * (t_ctx - t_c)
+    create_parts = {"ms_dlopen_libmgicp_hip_rccl": round(1e3 * (t_dl - t_c), 3),
+                    "ms_hip_runtime_device_init": round(1e3 * (t_rt - t_dl), 3),
+                    "ms_mgicp_create_context": round(1e3 * (t_ctx - t_rt), 3)}
     transport = "local"
     transport_notes = []
     if world > 1:
@@ -348,10 +364,16 @@ def main():
 
     # warmup: the first align builds grids + covariances (ms-to-converge incl. one-time work)
     first = None
+    warm = []  # aligns 1..W after set_*, the 1-NN cell lists built by aligns 3-4
     for w in range(max(1, args.warmup)):
+        t_w = time.perf_counter()
         eng.align()
+        t_w = time.perf_counter() - t_w
         if w == 0:
             first = dict(eng.last_result)
+        vs = eng.vlist_stats() if world == 1 else {}
+        warm.append({"align": w + 1, "ms_wall": round(1e3 * t_w, 3), "ms_loop": round(eng.last_result["ms_loop"], 3),
+                     "lists": vs.get("lists"), "requested": vs.get("requested")})
     iters_per_align = eng.last_result["iterations"]
     kt_cov = eng.kernel_times()  # profiling is off until now; filled below
     # the target's 1-NN cell lists after the warmup aligns (built by their sweeps; the timed aligns
@@ -837,6 +859,11 @@ def main():
         "vlist": vlist,
         "ms_to_converge_first": round(first["ms_total"], 3),
         "ms_create": round(ms_create, 3),
+        "ms_create_parts": create_parts,
+        "aligns_after_set": warm,
+        # the cell lists' build time: the warmup aligns' wall time beyond the first list-free steady align
+        "vlist_build_ms_estimate": (round(sum(max(0.0, a["ms_wall"] - warm[1]["ms_wall"]) for a in warm[2:]), 3)
+                                    if len(warm) >= 3 else None),
         "ms_to_converge_new_clouds_warm_process": new_clouds,
         "ms_to_converge_first_detail": {k: round(first[k], 3) for k in ("ms_upload", "ms_prep", "ms_loop")},
         "ms_to_converge_cached": round(1e3 * dt / args.steps, 3),
