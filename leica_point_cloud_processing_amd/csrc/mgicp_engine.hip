@@ -3774,6 +3774,8 @@ int mgicp_debug_option(mgicp_ctx* ctx, const char* name, double value) {
     ctx->lazy_src_cov = on;
     ctx->src.have_cov = false;
     ctx->src_lazy_ready = false;
+  } else if (n == "async_ring_cap") {                   // rings the source's lazy-mode head start searches (-1: all)
+    ctx->async_ring_cap = iv;
   } else if (n == "knn_wave") {                         // k-NN: lazy pass + hand-offs one wave per point (1) or per lane (0)
     ctx->knn_wave = on;
   } else if (n == "knn_logged") {                       // k-NN: the logged kernel + hand-off (1) or the register-list kernel only (0)
