@@ -1064,28 +1064,68 @@ __global__ __launch_bounds__(256) void knn_wave_kernel(GridView g, double eps, c
       if (xlo > xhi || ylo > yhi || zlo > zhi) continue;
       const int ny_r = yhi - ylo + 1;
       const int nrows = (zhi - zlo + 1) * ny_r;
-      for (int t = lane; t < nrows; t += 64) {
-        const int z = zlo + t / ny_r, y = ylo + t % ny_r;
-        const bool zf = (z == z0) || (z == z1);
-        const float gz = cell_gap(qz, g.oz, g.h, z, g.slop);
-        const float gy = cell_gap(qy, g.oy, g.h, y, g.slop);
-        const float gyz = gy * gy + gz * gz;
-        const float w = fminf(L.kth2(), wb) * 1.00001f;
-        if (gyz > w) continue;
-        const uint32_t* row = g.cell_start + (static_cast<size_t>(z) * g.ny + y) * g.nx;
-        if (zf || y == y0 || y == y1) {
-          const float rx = sqrtf(w - gyz) + g.slop;
-          const int xa = max(xlo, qcell(qx - rx, g.ox, g.inv_h));
-          const int xb = min(xhi, qcell(qx + rx, g.ox, g.inv_h));
-          if (xa <= xb) L.range(g, qx, qy, qz, row[xa], row[xb + 1]);
-        } else {
-          if (x0 >= 0) {
-            const float gx = cell_gap(qx, g.ox, g.h, x0, g.slop);
-            if (gx * gx + gyz <= w) L.range(g, qx, qy, qz, row[x0], row[x0 + 1]);
+      // rows in batches of 64 (one per lane): each lane forms its row's candidate ranges (pruned against
+      // the wave's bound), then the batch's points are flattened over the wave -- lane l tests points l,
+      // l + 64, ... of the concatenated ranges -- so a row crossing a dense surface does not leave one lane
+      // to scan it while 63 wait (the hand-off's points: dense clusters, duplicates)
+      for (int t0 = 0; t0 < nrows; t0 += 64) {
+        uint32_t a1 = 0, b1 = 0, a2 = 0, b2 = 0;
+        const int t = t0 + lane;
+        float wbb = L.kth2();
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) wbb = fminf(wbb, __shfl_xor(wbb, o, 64));
+        const float w = fminf(wbb, wb) * 1.00001f;
+        if (t < nrows) {
+          const int z = zlo + t / ny_r, y = ylo + t % ny_r;
+          const bool zf = (z == z0) || (z == z1);
+          const float gz = cell_gap(qz, g.oz, g.h, z, g.slop);
+          const float gy = cell_gap(qy, g.oy, g.h, y, g.slop);
+          const float gyz = gy * gy + gz * gz;
+          if (gyz <= w) {
+            const uint32_t* row = g.cell_start + (static_cast<size_t>(z) * g.ny + y) * g.nx;
+            if (zf || y == y0 || y == y1) {
+              const float rx = sqrtf(w - gyz) + g.slop;
+              const int xa = max(xlo, qcell(qx - rx, g.ox, g.inv_h));
+              const int xb = min(xhi, qcell(qx + rx, g.ox, g.inv_h));
+              if (xa <= xb) { a1 = row[xa]; b1 = row[xb + 1]; }
+            } else {
+              if (x0 >= 0) {
+                const float gx = cell_gap(qx, g.ox, g.h, x0, g.slop);
+                if (gx * gx + gyz <= w) { a1 = row[x0]; b1 = row[x0 + 1]; }
+              }
+              if (x1 < g.nx) {
+                const float gx = cell_gap(qx, g.ox, g.h, x1, g.slop);
+                if (gx * gx + gyz <= w) { a2 = row[x1]; b2 = row[x1 + 1]; }
+              }
+            }
           }
-          if (x1 < g.nx) {
-            const float gx = cell_gap(qx, g.ox, g.h, x1, g.slop);
-            if (gx * gx + gyz <= fminf(L.kth2(), wb) * 1.00001f) L.range(g, qx, qy, qz, row[x1], row[x1 + 1]);
+        }
+        const uint32_t n1 = b1 - a1, cnt = n1 + (b2 - a2);
+        uint32_t inc = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t u = __shfl_up(inc, o, 64);
+          if (lane >= o) inc += u;
+        }
+        const uint32_t off = inc - cnt;
+        const uint32_t tot = __builtin_amdgcn_readlane(inc, 63);
+        for (uint32_t f0 = 0; f0 < tot; f0 += 64) {
+          const uint32_t f = f0 + static_cast<uint32_t>(lane);
+          // the owner: the last lane whose range starts at or before f (binary search over the offsets)
+          int lo = 0;
+#pragma unroll
+          for (int step = 32; step > 0; step >>= 1) {
+            const uint32_t om = __shfl(off, lo + step, 64);
+            if (lo + step < 64 && om <= f) lo += step;
+          }
+          const uint32_t o_off = __shfl(off, lo, 64), o_a1 = __shfl(a1, lo, 64), o_n1 = __shfl(n1, lo, 64);
+          const uint32_t o_a2 = __shfl(a2, lo, 64);
+          if (f < tot) {
+            const uint32_t i = f - o_off;
+            const uint32_t j = i < o_n1 ? o_a1 + i : o_a2 + (i - o_n1);
+            const float4 pt = g.pts[j];
+            const unsigned long long c = mkkey(dist2(qx, qy, qz, pt), pt.w);
+            if (c < L.key[K - 1]) L.insert(c, j);
           }
         }
       }
