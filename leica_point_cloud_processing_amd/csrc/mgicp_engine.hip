@@ -1347,6 +1347,8 @@ const uint32_t* query_perm(mgicp_ctx* ctx) {
   return ctx->qperm.p;
 }
 
+constexpr unsigned int kWaveKnnMax = 65536;  // r06: lazy / hand-off lists up to this size run knn_wave_kernel
+
 // covariances of sorted positions [p0, p1) into arrays of `stride` entries (default n)
 int compute_cov(mgicp_ctx* ctx, Cloud& cl, size_t p0, size_t p1, size_t stride = 0) {
   MGICP_TRACE_AT("cov: begin");
@@ -1381,7 +1383,7 @@ int compute_cov(mgicp_ctx* ctx, Cloud& cl, size_t p0, size_t p1, size_t stride =
     if (stats) std::fprintf(stderr, "[knn] %zu points, %u left to the register-list kernel\n", p1 - p0, nfb);
     if (nfb) {
       ProfScope ps(ctx, kFamCov);
-      if (ctx->knn_wave)
+      if (ctx->knn_wave && nfb <= kWaveKnnMax)
         HIPCK(launch_knn_wave(cl.view, ctx->prm.k, ctx->prm.gicp_eps, ctx->knn_fb.p, nullptr, nfb, cl.cov3(), ctx->stream));
       else
         HIPCK(launch_knn_cov(cl.view, ctx->prm.k, ctx->prm.gicp_eps, 0, nfb, cl.cov3(), ctx->knn_fb.p, nullptr,
@@ -1486,15 +1488,6 @@ int cov_lazy(mgicp_ctx* ctx) {
   unsigned int* cnt = reinterpret_cast<unsigned int*>(ctx->u64.p);  // [0] points to compute, [1] hand-offs
   HIPCK(hipMemsetAsync(cnt, 0, 2 * sizeof(unsigned int), ctx->stream));
   HIPCK(launch_cov_need(ctx->flags.p, ctx->cov_ok.p, p0, ns, ctx->cov_need.p, cnt, ctx->stream));
-  if (ctx->knn_wave && !knn_stats_on()) {
-    // r06: one wave per listed point, the count read on the device (no host round trip): the points a sweep
-    // accepts without a covariance are mostly the isolated ones the head start's ring cap left (C4F: debris
-    // and clutter near the part), whose long ring searches the per-lane kernel ran one lane each
-    ProfScope ps(ctx, kFamCov);
-    HIPCK(launch_knn_wave(ctx->src.view, ctx->prm.k, ctx->prm.gicp_eps, ctx->cov_need.p, cnt, ns, ctx->src.cov3(),
-                          ctx->stream, 8 * std::max(ctx->cus, 1)));
-    return MGICP_OK;
-  }
   HIPCK(hipMemcpyAsync(ctx->h_small, cnt, sizeof(unsigned int), hipMemcpyDeviceToHost, ctx->stream));
   int rc = sync(ctx);
   if (rc) return rc;
@@ -1502,7 +1495,12 @@ int cov_lazy(mgicp_ctx* ctx) {
   std::memcpy(&need, ctx->h_small, sizeof(need));
   if (knn_stats_on()) std::fprintf(stderr, "[knn-lazy] source covariances to compute for this sweep: %u\n", need);
   if (!need) return MGICP_OK;
-  if (ctx->knn_wave) {
+  // r06: few points (after the head start: mostly the isolated ones its ring cap left -- C4F's debris and
+  // clutter near the part, 21k in the first sweep) run one wave each, so their long ring searches do not
+  // leave a few per-lane waves as the launch's tail (C4F: 5 ms -> 0.9 ms); a bulk list (the synchronous
+  // path -- N > 1 ranks, profiling -- where the first sweep needs every source covariance) keeps the
+  // per-lane kernels, 64 points per wave
+  if (ctx->knn_wave && need <= kWaveKnnMax) {
     ProfScope ps(ctx, kFamCov);
     HIPCK(launch_knn_wave(ctx->src.view, ctx->prm.k, ctx->prm.gicp_eps, ctx->cov_need.p, nullptr, need, ctx->src.cov3(),
                           ctx->stream));
