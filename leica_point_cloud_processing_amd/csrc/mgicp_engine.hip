@@ -2591,11 +2591,16 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
     delete ctx;
     return MGICP_E_HIP;
   }
-  if (hipHostMalloc(reinterpret_cast<void**>(&ctx->h_small), kSmallBytes,
-                    hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
-      hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->d_small), ctx->h_small, 0) != hipSuccess ||
-      preload_kernels(ctx->h_small, kSmallBytes, ctx->stream) != hipSuccess ||
-      HostUploader::instance().init(ctx->host_threads) != hipSuccess) {
+  MGICP_TRACE_AT("create: stream");
+  bool ok = hipHostMalloc(reinterpret_cast<void**>(&ctx->h_small), kSmallBytes,
+                          hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
+            hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->d_small), ctx->h_small, 0) == hipSuccess;
+  MGICP_TRACE_AT("create: pinned words");
+  ok = ok && preload_kernels(ctx->h_small, kSmallBytes, ctx->stream) == hipSuccess;
+  MGICP_TRACE_AT("create: kernels loaded");
+  ok = ok && HostUploader::instance().init(ctx->host_threads) == hipSuccess;
+  MGICP_TRACE_AT("create: upload staging");
+  if (!ok) {
     if (ctx->h_small) (void)hipHostFree(ctx->h_small);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -2604,6 +2609,7 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
   // the pass path's pinned command / result words and the BAR command block (its memset is
   // synchronous): here, not in the first align, where they waited for the covariance head start
   (void)ensure_host_red(ctx);  // (retried by the first align if it failed)
+  MGICP_TRACE_AT("create: pass words + BAR block");
   // the stream of the covariance head start (created here: a stream's creation costs milliseconds
   // of host time, which set_* would otherwise pay before the launch).  A CU mask on it (leaving CUs to
   // the main stream) was measured -0.5 to -1.4 ms on new clouds (profiles/r04/ncab1) but a CU mask
@@ -2620,6 +2626,7 @@ int mgicp_create(mgicp_ctx** out, const mgicp_params* p) {
       if (ev) (void)hipEventDestroy(ev), ev = nullptr;
     ctx->aux_stream = nullptr;
   }
+  MGICP_TRACE_AT("create: aux stream");
   *out = ctx;
   return MGICP_OK;
 }
