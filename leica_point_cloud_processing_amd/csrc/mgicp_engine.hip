@@ -39,6 +39,7 @@ namespace {
 
 constexpr double kDefaultOccupancy = 10.0;          // mean points per non-empty cell (A/B: profiles/r01/ab_tocc)
 constexpr size_t kSmallBytes = size_t(64) << 10;  // pinned readback scratch per context
+constexpr size_t kSketchOffset = size_t(32) << 10;  // the grid sizing sketch's registers in it (16 KiB)
 constexpr size_t kMaxCells = size_t(1) << 29;       // dense cell table cap (2 GiB of uint32)
 constexpr size_t kMaxBoxCells = size_t(1) << 27;    // per-cell point boxes up to 4 GiB (32 B per cell)
 
@@ -1158,64 +1159,73 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl, bool defer_extras) {
     return nc;
   };
   double h = maxext > 0.f ? static_cast<double>(maxext) / std::cbrt(static_cast<double>(n)) : 1.0;
-  // r06: the cell size is a function of this cloud alone: the loop below always
-  // starts from the 3-D guess above -- never from this slot's previous grid or from the other cloud's
-  // (the loop accepts any size in a 0.6-1.6x occupancy band, so a different start would give a different
-  // grid for the same points; the source's grid sets the order of every objective sum)
+  // r06: the cell size is a function of this cloud alone -- never of this slot's
+  // previous grid or of the other cloud's (the source's grid sets the order of every objective sum).
+  // One sketch pass (cell_sketch_kernel) estimates the non-empty cells at kSketchScales sizes
+  // h0 * 2^(k - 10) around the 3-D guess h0 above; the size is interpolated in log-log between the two
+  // that bracket the target occupancy.  r01-r05 ran trial histograms instead (scattered atomics, a host
+  // round trip each, two per cloud on a surface: ~0.6-0.8 ms per 5M cloud before the sort)
   const bool fresh = true;
   h = std::max(h, 1e-6);
-  int nd[3];
-  double h_prev = 0, occ_prev = 0;
-  HIPCK(ctx->u64.reserve(1));
-  HIPCK(ctx->keys.reserve(n));
-  // the sizing histogram also writes the cell keys: when its cell size is accepted as is, the
-  // final keyed histogram pass is skipped
-  double h_keys = -1.0;
-  for (int it = 0; it < 6 && maxext > 0.f; ++it) {
-    size_t nc = dims(h, nd);
-    int guard = 0;
-    while (nc > kMaxCells && guard++ < 64) {
-      h *= std::cbrt(static_cast<double>(nc) / kMaxCells) * 1.01;
-      nc = dims(h, nd);
+  if (maxext > 0.f && n > 1) {
+    SketchScales sc;
+    double hk[kSketchScales];
+    for (int k = 0; k < kSketchScales; ++k) {
+      hk[k] = h * std::ldexp(1.0, k - 10);
+      sc.inv[k] = static_cast<float>(1.0 / hk[k]);
     }
-    HIPCK(ctx->counts.reserve(nc + 1));
-    MGICP_TRACE_AT("grid: counts reserved");
-    HIPCK(hipMemsetAsync(ctx->counts.p, 0, (nc + 1) * sizeof(uint32_t), s));
-    HIPCK(hipMemsetAsync(ctx->u64.p, 0, sizeof(unsigned long long), s));
-    HIPCK(launch_cell_hist(cl.orig.p, n, mn[0], mn[1], mn[2], static_cast<float>(1.0 / h), nd[0],
-                           nd[1], nd[2], ctx->counts.p, ctx->keys.p, s));
-    HIPCK(launch_count_nonzero(ctx->counts.p, nc, ctx->u64.p, s));
-    HIPCK(hipMemcpyAsync(ctx->h_small, ctx->u64.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    HIPCK(ctx->scratch.reserve(static_cast<size_t>(kSketchBlocks + 32) * kSketchScales * kSketchR));
+    HIPCK(launch_cell_sketch(cl.orig.p, n, mn[0], mn[1], mn[2], sc, ctx->scratch.p, ctx->d_small + kSketchOffset, s));
     rc = sync(ctx);
     if (rc) return rc;
-    unsigned long long nonempty = 0;
-    std::memcpy(&nonempty, ctx->h_small, sizeof(nonempty));
-    MGICP_TRACE_AT("grid: sizing histogram synced");
-    const double occ = static_cast<double>(n) / std::max<unsigned long long>(nonempty, 1);
-    if ((occ > 0.6 * target_occ && occ < 1.6 * target_occ) || nc >= kMaxCells / 2) {
-      h_keys = h;  // counts and keys of this pass are the final ones
-      break;
+    MGICP_TRACE_AT("grid: sizing sketch synced");
+    const unsigned char* regs = ctx->h_small + kSketchOffset;
+    double occ[kSketchScales];
+    for (int k = 0; k < kSketchScales; ++k) {
+      // HyperLogLog estimate of the non-empty cells (linear counting while registers are still zero)
+      double inv_sum = 0.0;
+      int zeros = 0;
+      for (int j = 0; j < kSketchR; ++j) {
+        const int r = regs[k * kSketchR + j];
+        inv_sum += std::ldexp(1.0, -r);
+        zeros += r == 0;
+      }
+      const double R = kSketchR;
+      double e = 0.7213 / (1.0 + 1.079 / R) * R * R / inv_sum;
+      if (e <= 2.5 * R && zeros > 0) e = R * std::log(R / zeros);
+      occ[k] = static_cast<double>(n) / std::max(e, 1.0);
     }
-    if (nonempty <= 1 && occ < target_occ) break;  // everything in one cell already
-    double dim = 2.0;
-    if (h_prev > 0 && occ_prev > 0 && std::fabs(std::log(h / h_prev)) > 1e-3) {
-      dim = std::log(occ / occ_prev) / std::log(h / h_prev);
+    int k1 = -1;
+    for (int k = 0; k < kSketchScales && k1 < 0; ++k)
+      if (occ[k] >= target_occ) k1 = k;
+    if (k1 < 0) {
+      h = hk[kSketchScales - 1];  // fewer points than the target per cell even at the coarsest size
+    } else if (k1 == 0) {
+      // finer than the finest size: extrapolate with the finest pair's growth exponent (1-3)
+      double dim = std::log(std::max(occ[1], occ[0]) / occ[0]) / std::log(2.0);
       dim = std::min(3.0, std::max(1.0, dim));
+      h = hk[0] * std::pow(target_occ / occ[0], 1.0 / dim);
+    } else {
+      const double t = (std::log(target_occ) - std::log(occ[k1 - 1])) / (std::log(occ[k1]) - std::log(occ[k1 - 1]));
+      h = hk[k1 - 1] * std::exp2(std::min(1.0, std::max(0.0, t)));
     }
-    h_prev = h;
-    occ_prev = occ;
-    h = h * std::pow(target_occ / occ, 1.0 / dim);
     h = std::max(h, 1e-6);
+    if (trace_on()) {
+      std::fprintf(stderr, "[mgicp] grid sizing n %zu h0 %.6g -> h %.6g (target %.1f); estimated occupancy", n, hk[10],
+                   h, target_occ);
+      for (int k = 0; k < kSketchScales; ++k) std::fprintf(stderr, " %.3g", occ[k]);
+      std::fprintf(stderr, "\n");
+    }
   }
+  int nd[3];
   size_t nc = dims(h, nd);
   while (nc > kMaxCells) {
     h *= std::cbrt(static_cast<double>(nc) / kMaxCells) * 1.01;
     nc = dims(h, nd);
   }
   const float inv_h = static_cast<float>(1.0 / h);
-  const bool have_keys = h_keys == h;
-  // 3. final histogram with keys (unless the accepted sizing pass made them), scan ->
-  // cell_start, stable radix sort -> permutation
+  // 3. cell keys, stable radix sort -> permutation, cell_start from the sorted keys (cell_end_kernel +
+  // an exclusive max-scan: no histogram of atomics)
   HIPCK(ctx->counts.reserve(nc + 1));
   HIPCK(ctx->keys.reserve(n));
   HIPCK(ctx->keys_sorted.reserve(n));
@@ -1224,21 +1234,26 @@ int build_grid(mgicp_ctx* ctx, Cloud& cl, bool defer_extras) {
   HIPCK(cl.cell_start.reserve(nc + 1));
   HIPCK(cl.pts.reserve(n));
   MGICP_TRACE_AT("grid: final buffers reserved");
-  if (!have_keys) {
-    HIPCK(hipMemsetAsync(ctx->counts.p, 0, (nc + 1) * sizeof(uint32_t), s));
-    HIPCK(launch_cell_hist(cl.orig.p, n, mn[0], mn[1], mn[2], inv_h, nd[0], nd[1], nd[2],
-                           ctx->counts.p, ctx->keys.p, s));
-  }
+  HIPCK(launch_cell_hist(cl.orig.p, n, mn[0], mn[1], mn[2], inv_h, nd[0], nd[1], nd[2], nullptr, ctx->keys.p, s));
   int bits = 1;
   while ((size_t(1) << bits) < nc && bits < 32) ++bits;
-  const size_t sb = std::max(sort_scratch_bytes(n, bits), scan_scratch_bytes(nc + 1));
+  const size_t sb = std::max(sort_scratch_bytes(n, bits), cell_start_scratch_bytes(nc));
   HIPCK(ctx->scratch.reserve(sb));
-  HIPCK(launch_exclusive_scan(ctx->scratch.p, sb, ctx->counts.p, cl.cell_start.p, nc + 1, s));
   HIPCK(launch_iota(ctx->vals.p, n, s));
   HIPCK(launch_sort_pairs(ctx->scratch.p, sb, ctx->keys.p, ctx->keys_sorted.p, ctx->vals.p,
                           cl.perm.p, n, bits, s));
+  HIPCK(launch_cell_starts(ctx->keys_sorted.p, n, nc, ctx->counts.p, cl.cell_start.p, ctx->scratch.p, sb, s));
   HIPCK(launch_gather_sorted(cl.orig.p, cl.perm.p, n, cl.pts.p, s));
   MGICP_TRACE_AT("grid: sort queued");
+  if (trace_on() && n > 0) {  // diagnostics: the grid's real occupancy (host copy of the sorted keys)
+    std::vector<uint32_t> ks(n);
+    HIPCK(hipMemcpyAsync(ks.data(), ctx->keys_sorted.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    if ((rc = sync(ctx))) return rc;
+    size_t runs = 1;
+    for (size_t i = 1; i < n; ++i) runs += ks[i] != ks[i - 1];
+    std::fprintf(stderr, "[mgicp] grid n %zu h %.6g cells %d x %d x %d, non-empty %zu, occupancy %.2f\n", n, h, nd[0],
+                 nd[1], nd[2], runs, static_cast<double>(n) / runs);
+  }
   if (!defer_extras) {
     rc = sync(ctx);
     if (rc) return rc;

@@ -113,8 +113,22 @@ hipError_t launch_bbox(const float4* pts, size_t n, float* partial /*nb*8*/, int
 hipError_t launch_cell_hist(const float4* pts, size_t n, float ox, float oy, float oz,
                             float inv_h, int nx, int ny, int nz, uint32_t* counts,
                             uint32_t* keys /*nullable*/, hipStream_t s);
-hipError_t launch_count_nonzero(const uint32_t* counts, size_t nc, unsigned long long* out,
-                                hipStream_t s);
+// r06: the grid's sizing sketch (cell_sketch_kernel): kSketchR one-byte HyperLogLog registers of the
+// occupied cells at each of kSketchScales cell sizes (1 / inv[k]) over origin (ox, oy, oz), in one pass;
+// `partial` holds (kSketchBlocks + 32) * kSketchScales * kSketchR bytes, the merged registers land in `out`
+constexpr int kSketchScales = 16;
+constexpr int kSketchLog2R = 7;  // 128 registers per size (~9 % error): 8 KiB of LDS, so a sketch block
+                                  // fits beside the source's k-NN (12 KiB per wave, 12 waves per CU)
+constexpr int kSketchR = 1 << kSketchLog2R;
+constexpr int kSketchBlocks = 256;  // of 256 threads
+struct SketchScales { float inv[kSketchScales]; };
+hipError_t launch_cell_sketch(const float4* pts, size_t n, float ox, float oy, float oz, const SketchScales& sc,
+                              uint8_t* partial, uint8_t* out, hipStream_t s);
+// r06: cell_start[0..nc] of a grid from its sorted keys (no histogram): `ends` (nc + 1 words) is
+// zeroed and receives each non-empty cell's end, then an exclusive max-scan gives the starts
+size_t cell_start_scratch_bytes(size_t nc);
+hipError_t launch_cell_starts(const uint32_t* keys_sorted, size_t n, size_t nc, uint32_t* ends, uint32_t* cell_start,
+                              void* scratch, size_t scratch_bytes, hipStream_t s);
 hipError_t launch_gather_sorted(const float4* pts, const uint32_t* perm, size_t n,
                                 float4* out, hipStream_t s);
 hipError_t launch_xform_points(const float4* in, size_t n, Xf34 T, float4* out,

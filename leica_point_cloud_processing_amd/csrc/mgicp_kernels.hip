@@ -578,6 +578,7 @@ __global__ void cell_hist_kernel(const float4* pts, size_t n, float ox, float oy
     lin = cx + static_cast<uint32_t>(nx) * (cy + static_cast<uint32_t>(ny) * cz);
     if (keys) keys[i] = lin;
   }
+  if (!counts) return;  // r06: keys only (the grid's counts come from the sorted keys, cell_end_kernel)
   // r03: scan-ordered clouds (a scanner's line order) put runs of consecutive points into one cell;
   // the run's first lane adds the run length, one atomic per run instead of one per point.  The
   // synthetic bench clouds are in random order (no runs): there the kernel stays bound by the
@@ -594,17 +595,80 @@ __global__ void cell_hist_kernel(const float4* pts, size_t n, float ox, float oy
   }
 }
 
-__global__ __launch_bounds__(256) void count_nonzero_kernel(const uint32_t* c, size_t n,
-                                                            unsigned long long* out) {
-  unsigned long long cnt = 0;
-  for (size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
-       i += static_cast<size_t>(gridDim.x) * blockDim.x)
-    cnt += (c[i] != 0u);
-  for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off);
-  __shared__ unsigned long long sm[4];
-  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = cnt;
+// r06: the grid's sizing sketch.  build_grid aims at ~10 points per non-empty cell; r01-r05 found the cell
+// size by trial histograms (an atomic per point into the counts -- scattered atomics, ~250 us per 5M
+// points -- then a count of the non-empty cells and a host round trip, twice per cloud on surfaces).
+// Here ONE pass estimates the number of non-empty cells at kSketchScales cell sizes at once: per size a
+// HyperLogLog sketch of the occupied cells (kSketchR one-byte registers, LDS atomicMax, a fixed 32-bit
+// hash of the cell coordinates), block sketches written to `partial` and max-merged by
+// sketch_merge_kernel.  The estimate only picks the cell size (every grid is exact); max is
+// order-independent, so the size is a function of the cloud alone.
+__device__ __forceinline__ unsigned int fmix32(unsigned int h) {  // MurmurHash3's finaliser
+  h ^= h >> 16;
+  h *= 0x85ebca6bu;
+  h ^= h >> 13;
+  h *= 0xc2b2ae35u;
+  h ^= h >> 16;
+  return h;
+}
+
+__device__ __forceinline__ unsigned int sketch_cell(float v, float inv) {
+  return static_cast<unsigned int>(static_cast<int>(fminf(fmaxf(floorf(v * inv), -1.0e9f), 1.0e9f)));
+}
+
+__global__ __launch_bounds__(256) void cell_sketch_kernel(const float4* __restrict__ pts, size_t n, float ox, float oy,
+                                                          float oz, SketchScales sc, uint8_t* __restrict__ partial) {
+  constexpr int R = kSketchR, S = kSketchScales;
+  __shared__ unsigned int reg[S * R];
+  for (int t = threadIdx.x; t < S * R; t += blockDim.x) reg[t] = 0u;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(out, sm[0] + sm[1] + sm[2] + sm[3]);
+  for (size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<size_t>(gridDim.x) * blockDim.x) {
+    const float4 p = pts[i];
+    const float fx = p.x - ox, fy = p.y - oy, fz = p.z - oz;
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+      const float inv = sc.inv[k];
+      const unsigned int key = fmix32(sketch_cell(fx, inv) * 0x9e3779b1u ^ sketch_cell(fy, inv) * 0x85ebca77u ^
+                                      sketch_cell(fz, inv) * 0xc2b2ae3du);
+      const unsigned int idx = key >> (32 - kSketchLog2R);
+      const unsigned int rank = static_cast<unsigned int>(__builtin_clz((key << kSketchLog2R) | (1u << (kSketchLog2R - 1)))) + 1u;
+      // most updates change nothing once the registers fill up: a plain read first (same-address reads
+      // broadcast) keeps the LDS atomics -- serialised per address, many lanes share a cell at coarse
+      // sizes -- to the few that raise a register
+      if (rank > reg[k * R + idx]) atomicMax(&reg[k * R + idx], rank);
+    }
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < S * R; t += blockDim.x)
+    partial[static_cast<size_t>(blockIdx.x) * (S * R) + t] = static_cast<uint8_t>(reg[t]);
+}
+
+// max-merge of the block sketches: blockIdx.y takes blocks [y nblocks / ny, (y + 1) nblocks / ny) into
+// partial row nblocks + y (ny rows after the block rows), then the ny rows into `out` (ny == 1)
+__global__ __launch_bounds__(256) void sketch_merge_kernel(uint8_t* __restrict__ partial, int b0, int nblocks,
+                                                           uint8_t* __restrict__ out) {
+  constexpr int SR = kSketchScales * kSketchR;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= SR) return;
+  const int ny = gridDim.y, y = blockIdx.y;
+  const int lo = b0 + y * nblocks / ny, hi = b0 + (y + 1) * nblocks / ny;
+  unsigned int m = 0;
+#pragma unroll 8
+  for (int b = lo; b < hi; ++b) m = max(m, static_cast<unsigned int>(partial[static_cast<size_t>(b) * SR + t]));
+  if (out) out[t] = static_cast<uint8_t>(m);
+  else partial[static_cast<size_t>(b0 + nblocks + y) * SR + t] = static_cast<uint8_t>(m);
+}
+
+// r06: cell_start from the sorted keys: the last point of each non-empty cell stores the cell's end
+// (its position + 1) into `ends` (zeroed), and an exclusive max-scan over the nc + 1 entries then gives
+// every cell's start (the end of the nearest non-empty cell before it) -- the exclusive prefix sum of the
+// per-cell counts, without a histogram of atomics
+__global__ void cell_end_kernel(const uint32_t* __restrict__ keys_sorted, size_t n, uint32_t* __restrict__ ends) {
+  const size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t k = keys_sorted[i];
+  if (i + 1 == n || keys_sorted[i + 1] != k) ends[k] = static_cast<uint32_t>(i + 1);
 }
 
 __global__ void gather_sorted_kernel(const float4* pts, const uint32_t* perm, size_t n,
@@ -3736,11 +3800,31 @@ hipError_t launch_cell_hist(const float4* pts, size_t n, float ox, float oy, flo
   return hipGetLastError();
 }
 
-hipError_t launch_count_nonzero(const uint32_t* counts, size_t nc, unsigned long long* out,
-                                hipStream_t s) {
-  const unsigned nb = static_cast<unsigned>(std::min<size_t>(nblk(nc), 4096));
-  count_nonzero_kernel<<<nb, 256, 0, s>>>(counts, nc, out);
+hipError_t launch_cell_sketch(const float4* pts, size_t n, float ox, float oy, float oz, const SketchScales& sc,
+                              uint8_t* partial, uint8_t* out, hipStream_t s) {
+  constexpr int SR = kSketchScales * kSketchR, kSlices = 32;
+  cell_sketch_kernel<<<kSketchBlocks, 256, 0, s>>>(pts, n, ox, oy, oz, sc, partial);
+  sketch_merge_kernel<<<dim3((SR + 255) / 256, kSlices), 256, 0, s>>>(partial, 0, kSketchBlocks, nullptr);
+  sketch_merge_kernel<<<dim3((SR + 255) / 256, 1), 256, 0, s>>>(partial, kSketchBlocks, kSlices, out);
   return hipGetLastError();
+}
+
+size_t cell_start_scratch_bytes(size_t nc) {
+  size_t bytes = 0;
+  (void)hipcub::DeviceScan::ExclusiveScan(nullptr, bytes, static_cast<const uint32_t*>(nullptr),
+                                          static_cast<uint32_t*>(nullptr), hipcub::Max(), 0u,
+                                          static_cast<int>(nc + 1));
+  return bytes;
+}
+
+hipError_t launch_cell_starts(const uint32_t* keys_sorted, size_t n, size_t nc, uint32_t* ends, uint32_t* cell_start,
+                              void* scratch, size_t scratch_bytes, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(ends, 0, (nc + 1) * sizeof(uint32_t), s);
+  if (e != hipSuccess) return e;
+  if (n) cell_end_kernel<<<nblk(n), 256, 0, s>>>(keys_sorted, n, ends);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  return hipcub::DeviceScan::ExclusiveScan(scratch, scratch_bytes, static_cast<const uint32_t*>(ends), cell_start,
+                                           hipcub::Max(), 0u, static_cast<int>(nc + 1), s);
 }
 
 hipError_t launch_gather_sorted(const float4* pts, const uint32_t* perm, size_t n, float4* out,
@@ -4342,7 +4426,9 @@ hipError_t preload_kernels(void* pinned, size_t pinned_bytes, hipStream_t s) {
       reinterpret_cast<const void*>(&pack_points_kernel),
       reinterpret_cast<const void*>(&bbox_kernel),
       reinterpret_cast<const void*>(&cell_hist_kernel),
-      reinterpret_cast<const void*>(&count_nonzero_kernel),
+      reinterpret_cast<const void*>(&cell_sketch_kernel),
+      reinterpret_cast<const void*>(&sketch_merge_kernel),
+      reinterpret_cast<const void*>(&cell_end_kernel),
       reinterpret_cast<const void*>(&gather_sorted_kernel),
       reinterpret_cast<const void*>(&xform_points_kernel),
       reinterpret_cast<const void*>(&empty_init_kernel),

@@ -312,6 +312,46 @@ def test_grid_lattice_ties(engine_mod):
     np.testing.assert_array_equal(tj_ref, tj_gpu)
 
 
+def _sizing_shapes():
+    rng = np.random.default_rng(11)
+    line = np.zeros((30000, 3), np.float32)
+    line[:, 0] = rng.uniform(0.0, 3.0, 30000)
+    line[:, 1:] = rng.normal(0.0, 1e-4, (30000, 2))
+    plane = np.column_stack([rng.uniform(0, 1, 40000), rng.uniform(0, 0.5, 40000), rng.normal(0, 2e-4, 40000)])
+    vol = rng.uniform(-0.2, 0.2, (40000, 3))
+    # a dense clump with outliers: the bbox is ~25x the clump, most of the grid empty (outliers metres away
+    # would push the dense cell table past its 2^29-cell cap -- DESIGN "Limits")
+    clump = np.vstack([rng.normal(0.0, 0.01, (30000, 3)), rng.uniform(-0.5, 0.5, (40, 3))])
+    tiny = rng.uniform(0, 0.05, (21, 3))
+    return {"line": line, "plane": plane, "volume": vol, "clump": clump, "tiny": tiny}
+
+
+@pytest.mark.parametrize("shape", ["line", "plane", "volume", "clump", "tiny"])
+def test_grid_sizing_any_shape(engine_mod, shape):
+    """r06: the grid's cell size comes from a HyperLogLog sketch of the occupied cells at 16 sizes
+    (cell_sketch_kernel); whatever size it picks, the searches stay exact -- covariances and
+    correspondences of 1-D, 2-D, 3-D, clumped-with-outliers and minimal clouds equal the oracle's."""
+    from oracle import ref
+
+    pts = _sizing_shapes()[shape].astype(np.float32)
+    e = engine_mod()
+    e.set_source_xyz(pts)
+    e.set_target_xyz(pts)
+    for which in ("source", "target"):
+        c_gpu = e.debug_covariances(which, len(pts))
+        c_ref = ref.covariances(pts)
+        assert np.abs(c_gpu - c_ref).max() <= 1e-12 * max(1.0, np.abs(c_ref).max()), which
+    o = ref.RefGICP()
+    o.set_source(pts)
+    o.set_target(pts)
+    T = np.eye(4, dtype=np.float32)
+    T[:3, 3] = [0.004, -0.003, 0.002]
+    mr, tj_ref, _, _ = o.correspondences(T)
+    mg, tj_gpu, _ = e.debug_correspondences(T, len(pts))
+    assert mr == mg
+    np.testing.assert_array_equal(tj_ref, tj_gpu)
+
+
 @pytest.mark.gpu
 def test_seeded_correspondences_exact(engine_mod, part_small):
     """Outer iterations >= 2 seed the 1-NN search with the previous match.  Sequences of seeded
