@@ -120,7 +120,7 @@ constexpr int kSketchScales = 16;
 constexpr int kSketchLog2R = 7;  // 128 registers per size (~9 % error): 8 KiB of LDS, so a sketch block
                                   // fits beside the source's k-NN (12 KiB per wave, 12 waves per CU)
 constexpr int kSketchR = 1 << kSketchLog2R;
-constexpr int kSketchBlocks = 256;  // of 256 threads
+constexpr int kSketchBlocks = 1024;  // of 256 threads (4 per CU: the per-scale LDS read-check is latency-bound)
 struct SketchScales { float inv[kSketchScales]; };
 hipError_t launch_cell_sketch(const float4* pts, size_t n, float ox, float oy, float oz, const SketchScales& sc,
                               uint8_t* partial, uint8_t* out, hipStream_t s);

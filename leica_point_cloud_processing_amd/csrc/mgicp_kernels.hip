@@ -708,9 +708,17 @@ __global__ void empty_init_kernel(const uint32_t* __restrict__ cs, size_t nc, ui
     const float cx = ox + (static_cast<float>(x) + 0.5f) * h, cy = oy + (static_cast<float>(y) + 0.5f) * h,
                 cz = oz + (static_cast<float>(z) + 0.5f) * h;
     float bd = INFINITY;
-    for (uint32_t j = a; j < b; ++j) {
-      const float d = dist2(cx, cy, cz, pts[j]);
-      if (d < bd) { bd = d; best = j; }
+    // r06: 4 loads in flight per round (a wave's few non-empty cells otherwise walk their points one
+    // dependent load at a time); the clamped duplicates of a short tail are skipped
+    for (uint32_t j0 = a; j0 < b; j0 += 4) {
+      float4 p[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) p[u] = pts[min(j0 + u, b - 1)];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float d = dist2(cx, cy, cz, p[u]);
+        if (j0 + u < b && d < bd) { bd = d; best = j0 + u; }
+      }
     }
   }
   seed[c] = best;
@@ -720,40 +728,54 @@ __global__ void empty_init_kernel(const uint32_t* __restrict__ cs, size_t nc, ui
 // element stride `stride`: out(c) = min_{|d| <= kEmptyCap} max(|d|, in(c + d*stride)), capped at
 // kEmptyCap + 1.  With seeds, the seed of the winning cell travels along (first winner in |d|, minus
 // side first), so the final seed lies in a Chebyshev-nearest non-empty cell.  r04: all 2 kEmptyCap
-// neighbours are loaded up front (clamped addresses, out-of-line slots read as empty) and the
-// candidates are then taken in the original order from registers -- the loop of r01 issued its loads
-// one |d| at a time behind the early exit (~275 us per pass at C4's 19.5M target cells)
+// neighbours are loaded up front (out-of-line slots read as empty) and the candidates are then taken
+// in the original order from registers.  r06: a thread takes 4 consecutive cells of one line, so the
+// 2 kEmptyCap + 4 loaded bytes serve all four (r04: 2 kEmptyCap + 1 byte loads per cell, ~170 us
+// per pass at C4's 14-20M target cells); consecutive threads take neighbouring lines (y / z passes)
+// or neighbouring groups of a row (x pass), so every load instruction stays coalesced.
+constexpr int kEmptyGroup = 4;
 __global__ __launch_bounds__(256) void empty_pass_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
-                                                         size_t nc, int n, size_t stride,
+                                                         size_t nlines, int n, size_t stride,
                                                          const uint32_t* __restrict__ sin,
                                                          uint32_t* __restrict__ sout) {
-  constexpr int cap = kEmptyCap;
-  const size_t c = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (c >= nc) return;
-  const int x = static_cast<int>((c / stride) % static_cast<size_t>(n));
-  int vm[cap], vp[cap];
+  constexpr int cap = kEmptyCap, G = kEmptyGroup, W = 2 * cap + G;
+  const size_t ng = static_cast<size_t>((n + G - 1) / G);
+  const size_t t = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= nlines * ng) return;
+  size_t L, g;
+  if (stride == 1) { L = t / ng; g = t % ng; }
+  else { L = t % nlines; g = t / nlines; }
+  // line L's first cell: lines are indexed by the cell's coordinates off this axis
+  const size_t base = (L % stride) + (L / stride) * stride * static_cast<size_t>(n);
+  const int i0 = static_cast<int>(g) * G;
+  int win[W];  // in() of cells i0 - cap .. i0 + G - 1 + cap of the line (255 outside it)
 #pragma unroll
-  for (int d = 1; d <= cap; ++d) {
-    const int am = min(d, x), ap = min(d, n - 1 - x);  // clamped: an in-line address
-    const int lm = in[c - static_cast<size_t>(am) * stride], lp = in[c + static_cast<size_t>(ap) * stride];
-    vm[d - 1] = am == d ? lm : 255;
-    vp[d - 1] = ap == d ? lp : 255;
+  for (int w = 0; w < W; ++w) {
+    const int i = i0 - cap + w;
+    const int ic = min(max(i, 0), n - 1);  // clamped: an in-line address
+    const int v = in[base + static_cast<size_t>(ic) * stride];
+    win[w] = (i == ic) ? v : 255;
   }
-  int best = min(static_cast<int>(in[c]), cap + 1);
-  int dbest = 0;  // signed offset of the winner
 #pragma unroll
-  for (int d = 1; d <= cap; ++d) {
-    if (d < best) {
-      const int v = max(d, vm[d - 1]);
-      if (v < best) { best = v; dbest = -d; }
-      const int w = max(d, vp[d - 1]);
-      if (w < best) { best = w; dbest = d; }
+  for (int u = 0; u < G; ++u) {
+    if (i0 + u >= n) break;
+    const size_t c = base + static_cast<size_t>(i0 + u) * stride;
+    int best = min(win[cap + u], cap + 1);
+    int dbest = 0;  // signed offset of the winner
+#pragma unroll
+    for (int d = 1; d <= cap; ++d) {
+      if (d < best) {
+        const int v = max(d, win[cap + u - d]);
+        if (v < best) { best = v; dbest = -d; }
+        const int w = max(d, win[cap + u + d]);
+        if (w < best) { best = w; dbest = d; }
+      }
     }
-  }
-  out[c] = static_cast<uint8_t>(min(best, cap + 1));
-  if (sout) {
-    const size_t arg = dbest < 0 ? c - static_cast<size_t>(-dbest) * stride : c + static_cast<size_t>(dbest) * stride;
-    sout[c] = best <= cap ? sin[arg] : 0xffffffffu;
+    out[c] = static_cast<uint8_t>(min(best, cap + 1));
+    if (sout) {
+      const size_t arg = dbest < 0 ? c - static_cast<size_t>(-dbest) * stride : c + static_cast<size_t>(dbest) * stride;
+      sout[c] = best <= cap ? sin[arg] : 0xffffffffu;
+    }
   }
 }
 
@@ -3846,19 +3868,19 @@ hipError_t launch_empty_map(const uint32_t* cell_start, int nx, int ny, int nz, 
   const size_t nc = static_cast<size_t>(nx) * ny * nz;
   if (!nc) return hipSuccess;
   uint32_t* s2 = seed ? seed_scratch : nullptr;
-  empty_init_kernel<<<nblk(nc), 256, 0, s>>>(cell_start, nc, out, seed, g ? g->pts : nullptr, nx, ny,
+  // init -> scratch, then x: scratch -> out, y: out -> scratch, z: scratch -> out (r06: the result lands
+  // in `out` / `seed` without the copies of r01-r05)
+  empty_init_kernel<<<nblk(nc), 256, 0, s>>>(cell_start, nc, scratch, s2, g ? g->pts : nullptr, nx, ny,
                                              g ? g->ox : 0.f, g ? g->oy : 0.f, g ? g->oz : 0.f, g ? g->h : 0.f);
-  empty_pass_kernel<<<nblk(nc), 256, 0, s>>>(out, scratch, nc, nx, 1, seed, s2);
-  empty_pass_kernel<<<nblk(nc), 256, 0, s>>>(scratch, out, nc, ny, static_cast<size_t>(nx), s2, seed);
-  empty_pass_kernel<<<nblk(nc), 256, 0, s>>>(out, scratch, nc, nz, static_cast<size_t>(nx) * ny, seed,
-                                             s2);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  if (seed) {
-    e = hipMemcpyAsync(seed, s2, nc * sizeof(uint32_t), hipMemcpyDeviceToDevice, s);
-    if (e != hipSuccess) return e;
-  }
-  return hipMemcpyAsync(out, scratch, nc, hipMemcpyDeviceToDevice, s);
+  auto pass = [&](const uint8_t* in, uint8_t* o, int n, size_t stride, const uint32_t* si, uint32_t* so) {
+    const size_t nlines = nc / static_cast<size_t>(n);
+    const size_t nt = nlines * static_cast<size_t>((n + kEmptyGroup - 1) / kEmptyGroup);
+    empty_pass_kernel<<<nblk(nt), 256, 0, s>>>(in, o, nlines, n, stride, si, so);
+  };
+  pass(scratch, out, nx, 1, s2, seed);
+  pass(out, scratch, ny, static_cast<size_t>(nx), seed, s2);
+  pass(scratch, out, nz, static_cast<size_t>(nx) * ny, s2, seed);
+  return hipGetLastError();
 }
 
 hipError_t launch_cell_boxes(const float4* pts, const uint32_t* cell_start, size_t nc, float4* boxes,
