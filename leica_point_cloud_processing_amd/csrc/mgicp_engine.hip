@@ -1962,8 +1962,8 @@ int vl_prepare(mgicp_ctx* ctx) {
     // list starts are stored in units of 4 entries in 25 bits: at most 2^27 entries (16 bytes each)
     const size_t cap = std::min<size_t>(size_t(1) << 27, std::max<size_t>(size_t(1) << 22, 32 * t.n));
     HIPCK(ctx->vl_pool.reserve(cap));
-    HIPCK(ctx->vl_ctr.reserve(4));
-    HIPCK(hipMemsetAsync(ctx->vl_ctr.p, 0, 4 * sizeof(unsigned int), ctx->stream));
+    HIPCK(ctx->vl_ctr.reserve(8));  // [4]: the build's second-pass cells (r06)
+    HIPCK(hipMemsetAsync(ctx->vl_ctr.p, 0, 8 * sizeof(unsigned int), ctx->stream));
     v.cell = ctx->vl_cell.p;
     v.pool = ctx->vl_pool.p;
     v.pool_cap = static_cast<uint32_t>(cap);

@@ -190,7 +190,8 @@ struct VListView {
   float4* pool;          // list entries {x, y, z, bits(sorted target position)}
   const float4* tpts;    // the target's sorted points (w = original index: exact-distance ties only)
   uint32_t pool_cap;     // entries (< 2^26)
-  unsigned int* ctr;     // [0] pool head (persistent), [1] cells requested, [2] queries pending (per sweep)
+  unsigned int* ctr;     // [0] pool head (persistent), [1] cells requested, [2] queries pending, [3] deferred
+                         // chunks, [4] cells left to the build's second pass (per sweep)
   uint32_t* build;       // requested cells of this sweep
   uint32_t* bcentre;     // per requested cell: sorted position of the cell centre's 1-NN (or none)
   uint32_t build_cap;

@@ -2125,20 +2125,25 @@ __device__ __forceinline__ bool vl_dominates(const double (&a3)[3], double a2, c
 // corner's nearest candidate), drop every candidate an anchor dominates, then every survivor another
 // survivor dominates (dominance is transitive, so the order of the drops does not matter), append the
 // rest to the pool padded to a multiple of 4 entries with far sentinels.
-constexpr int kVlWaves = 2;  // waves per build block (LDS: kVlCand x 20 bytes per wave)
-__global__ __launch_bounds__(64 * kVlWaves) void vl_build_kernel(GridView tg, VListView v) {
-  __shared__ float4 cand[kVlWaves][kVlCand];
-  __shared__ uint32_t cpos[kVlWaves][kVlCand];
-  __shared__ uint32_t rowa[kVlWaves][64], rowp[kVlWaves][64];
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const unsigned int n = min(v.ctr[1], v.build_cap);
-  const unsigned int nwv = gridDim.x * static_cast<unsigned int>(kVlWaves);
-  for (unsigned int sl = blockIdx.x * kVlWaves + static_cast<unsigned int>(wid); sl < n; sl += nwv) {
-    const uint32_t ci = v.build[sl];
-    const uint32_t tc = v.bcentre[sl];
+// r06: two passes.  The first (vl_build_kernel) keeps at most kVlCandS candidates per wave in LDS (16 B
+// each: the sorted position rides in w) and the anchors in LDS instead of registers, so that more build
+// waves share a SIMD (r05: 174 VGPRs and 20 KB of LDS per wave, 1.5 waves per SIMD, latency-bound); a
+// cell with more candidates stays requested and the second pass (vl_build_large_kernel, kVlCand
+// candidates) builds it.  Both run the same per-cell body: the lists are those of the r05 kernel.
+constexpr int kVlWaves = 2;    // waves per block of the large pass (LDS: kVlCand x 16 bytes per wave)
+constexpr int kVlCandS = 512;  // candidates a first-pass wave keeps (8 KB of LDS: 4 waves per SIMD, as the VGPRs allow)
+constexpr int kVlWavesS = 4;   // waves per first-pass block
+constexpr int kVlGU = 2;       // candidate loads per lane in flight per gather round (r05: 4; registers)
+
+template <int kCand, bool kLast>
+__device__ __forceinline__ void vl_build_cell(const GridView& tg, const VListView& v, uint32_t sl, uint32_t ci, uint32_t tc,
+                                              int lane, float4* __restrict__ cand, uint32_t* __restrict__ rowa,
+                                              uint32_t* __restrict__ rowp, double* __restrict__ anc,
+                                              unsigned int& pk_off, unsigned int& pk_left, unsigned int pk_chunk) {
+  {
     if (tc == 0xffffffffu) {
       if (lane == 0) v.cell[ci] = kVlReject;
-      continue;
+      return;
     }
 #if MGICP_VL_DIAG
     unsigned long long vt0 = __builtin_amdgcn_s_memtime();
@@ -2184,11 +2189,21 @@ __global__ __launch_bounds__(64 * kVlWaves) void vl_build_kernel(GridView tg, VL
           const float zl = tg.oz + static_cast<float>(z) * tg.h, yl = tg.oy + static_cast<float>(y) * tg.h;
           const float gz = fmaxf(fmaxf(lof[2] - (zl + tg.h), zl - hif[2]) - tg.slop, 0.f);
           const float gy = fmaxf(fmaxf(lof[1] - (yl + tg.h), yl - hif[1]) - tg.slop, 0.f);
-          if (gy * gy + gz * gz <= R2f) {
-            const uint32_t row = (static_cast<uint32_t>(z) * static_cast<uint32_t>(tg.ny) + static_cast<uint32_t>(y)) *
-                                 static_cast<uint32_t>(tg.nx);
-            a = tg.cell_start[row + x0];
-            cnt = tg.cell_start[row + x1 + 1] - a;
+          const float gyz = gy * gy + gz * gz;
+          if (gyz <= R2f) {
+            // r06: only the row's chord of the grown ball (the box grown by R is a cube of up to 2 x 40 mm
+            // around an off-surface cell, its rows' full x spans held ~70x the ball's candidates).  A kept
+            // point has gx^2 <= R2f - gyz up to the fp32 rounding of both sums (< 1e-6 R2f); slop covers the
+            // coordinates' own rounding, qcell is monotone: every point of S is in [xa, xb]
+            const float rx = sqrtf(fmaxf(R2f - gyz, 0.f) + 1e-6f * R2f) * 1.0001f + tg.slop;
+            const int xa = max(x0, qcell(lof[0] - rx, tg.ox, tg.inv_h));
+            const int xb = min(x1, qcell(hif[0] + rx, tg.ox, tg.inv_h));
+            if (xa <= xb) {
+              const uint32_t row = (static_cast<uint32_t>(z) * static_cast<uint32_t>(tg.ny) + static_cast<uint32_t>(y)) *
+                                   static_cast<uint32_t>(tg.nx);
+              a = tg.cell_start[row + xa];
+              cnt = tg.cell_start[row + xb + 1] - a;
+            }
           }
         }
         uint32_t inc = cnt;
@@ -2198,29 +2213,29 @@ __global__ __launch_bounds__(64 * kVlWaves) void vl_build_kernel(GridView tg, VL
           if (lane >= off) inc += u;
         }
         const uint32_t tot = __builtin_amdgcn_readlane(inc, 63);
-        rowa[wid][lane] = a;
-        rowp[wid][lane] = inc - cnt;
+        rowa[lane] = a;
+        rowp[lane] = inc - cnt;
         lds_wave_sync();
-        for (uint32_t t0 = 0; t0 < tot && !ovf; t0 += 256) {
-          float4 pt[4];
-          uint32_t pj[4];
+        for (uint32_t t0 = 0; t0 < tot && !ovf; t0 += 64 * kVlGU) {
+          float4 pt[kVlGU];
+          uint32_t pj[kVlGU];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
+          for (int u = 0; u < kVlGU; ++u) {
             const uint32_t tt = t0 + static_cast<uint32_t>(lane + 64 * u);
             uint32_t j = 0;
             if (tt < tot) {
               int lo_r = 0, hi_r = 63;  // the last row whose exclusive prefix is <= tt
               while (lo_r < hi_r) {
                 const int mid = (lo_r + hi_r + 1) >> 1;
-                if (rowp[wid][mid] <= tt) lo_r = mid; else hi_r = mid - 1;
+                if (rowp[mid] <= tt) lo_r = mid; else hi_r = mid - 1;
               }
-              j = rowa[wid][lo_r] + (tt - rowp[wid][lo_r]);
+              j = rowa[lo_r] + (tt - rowp[lo_r]);
             }
             pj[u] = j;
             pt[u] = tg.pts[j];
           }
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
+          for (int u = 0; u < kVlGU; ++u) {
             const uint32_t tt = t0 + static_cast<uint32_t>(lane + 64 * u);
             const float gx = fmaxf(fmaxf(lof[0] - pt[u].x, pt[u].x - hif[0]), 0.f);
             const float gy = fmaxf(fmaxf(lof[1] - pt[u].y, pt[u].y - hif[1]), 0.f);
@@ -2229,20 +2244,25 @@ __global__ __launch_bounds__(64 * kVlWaves) void vl_build_kernel(GridView tg, VL
             const unsigned long long m = __builtin_amdgcn_ballot_w64(keep);
             const int o = static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<unsigned int>(m >> 32),
                                                                     __builtin_amdgcn_mbcnt_lo(static_cast<unsigned int>(m), 0u)));
-            if (keep && nc + o < kVlCand) {
-              cand[wid][nc + o] = pt[u];
-              cpos[wid][nc + o] = pj[u];
-            }
+            if (keep && nc + o < kCand) cand[nc + o] = make_float4(pt[u].x, pt[u].y, pt[u].z, __uint_as_float(pj[u]));
             nc += __builtin_popcountll(m);
           }
-          if (nc > kVlCand) ovf = true;
+          if (nc > kCand) ovf = true;
         }
         lds_wave_sync();  // rowa / rowp are rewritten by the next batch of rows
       }
     }
+    if (ovf && !kLast) {  // stays requested: the large pass builds it (listed at the free end of `build`)
+      if (lane == 0) {
+        const unsigned int r = atomicAdd(&v.ctr[4], 1u);
+        const unsigned int n = min(v.ctr[1], v.build_cap);
+        if (r < v.build_cap - n) v.build[v.build_cap - 1u - r] = sl;
+      }
+      return;
+    }
     if (ovf || nc == 0) {
       if (lane == 0) v.cell[ci] = ovf ? kVlOverflow : kVlReject;
-      continue;
+      return;
     }
     lds_wave_sync();
 #if MGICP_VL_DIAG
@@ -2264,7 +2284,7 @@ __global__ __launch_bounds__(64 * kVlWaves) void vl_build_kernel(GridView tg, VL
     const float cf[3] = {static_cast<float>(ctr[0]), static_cast<float>(ctr[1]), static_cast<float>(ctr[2])};
     const float hf[3] = {static_cast<float>(hx[0]), static_cast<float>(hx[1]), static_cast<float>(hx[2])};
     for (int kq = lane; kq < nc; kq += 64) {
-      const float4 tp = cand[wid][kq];
+      const float4 tp = cand[kq];
       const float tx = tp.x - cf[0], ty = tp.y - cf[1], tz = tp.z - cf[2];
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
@@ -2276,22 +2296,32 @@ __global__ __launch_bounds__(64 * kVlWaves) void vl_build_kernel(GridView tg, VL
         ak[c] = key < ak[c] ? key : ak[c];
       }
     }
-    double an[9][3];
-    an[0][0] = pc3[0] - ctr[0];
-    an[0][1] = pc3[1] - ctr[1];
-    an[0][2] = pc3[2] - ctr[2];
+    // the anchors (wave-uniform) go straight to LDS: {x, y, z, |a|^2} relative to the box centre, the
+    // centre's 1-NN first (not 72 VGPRs held through stage 1)
+    {
+      const double a0 = pc3[0] - ctr[0], a1 = pc3[1] - ctr[1], a2 = pc3[2] - ctr[2];
+      if (lane == 0) {
+        anc[0] = a0;
+        anc[1] = a1;
+        anc[2] = a2;
+        anc[3] = a0 * a0 + a1 * a1 + a2 * a2;
+      }
+    }
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
       const unsigned long long m = wave_min_u64(ak[c]);
       const int kq = static_cast<int>(static_cast<unsigned int>(m));
-      const float4 ap = cand[wid][kq];
-      an[1 + c][0] = static_cast<double>(ap.x) - ctr[0];
-      an[1 + c][1] = static_cast<double>(ap.y) - ctr[1];
-      an[1 + c][2] = static_cast<double>(ap.z) - ctr[2];
+      const float4 ap = cand[kq];
+      const double a0 = static_cast<double>(ap.x) - ctr[0], a1 = static_cast<double>(ap.y) - ctr[1],
+                   a2 = static_cast<double>(ap.z) - ctr[2];
+      if (lane == 0) {
+        anc[4 * (1 + c) + 0] = a0;
+        anc[4 * (1 + c) + 1] = a1;
+        anc[4 * (1 + c) + 2] = a2;
+        anc[4 * (1 + c) + 3] = a0 * a0 + a1 * a1 + a2 * a2;
+      }
     }
-    double an2[9];
-#pragma unroll
-    for (int a = 0; a < 9; ++a) an2[a] = an[a][0] * an[a][0] + an[a][1] * an[a][1] + an[a][2] * an[a][2];
+    lds_wave_sync();
     // stage 1: the anchors' dominance, survivors compacted to the front of cand (in order: a batch is
     // read whole before its survivors are written, and they land at or before their own slots)
     int ns = 0;
@@ -2299,10 +2329,8 @@ __global__ __launch_bounds__(64 * kVlWaves) void vl_build_kernel(GridView tg, VL
       const int kq = i0 + lane;
       bool keep = false;
       float4 tp = make_float4(0.f, 0.f, 0.f, 0.f);
-      uint32_t tj = 0;
       if (kq < nc) {
-        tp = cand[wid][kq];
-        tj = cpos[wid][kq];
+        tp = cand[kq];
         const double t3[3] = {static_cast<double>(tp.x) - ctr[0], static_cast<double>(tp.y) - ctr[1],
                               static_cast<double>(tp.z) - ctr[2]};
         double M2 = 0.0, tt = 0.0;
@@ -2315,17 +2343,17 @@ __global__ __launch_bounds__(64 * kVlWaves) void vl_build_kernel(GridView tg, VL
         const double margin = 1e-5 * M2 + 1e-15;
         bool dom = false;
 #pragma unroll
-        for (int a = 0; a < 9; ++a) dom = dom || vl_dominates(an[a], an2[a], t3, tt, margin, hx);
+        for (int a = 0; a < 9; ++a) {
+          const double a3[3] = {anc[4 * a + 0], anc[4 * a + 1], anc[4 * a + 2]};
+          dom = dom || vl_dominates(a3, anc[4 * a + 3], t3, tt, margin, hx);
+        }
         keep = !dom;
       }
       lds_wave_sync();
       const unsigned long long m = __builtin_amdgcn_ballot_w64(keep);
       const int o = static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<unsigned int>(m >> 32),
                                                               __builtin_amdgcn_mbcnt_lo(static_cast<unsigned int>(m), 0u)));
-      if (keep) {
-        cand[wid][ns + o] = tp;
-        cpos[wid][ns + o] = tj;
-      }
+      if (keep) cand[ns + o] = tp;
       ns += __builtin_popcountll(m);
       lds_wave_sync();
     }
@@ -2342,14 +2370,14 @@ __global__ __launch_bounds__(64 * kVlWaves) void vl_build_kernel(GridView tg, VL
     // long list)
     const bool pair = ns <= 256;
     uint32_t keepm = 0;
-    for (int i = 0; i < kVlCand / 64; ++i) {
+    for (int i = 0; i < kCand / 64; ++i) {
       const int kq = lane + 64 * i;
       if (kq >= ns) break;
       if (!pair) {
         keepm |= 1u << i;
         continue;
       }
-      const float4 tp = cand[wid][kq];
+      const float4 tp = cand[kq];
       const double t3[3] = {static_cast<double>(tp.x) - ctr[0], static_cast<double>(tp.y) - ctr[1],
                             static_cast<double>(tp.z) - ctr[2]};
       double M2 = 0.0, tt = 0.0;
@@ -2363,7 +2391,7 @@ __global__ __launch_bounds__(64 * kVlWaves) void vl_build_kernel(GridView tg, VL
       bool dom = false;
       for (int j = 0; j < ns && !dom; ++j) {
         if (j == kq) continue;
-        const float4 ap = cand[wid][j];
+        const float4 ap = cand[j];
         const double a3[3] = {static_cast<double>(ap.x) - ctr[0], static_cast<double>(ap.y) - ctr[1],
                               static_cast<double>(ap.z) - ctr[2]};
         const double a2 = a3[0] * a3[0] + a3[1] * a3[1] + a3[2] * a3[2];
@@ -2385,27 +2413,39 @@ __global__ __launch_bounds__(64 * kVlWaves) void vl_build_kernel(GridView tg, VL
 #endif
     const bool lng = cntl >= static_cast<unsigned int>(kVlLong);
     const unsigned int cnt4 = ((cntl + 3u) & ~3u) + (lng ? 4u : 0u);
-    // pool head: no reservation once the head has passed the cap, so the head exceeds the cap by at
-    // most the reservations of the waves in flight (never wraps); the fit test cannot overflow
+    // the list's place in the pool: r06, from the wave's own pool chunk (pk_chunk entries reserved at a
+    // time) -- one returning atomic on the pool head per CELL serialised the whole build on that one L2
+    // line (r05: ~34 ns per cell, 143 ms for C4's 4.19M cells).  Pool head: no reservation once the head
+    // has passed the cap, so the head exceeds the cap by at most the reservations of the waves in flight
+    // (never wraps); the fit test cannot overflow.  Where a list lands changes no result.
     unsigned int off = 0xffffffffu;
-    if (lane == 0 && __hip_atomic_load(&v.ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < v.pool_cap)
-      off = atomicAdd(&v.ctr[0], cnt4);
-    off = __builtin_amdgcn_readfirstlane(off);
-    if (off >= v.pool_cap || cnt4 > v.pool_cap - off) {
-      if (lane == 0) v.cell[ci] = kVlOverflow;
-      continue;
+    if (cnt4 <= pk_left) {
+      off = pk_off;
+      pk_off += cnt4;
+      pk_left -= cnt4;
+    } else {
+      const unsigned int r = max(cnt4, pk_chunk);
+      if (lane == 0 && __hip_atomic_load(&v.ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < v.pool_cap)
+        off = atomicAdd(&v.ctr[0], r);
+      off = __builtin_amdgcn_readfirstlane(off);
+      if (off >= v.pool_cap || r > v.pool_cap - off) {
+        if (lane == 0) v.cell[ci] = kVlOverflow;
+        return;
+      }
+      pk_off = off + cnt4;
+      pk_left = r - cnt4;
     }
     const unsigned int e0 = off + (lng ? 4u : 0u);
     if (lng && lane < 4) v.pool[off + lane] = make_float4(__uint_as_float(cntl), 0.f, 0.f, 0.f);
     unsigned int run = 0;
-    for (int i = 0; i < kVlCand / 64; ++i) {
+    for (int i = 0; i < kCand / 64; ++i) {
       const bool b = (keepm >> i) & 1u;
       const unsigned long long m = __builtin_amdgcn_ballot_w64(b);
       if (b) {
         const unsigned int o = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned int>(m >> 32),
                                                          __builtin_amdgcn_mbcnt_lo(static_cast<unsigned int>(m), 0u));
-        const float4 c4 = cand[wid][lane + 64 * i];
-        v.pool[e0 + run + o] = make_float4(c4.x, c4.y, c4.z, __uint_as_float(cpos[wid][lane + 64 * i]));
+        const float4 c4 = cand[lane + 64 * i];
+        v.pool[e0 + run + o] = c4;
       }
       run += static_cast<unsigned int>(__builtin_popcountll(m));
     }
@@ -2413,7 +2453,70 @@ __global__ __launch_bounds__(64 * kVlWaves) void vl_build_kernel(GridView tg, VL
     if (static_cast<unsigned int>(lane) < npad)  // far sentinels (d2 = inf) up to the multiple of 4
       v.pool[e0 + cntl + lane] = make_float4(3.0e38f, 3.0e38f, 3.0e38f, 0.f);
     if (lane == 0) v.cell[ci] = ((off >> 2) << 6) | (lng ? static_cast<unsigned int>(kVlLong) : cntl);
-    lds_wave_sync();  // cand / cpos are rewritten for the wave's next cell
+    lds_wave_sync();  // cand is rewritten for the wave's next cell
+  }
+}
+
+// a build wave's pool chunk: 512 entries, fewer when the pool is small (the chunks every wave of a launch
+// may leave unfilled stay below 1/16 of the pool); a multiple of 4
+__device__ __forceinline__ unsigned int vl_pool_chunk(const VListView& v, unsigned int nwaves) {
+  const unsigned int c = v.pool_cap / (16u * max(nwaves, 1u));
+  return max(16u, min(512u, c)) & ~3u;
+}
+
+// first pass: one wave per requested cell, at most kVlCandS candidates
+__global__ __launch_bounds__(64 * kVlWavesS) void vl_build_kernel(GridView tg, VListView v) {
+  __shared__ float4 cand[kVlWavesS][kVlCandS];
+  __shared__ uint32_t rowa[kVlWavesS][64], rowp[kVlWavesS][64];
+  __shared__ double anc[kVlWavesS][36];
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const unsigned int n = min(v.ctr[1], v.build_cap);
+  const unsigned int nwv = gridDim.x * static_cast<unsigned int>(kVlWavesS);
+  unsigned int pk_off = 0, pk_left = 0;
+  const unsigned int pk_chunk = vl_pool_chunk(v, nwv);
+  for (unsigned int sl = blockIdx.x * kVlWavesS + static_cast<unsigned int>(wid); sl < n; sl += nwv)
+    vl_build_cell<kVlCandS, false>(tg, v, sl, v.build[sl], v.bcentre[sl], lane, cand[wid], rowa[wid], rowp[wid], anc[wid],
+                                   pk_off, pk_left, pk_chunk);
+}
+
+// second pass: the cells the first left requested (more than kVlCandS candidates); each wave checks 64
+// slots per round (one load of the slots and their states), then builds its requested cells in turn
+__global__ __launch_bounds__(64 * kVlWaves) void vl_build_large_kernel(GridView tg, VListView v) {
+  __shared__ float4 cand[kVlWaves][kVlCand];
+  __shared__ uint32_t rowa[kVlWaves][64], rowp[kVlWaves][64];
+  __shared__ double anc[kVlWaves][36];
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const unsigned int n = min(v.ctr[1], v.build_cap);
+  const unsigned int nwv = gridDim.x * static_cast<unsigned int>(kVlWaves);
+  unsigned int pk_off = 0, pk_left = 0;
+  const unsigned int pk_chunk = vl_pool_chunk(v, nwv);
+  // the first pass listed its cells at the free end of `build` (all of them when they fit): one wave each
+  const unsigned int nr = v.ctr[4];
+  if (nr <= v.build_cap - n) {
+    for (unsigned int i = blockIdx.x * kVlWaves + static_cast<unsigned int>(wid); i < nr; i += nwv) {
+      const unsigned int sl = v.build[v.build_cap - 1u - i];
+      vl_build_cell<kVlCand, true>(tg, v, sl, v.build[sl], v.bcentre[sl], lane, cand[wid], rowa[wid], rowp[wid],
+                                   anc[wid], pk_off, pk_left, pk_chunk);
+    }
+    return;
+  }
+  // (no room for the list: every slot's state checked, 64 per wave and round)
+  for (unsigned int s0 = (blockIdx.x * kVlWaves + static_cast<unsigned int>(wid)) * 64u; s0 < n; s0 += nwv * 64u) {
+    const unsigned int sl = s0 + static_cast<unsigned int>(lane);
+    uint32_t ci = 0;
+    bool todo = false;
+    if (sl < n) {
+      ci = v.build[sl];
+      todo = v.cell[ci] == kVlRequested;
+    }
+    unsigned long long m = __builtin_amdgcn_ballot_w64(todo);
+    while (m) {
+      const int l = static_cast<int>(__builtin_ctzll(m));
+      m &= m - 1;
+      const uint32_t c = __builtin_amdgcn_readlane(ci, l);
+      vl_build_cell<kVlCand, true>(tg, v, s0 + static_cast<unsigned int>(l), c, v.bcentre[s0 + static_cast<unsigned int>(l)], lane, cand[wid], rowa[wid],
+                                   rowp[wid], anc[wid], pk_off, pk_left, pk_chunk);
+    }
   }
 }
 
@@ -2443,19 +2546,30 @@ __global__ __launch_bounds__(256) void vl_fallback_kernel(GridView tg, VListView
 
 // diagnostics: [0] cells listed [1] list entries [2] reject [3] overflow [4] requested [5] not built,
 // [8 + L] cells with list length L (L < 56)
-__global__ void vl_stats_kernel(const uint32_t* __restrict__ cell, size_t n, unsigned long long* out) {
+__global__ __launch_bounds__(256) void vl_stats_kernel(const uint32_t* __restrict__ cell, size_t n,
+                                                       unsigned long long* out) {
+  // r06: per-block LDS counts, one atomic per block and counter (r05: one global atomic per listed cell on
+  // 64 shared addresses, 23 ms per call at C4)
+  __shared__ unsigned int cnt[64];
+  if (threadIdx.x < 64) cnt[threadIdx.x] = 0u;
+  __syncthreads();
+  unsigned int entries = 0;
   for (size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
        i += static_cast<size_t>(gridDim.x) * blockDim.x) {
     const uint32_t c = cell[i];
     if (c == kVlNotBuilt) continue;  // the common case: no atomics
     if (c < kVlTouched) {
-      atomicAdd(&out[0], 1ull);
-      atomicAdd(&out[1], static_cast<unsigned long long>(c & 63u));
-      atomicAdd(&out[8 + min(c & 63u, 55u)], 1ull);
+      atomicAdd(&cnt[0], 1u);
+      entries += c & 63u;
+      atomicAdd(&cnt[8 + min(c & 63u, 55u)], 1u);
     } else {
-      atomicAdd(&out[c == kVlReject ? 2 : c == kVlOverflow ? 3 : c == kVlRequested ? 4 : 5], 1ull);
+      atomicAdd(&cnt[c == kVlReject ? 2 : c == kVlOverflow ? 3 : c == kVlRequested ? 4 : 5], 1u);
     }
   }
+  atomicAdd(&cnt[1], entries);
+  __syncthreads();
+  if (threadIdx.x < 64 && cnt[threadIdx.x] != 0u)
+    atomicAdd(&out[threadIdx.x], static_cast<unsigned long long>(cnt[threadIdx.x]));
 }
 
 #if MGICP_CORR_PHASES
@@ -3986,7 +4100,7 @@ hipError_t launch_vl_sweep(const GridView& tgt, const VListView& vl, const float
                            Xf34 T, double thr, int seeded, uint32_t* nn_pos, uint32_t* flags, int cus,
                            hipStream_t s, const FusedCompact* fc) {
   if (p1 <= p0) return hipSuccess;
-  hipError_t e = hipMemsetAsync(vl.ctr + 1, 0, 3 * sizeof(unsigned int), s);
+  hipError_t e = hipMemsetAsync(vl.ctr + 1, 0, 4 * sizeof(unsigned int), s);
   if (e != hipSuccess) return e;
   if (fc)
     vl_query_compact_kernel<<<chunk_count(p1 - p0), 256, 0, s>>>(vl, src, p0, p1 - p0, T, thr, nn_pos, flags, fc->cov_s,
@@ -3999,7 +4113,8 @@ hipError_t launch_vl_sweep(const GridView& tgt, const VListView& vl, const float
   const double rc = vl.gate * (1.0 + 1e-5) + 1e-9 + hd;
   const unsigned g = static_cast<unsigned>(std::max(cus, 1));
   vl_centre_kernel<<<4 * g, 256, 0, s>>>(tgt, vl, rc * rc * (1.0 + 1e-5));
-  vl_build_kernel<<<8 * g, 64 * kVlWaves, 0, s>>>(tgt, vl);
+  vl_build_kernel<<<8 * g, 64 * kVlWavesS, 0, s>>>(tgt, vl);
+  vl_build_large_kernel<<<4 * g, 64 * kVlWaves, 0, s>>>(tgt, vl);
   vl_fallback_kernel<<<8 * g, 256, 0, s>>>(tgt, vl, src, p0, T, thr, seeded, nn_pos, flags);
   return hipGetLastError();
 }
