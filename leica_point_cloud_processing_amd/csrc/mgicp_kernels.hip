@@ -1903,6 +1903,47 @@ __device__ __forceinline__ void vl_cell_xyz(const VListView& v, uint32_t ci, uin
 __device__ __forceinline__ void mahalanobis(const Rot33d& R, const double (&C1)[3][3],
                                             const double (&C2)[3][3], double (&m6)[6]);
 
+// the minimum (fp32 d2, original-index tie-break) over the built list of state `st` (< kVlTouched):
+// its d2 (inf: none), winner position bp and entry w (bp / w untouched when the list holds no point)
+__device__ __forceinline__ float vl_list_min(const VListView& v, uint32_t st, float qx, float qy, float qz,
+                                             uint32_t& bp, float4& w) {
+  float bd = INFINITY;
+  uint32_t off = (st >> 6) << 2, cnt = st & 63u;
+  if (cnt == static_cast<uint32_t>(kVlLong)) {  // a long list: count in the header entry
+    cnt = __float_as_uint(v.pool[off].x);
+    off += 4;
+  }
+  // lists are padded to a multiple of 4 with far sentinels (d2 = inf): kVlBatch entries per round in
+  // flight (groups of 4 past the list's end are not loaded)
+  const float4* e = v.pool + off;
+  for (uint32_t j = 0; j < cnt; j += kVlBatch) {
+    float4 a[kVlBatch];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) a[u] = e[j + u];
+#pragma unroll
+    for (int u = 4; u < kVlBatch; ++u)
+      a[u] = j + (u & ~3) < cnt ? e[j + u] : make_float4(3.0e38f, 3.0e38f, 3.0e38f, 0.f);
+#pragma unroll
+    for (int u = 0; u < kVlBatch; ++u) {
+      const float d = dist2(qx, qy, qz, a[u]);
+      const uint32_t pu = __float_as_uint(a[u].w);
+      if (d < bd) {
+        bd = d;
+        bp = pu;
+        w = a[u];
+      } else if (d == bd && d < INFINITY && pu != bp) {
+        // an exact-distance tie (measure zero on scans, lattices have them): the lower original
+        // index wins, as the (d2, index) key of every other 1-NN search
+        if (__float_as_uint(v.tpts[pu].w) < __float_as_uint(v.tpts[bp].w)) {
+          bp = pu;
+          w = a[u];
+        }
+      }
+    }
+  }
+  return bd;
+}
+
 // One query of a listed sweep (every lane of the wave calls it: the request / pending lists take one
 // atomic per wave).  Returns 1 accepted (nn / winner coordinates in bp / w), 0 rejected or not live,
 // 2 pending (the cell has no list yet: vl_fallback_kernel answers it); s = the source point.
@@ -1961,42 +2002,7 @@ __device__ __forceinline__ int vl_query_point(const VListView& v, const float4* 
   w = make_float4(0.f, 0.f, 0.f, 0.f);
   if (!live) return 0;
   if (pending) return 2;
-  float bd = INFINITY;
-  if (st < kVlTouched) {
-    uint32_t off = (st >> 6) << 2, cnt = st & 63u;
-    if (cnt == static_cast<uint32_t>(kVlLong)) {  // a long list: count in the header entry
-      cnt = __float_as_uint(v.pool[off].x);
-      off += 4;
-    }
-    // lists are padded to a multiple of 4 with far sentinels (d2 = inf): kVlBatch entries per round in
-    // flight (groups of 4 past the list's end are not loaded)
-    const float4* e = v.pool + off;
-    for (uint32_t j = 0; j < cnt; j += kVlBatch) {
-      float4 a[kVlBatch];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) a[u] = e[j + u];
-#pragma unroll
-      for (int u = 4; u < kVlBatch; ++u)
-        a[u] = j + (u & ~3) < cnt ? e[j + u] : make_float4(3.0e38f, 3.0e38f, 3.0e38f, 0.f);
-#pragma unroll
-      for (int u = 0; u < kVlBatch; ++u) {
-        const float d = dist2(qx, qy, qz, a[u]);
-        const uint32_t pu = __float_as_uint(a[u].w);
-        if (d < bd) {
-          bd = d;
-          bp = pu;
-          w = a[u];
-        } else if (d == bd && d < INFINITY && pu != bp) {
-          // an exact-distance tie (measure zero on scans, lattices have them): the lower original
-          // index wins, as the (d2, index) key of every other 1-NN search
-          if (__float_as_uint(v.tpts[pu].w) < __float_as_uint(v.tpts[bp].w)) {
-            bp = pu;
-            w = a[u];
-          }
-        }
-      }
-    }
-  }
+  const float bd = st < kVlTouched ? vl_list_min(v, st, qx, qy, qz, bp, w) : INFINITY;
   const bool ok = bp != 0xffffffffu && static_cast<double>(bd) < thr;
   if (!ok) bp = 0xffffffffu;
   return ok ? 1 : 0;
@@ -2530,6 +2536,23 @@ __global__ __launch_bounds__(256) void vl_fallback_kernel(GridView tg, VListView
     const float4 s = src[p0 + k];
     float qx, qy, qz;
     xform(T, s.x, s.y, s.z, qx, qy, qz);
+    // r06: a query whose cell this sweep's build just listed (or rejected) reads the list -- the listed
+    // sweep's exact answer -- instead of the per-lane grid search (the build runs before this kernel)
+    const int ix = qcell(qx, v.ox, v.inv_c), iy = qcell(qy, v.oy, v.inv_c), iz = qcell(qz, v.oz, v.inv_c);
+    const bool inside = ix >= 0 && ix < v.nx && iy >= 0 && iy < v.ny && iz >= 0 && iz < v.nz;
+    const uint32_t st = inside ? v.cell[static_cast<uint32_t>(ix) +
+                                        static_cast<uint32_t>(v.nx) * (static_cast<uint32_t>(iy) +
+                                                                       static_cast<uint32_t>(v.ny) * static_cast<uint32_t>(iz))]
+                               : kVlReject;
+    if (st < kVlTouched || st == kVlReject) {
+      uint32_t bp = 0xffffffffu;
+      float4 w;
+      const float bd = st < kVlTouched ? vl_list_min(v, st, qx, qy, qz, bp, w) : INFINITY;
+      const bool ok = bp != 0xffffffffu && static_cast<double>(bd) < thr;
+      nn_pos[k] = ok ? bp : 0xffffffffu;
+      flags[k] = ok ? 1u : 0u;
+      continue;
+    }
     NnVisitor vis;
     vis.init(qx, qy, qz, thr);
     if (!empty_reject(tg, qx, qy, qz, thr)) {  // r05: no point within the gate: rejected without a search
